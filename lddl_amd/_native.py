@@ -1,0 +1,49 @@
+"""ctypes binding of include/lddl_amd.h (the C ABI of lddl_amd/_lib/liblddl_amd.so).
+
+There is no fallback: if the library is missing the import fails loudly. Build it with
+`python -m lddl_amd.build` (or `__graft_entry__.build()`).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, '_lib', 'liblddl_amd.so')
+
+c_i64, c_u64, c_i32, c_u32, c_dbl, c_vp = (ctypes.c_int64, ctypes.c_uint64, ctypes.c_int32,
+                                           ctypes.c_uint32, ctypes.c_double, ctypes.c_void_p)
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+
+# name -> (restype, argtypes); must mirror include/lddl_amd.h exactly
+SIGNATURES = {
+    'lddl_last_error': (ctypes.c_char_p, []),
+    'lddl_version': (ctypes.c_int, []),
+    'lddl_synth_corpus': (c_i64, [c_u64, c_i64, c_i64, c_dbl, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
+                                  c_i64p, c_i64p, ctypes.c_int]),
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError('lddl_amd native library not built: {} is missing (run `python -m '
+                          'lddl_amd.build`). There is no CPU fallback.'.format(LIB_PATH))
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(status):
+    """Raise NativeError with the library's thread-local message on a negative status."""
+    if status < 0:
+        msg = lib.lddl_last_error()
+        raise NativeError((msg or b'unknown error').decode())
+    return status

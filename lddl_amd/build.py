@@ -1,0 +1,87 @@
+"""In-tree build of the native pieces.
+
+* lddl_amd/_lib/liblddl_amd.so : the product — HIP kernels for gfx950 + C-ABI host code
+  (hipcc --offload-arch=gfx950). Cross-compiles without a GPU.
+* oracle/_build/liblddl_oracle.so : the CPU restatement used only by tests / bench's cpu_baseline
+  (plain gcc, no HIP).
+
+Both are incremental (per-source object files, rebuilt when the source or any header is newer).
+"""
+import glob
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, 'lddl_amd', 'csrc')
+LIBDIR = os.path.join(ROOT, 'lddl_amd', '_lib')
+OBJDIR = os.path.join(ROOT, 'build', 'obj')
+LIB = os.path.join(LIBDIR, 'liblddl_amd.so')
+ORACLE_DIR = os.path.join(ROOT, 'oracle')
+ORACLE_LIB = os.path.join(ORACLE_DIR, '_build', 'liblddl_oracle.so')
+
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ARCH = 'gfx950'
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout)
+        raise RuntimeError('build failed: ' + ' '.join(cmd))
+    return r.stdout
+
+
+def build_product(verbose=False, jobs=8):
+    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(OBJDIR, exist_ok=True)
+    headers = glob.glob(os.path.join(ROOT, 'include', '*.h')) + glob.glob(os.path.join(CSRC, '*.h'))
+    srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')) + glob.glob(os.path.join(CSRC, '*.cpp')))
+    flags = ['-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function',
+             '-I' + os.path.join(ROOT, 'include'), '-I' + CSRC]
+    objs, jobs_list = [], []
+    for s in srcs:
+        o = os.path.join(OBJDIR, os.path.basename(s) + '.o')
+        objs.append(o)
+        if _newer(o, [s] + headers):
+            if s.endswith('.hip'):
+                cmd = [HIPCC, '--offload-arch=' + ARCH, '-x', 'hip'] + flags + ['-c', s, '-o', o]
+            else:
+                cmd = [HIPCC, '-x', 'c++'] + flags + ['-D__HIP_PLATFORM_AMD__', '-c', s, '-o', o]
+            jobs_list.append(cmd)
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        for out in ex.map(_run, jobs_list):
+            if verbose and out:
+                print(out)
+    if _newer(LIB, objs):
+        _run([HIPCC, '-shared', '-fPIC', '--offload-arch=' + ARCH, '-o', LIB] + objs +
+             ['-lpthread'])
+    return LIB
+
+
+def build_oracle():
+    os.makedirs(os.path.dirname(ORACLE_LIB), exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(ORACLE_DIR, '*.c')))
+    deps = srcs + glob.glob(os.path.join(ORACLE_DIR, '*.h'))
+    if srcs and _newer(ORACLE_LIB, deps):
+        _run(['gcc', '-O2', '-std=c11', '-fPIC', '-shared', '-Wall', '-o', ORACLE_LIB] + srcs +
+             ['-lm'])
+    return ORACLE_LIB
+
+
+def build_all(verbose=False):
+    lib = build_product(verbose=verbose)
+    orc = build_oracle()
+    return lib, orc
+
+
+if __name__ == '__main__':
+    print(build_all(verbose=True))
