@@ -215,7 +215,8 @@ def make_doc_lines(n_bytes, seed, nonascii):
     # edge documents: literal special tokens, a doc whose sentences all normalise away, a
     # one-sentence doc, tab-separated id, a doc with a >512-piece sentence
     lines.insert(3, 'edge-0 Look at [MASK] here. And [SEP] there [CLS]. Fine.')
-    lines.insert(5, 'edge-1 \u0000\u0001\u0002 ­​.')
+    lines.insert(5, 'edge-1 \u0000\u0001\u0002 \u00ad\u200b')
+    lines.insert(6, 'edge-1b Real sentence. \u0000\u0001 \u00ad. Another real one.')
     lines.insert(7, 'edge-2 Only one sentence here')
     lines.insert(9, 'edge-3\tTab separated id. Second one!')
     lines.insert(11, 'edge-4 ' + ' '.join(['plut'] * 600) + '. Short after.')
