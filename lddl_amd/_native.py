@@ -19,6 +19,12 @@ SIGNATURES = {
     'lddl_version': (ctypes.c_int, []),
     'lddl_synth_corpus': (c_i64, [c_u64, c_i64, c_i64, c_dbl, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                                   c_i64p, c_i64p, ctypes.c_int]),
+    'lddl_ctx_create': (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_vp, c_i64,
+                                       ctypes.POINTER(c_vp)]),
+    'lddl_ctx_destroy': (ctypes.c_int, [c_vp]),
+    'lddl_ctx_info': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
+    'lddl_ctx_render_table': (ctypes.c_int, [c_vp, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp)]),
+    'lddl_tokenize': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp]),
 }
 
 

@@ -1,0 +1,110 @@
+"""Device context: the GPU-resident equivalent of `transformers.BertTokenizerFast(vocab_file)`
+as the reference builds it (lddl/dask/bert/pretrain.py:584-587, lddl/torch/bert.py:343-346).
+
+All device buffers are torch.cuda tensors; kernels run on torch's current stream.
+"""
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from ._native import lib, check
+
+ASSETS = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'assets')
+SPECIALS = ('[PAD]', '[UNK]', '[CLS]', '[SEP]', '[MASK]')
+LEN_HAS_CLS_SEP = 1 << 30
+LEN_MASK = (1 << 30) - 1
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Context:
+    """Tokenizer tables resident in HBM.
+
+    do_lower_case follows BertTokenizerFast's default (True), which the reference keeps even for
+    cased vocabularies.
+    """
+
+    def __init__(self, vocab_file, do_lower_case=True, device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError('lddl_amd needs a ROCm GPU; there is no CPU fallback')
+        self.device = torch.device('cuda', torch.cuda.current_device() if device is None else device)
+        name = 'uncased' if do_lower_case else 'cased'
+        table = np.fromfile(os.path.join(ASSETS, 'bert_norm_{}.bin'.format(name)), np.uint8)
+        with open(vocab_file, 'rb') as f:
+            vocab = f.read()
+        self.tokens = vocab.decode('utf-8').split('\n')
+        if self.tokens and self.tokens[-1] == '':
+            self.tokens.pop()
+        self.vocab = {}
+        for i, t in enumerate(self.tokens):
+            self.vocab[t.rstrip('\r')] = i
+        h = ctypes.c_void_p()
+        check(lib.lddl_ctx_create(self.device.index, table.ctypes.data, len(table), vocab,
+                                  len(vocab), ctypes.byref(h)))
+        self._h = h
+        vs = ctypes.c_int32()
+        sp = (ctypes.c_int32 * 5)()
+        mp = ctypes.c_int32()
+        check(lib.lddl_ctx_info(h, ctypes.byref(vs), sp, ctypes.byref(mp)))
+        self.vocab_size = vs.value
+        self.special_ids = dict(zip(SPECIALS, list(sp)))
+        self.max_piece_bytes = mp.value
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, '_h', None):
+            lib.lddl_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return self.vocab_size
+
+    def convert_tokens_to_ids(self, tokens):
+        unk = self.special_ids['[UNK]']
+        return [self.vocab.get(t, unk) for t in tokens]
+
+    # ------------------------------------------------------------------------------------------
+    def tokenize(self, text, sent_off, max_pieces=512):
+        """WordPiece-tokenize device-resident sentences.
+
+        text: uint8 cuda tensor; sent_off: int64 cuda tensor [n_sent+1].
+        Returns (ids int32[n_bytes], sent_len int32[n_sent]): sentence s's pieces are
+        ids[sent_off[s] : sent_off[s] + (sent_len[s] & LEN_MASK)].
+        """
+        assert text.dtype == torch.uint8 and text.is_cuda and sent_off.dtype == torch.int64
+        n_sent = sent_off.numel() - 1
+        ids = torch.empty(max(text.numel(), 1), dtype=torch.int32, device=self.device)
+        sent_len = torch.empty(max(n_sent, 0), dtype=torch.int32, device=self.device)
+        check(lib.lddl_tokenize(self._h, _stream(), _ptr(text), text.numel(), _ptr(sent_off),
+                                n_sent, max_pieces, _ptr(ids), _ptr(sent_len)))
+        return ids, sent_len
+
+    def tokenize_host(self, text, sent_off, max_pieces=512):
+        """Convenience: numpy in, ragged numpy (ids, offsets) out."""
+        t = torch.from_numpy(np.ascontiguousarray(text, np.uint8)).to(self.device)
+        o = torch.from_numpy(np.ascontiguousarray(sent_off, np.int64)).to(self.device)
+        ids, sl = self.tokenize(t, o, max_pieces)
+        ids, sl = ids.cpu().numpy(), (sl.cpu().numpy() & LEN_MASK).astype(np.int64)
+        so = np.asarray(sent_off, np.int64)
+        out_off = np.zeros(len(sl) + 1, np.int64)
+        out_off[1:] = np.cumsum(sl)
+        flat = np.concatenate([ids[so[i]:so[i] + sl[i]] for i in range(len(sl))]) if len(sl) else \
+            np.zeros(0, np.int32)
+        return flat, out_off

@@ -1,0 +1,82 @@
+// Device-side shared definitions: context tables, vocab hash, wave primitives.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace lddl {
+
+// ---- vocab hash entry (16 B): exact key for pieces <= 12 bytes, prefix + tail check beyond ----
+// meta: bit31 valid | bit30 continuation ("##") | bit29 long (len > 12) | bits 28..21 len |
+//       bits 20..0 id
+struct alignas(16) VEnt {
+  uint64_t k0;
+  uint32_t k1;
+  uint32_t meta;
+};
+
+constexpr uint32_t kMetaValid = 1u << 31, kMetaCont = 1u << 30, kMetaLong = 1u << 29;
+
+__host__ __device__ inline uint32_t meta_len(uint32_t m) { return (m >> 21) & 0xFF; }
+__host__ __device__ inline int32_t meta_id(uint32_t m) { return (int32_t)(m & 0x1FFFFF); }
+
+__host__ __device__ inline uint64_t vhash(uint64_t k0, uint32_t k1, uint32_t len, uint32_t cont) {
+  uint64_t h = k0 * 0x9E3779B97F4A7C15ull;
+  h ^= ((uint64_t)k1 << 17) ^ ((uint64_t)len << 3) ^ (uint64_t)cont;
+  h ^= h >> 29;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 32;
+  return h;
+}
+
+// keep the low `len` bytes of a little-endian packed word (len in 0..8)
+__host__ __device__ inline uint64_t keep_bytes(uint64_t v, int len) {
+  return len >= 8 ? v : (len <= 0 ? 0 : (v & ((1ull << (8 * len)) - 1)));
+}
+
+// ---- normaliser table classes (tools/make_norm_tables.py) ----
+constexpr uint32_t kWord = 0, kDrop = 1, kSpace = 2, kIso = 3;
+constexpr uint32_t kIdent = 1u << 29, kMulti = 1u << 28;
+
+// Special tokens matched on raw text (added tokens, normalized=False), fixed order.
+constexpr int kNumSpecial = 5;  // [PAD] [UNK] [CLS] [SEP] [MASK]
+enum { kPad = 0, kUnk = 1, kCls = 2, kSep = 3, kMask = 4 };
+
+// Kernel-side view of a context (passed by value).
+struct Tables {
+  const uint16_t* l1;
+  const uint32_t* pages;
+  const uint8_t* pool;
+  const VEnt* vhash;
+  const uint8_t* vbytes;  // piece bytes without "##", piece i at vbytes[voff[i]..voff[i+1])
+  const int64_t* voff;
+  uint32_t vmask;
+  int32_t max_piece_bytes;
+  int32_t special_id[kNumSpecial];
+};
+
+// sent_len flag: the kept pieces contain a literal [CLS] or [SEP] (matters for static masking
+// candidates, pretrain.py:189-192)
+constexpr int32_t kLenHasClsSep = 1 << 30;
+constexpr int32_t kLenMask = (1 << 30) - 1;
+
+// ---- wave helpers (wave64) ----
+__device__ inline int lane_id() { return __lane_id(); }
+
+template <typename T>
+__device__ inline T wave_incl_scan(T v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    T o = __shfl_up(v, d, 64);
+    if (lane_id() >= d) v += o;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ inline T wave_sum(T v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+}  // namespace lddl

@@ -188,8 +188,14 @@ orc_tok* orc_tok_create(const uint8_t* table, int64_t table_len, const char* voc
     if (len > 0 && p[len - 1] == '\r') len--;
     uint8_t cont = 0;
     if (len > 2 && p[0] == '#' && p[1] == '#') { cont = 1; p += 2; len -= 2; }
-    if (vlookup(t, cont, p, len) >= 0) continue; /* first occurrence wins */
     uint64_t h = fnv(cont, p, len);
+    int dup = 0; /* a duplicated line maps to its LAST id, like HF's vocab HashMap */
+    for (uint64_t i = h & t->mask; t->slots[i].id >= 0; i = (i + 1) & t->mask) {
+      vent* e = &t->slots[i];
+      if (e->h == h && e->len == len && e->cont == cont &&
+          !memcmp(t->vblob + e->off, p, len)) { e->id = id; dup = 1; break; }
+    }
+    if (dup) continue;
     uint64_t i = h & t->mask;
     while (t->slots[i].id >= 0) i = (i + 1) & t->mask;
     t->slots[i] = (vent){h, id, len, (int32_t)(p - (const uint8_t*)t->vblob), cont};
