@@ -74,6 +74,79 @@ int lddl_tokenize(lddl_ctx* ctx, void* stream, const uint8_t* d_text, int64_t n_
                   const int64_t* d_sent_off, int64_t n_sent, int32_t max_pieces, int32_t* d_ids,
                   int32_t* d_sent_len);
 
+/* ---------------------------------------------------------------------------------------------
+ * NSP pairs + static masking for a batch of partitions (device in, device out).
+ * Replaces `_to_partition_pairs` (lddl/dask/bert/pretrain.py:386-402) =
+ *   for dup in range(duplicate_factor): for doc: create_pairs_from_document(...)  (241-365)
+ *     with _truncate_seq_pair (161-176) and, if masking, create_masked_lm_predictions (182-238)
+ *   random.shuffle(partition_pairs)
+ * after the empty-sentence / empty-document filtering of _get_documents (89-97).
+ * Inputs: the tokenizer output (d_ids, d_sent_len) over d_sent_off[n_sent+1];
+ *   d_doc_sent_off[n_doc+1] sentence offsets of documents (doc_sent_off[0]=0,
+ *   doc_sent_off[n_doc]=n_sent); d_part_doc_off[n_part+1] document offsets of partitions;
+ *   d_part_seed[n_part]: rng=LDDL_RNG_REPLAY reproduces CPython `random` after
+ *   random.seed(part_seed[p]) bit for bit (vocab_words in id order).
+ * lddl_pairs_plan runs the control plane and returns counts[5] = {pairs, tokens (sum of
+ * len(A)+len(B)), masked positions, kept sentences, kept documents}; the caller then allocates
+ * outputs and calls lddl_pairs_emit. Output pair q (partition order, then the partition shuffle):
+ *   tokens[tok_off[q] : tok_off[q] + len_a[q]] = A (masked), then B up to tok_off[q+1];
+ *   num_tokens = len(A)+len(B)+3; is_rn[q]; masked positions (sorted, in [CLS] A [SEP] B [SEP]
+ *   coordinates) pos[pos_off[q]:pos_off[q+1]] with original-token labels lab[...].
+ * ------------------------------------------------------------------------------------------- */
+typedef struct lddl_pairs lddl_pairs;
+enum { LDDL_RNG_REPLAY = 0, LDDL_RNG_NATIVE = 1 };
+typedef struct {
+  int32_t seq;            /* --target-seq-length */
+  int32_t dup;            /* --duplicate-factor */
+  int32_t masking;        /* --masking */
+  int32_t rng;            /* LDDL_RNG_REPLAY | LDDL_RNG_NATIVE */
+  double short_seq_prob;  /* --short-seq-prob */
+  double masked_lm_ratio; /* --masked-lm-ratio */
+  uint64_t native_seed;   /* counter-RNG key for LDDL_RNG_NATIVE */
+} lddl_pair_params;
+int lddl_pairs_plan(lddl_ctx* ctx, void* stream, const lddl_pair_params* params,
+                    const int64_t* d_sent_off, const int32_t* d_ids, const int32_t* d_sent_len,
+                    int64_t n_sent, const int64_t* d_doc_sent_off, int64_t n_doc,
+                    const int64_t* d_part_doc_off, const int64_t* d_part_seed, int64_t n_part,
+                    lddl_pairs** out, int64_t* counts);
+int lddl_pairs_emit(lddl_pairs* plan, void* stream, int32_t* d_tokens, int64_t* d_tok_off,
+                    int32_t* d_len_a, uint8_t* d_is_rn, uint16_t* d_pos, int32_t* d_lab,
+                    int64_t* d_pos_off);
+int lddl_pairs_destroy(lddl_pairs* plan, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Loader collate (lddl/torch/bert.py:69-149 `_to_encoded_inputs`), one batch, device in/out.
+ *   d_bytes: A / B strings of the batch (space-joined tokens, as stored in the parquet shards);
+ *   sample b: A = d_bytes[a_off[b], a_off[b+1]), B = d_bytes[b_off[b], b_off[b+1]);
+ *   d_na/d_nb: token counts; seq_len = roundup(max(na+nb+3), sequence_length_alignment).
+ *   Outputs int64 [batch, seq_len]: input_ids (convert_tokens_to_ids, [UNK] if absent),
+ *   token_type_ids, attention_mask, and either special_tokens_mask (dynamic masking) or labels
+ *   (static: d_lab_bytes/d_lab_off = masked_lm_labels strings, d_pos/d_pos_off = decoded
+ *   masked_lm_positions; unmasked slots = ignore_index). Unused outputs may be NULL.
+ * ------------------------------------------------------------------------------------------- */
+int lddl_collate_encode(lddl_ctx* ctx, void* stream, const uint8_t* d_bytes, const int64_t* d_a_off,
+                        const int64_t* d_b_off, const int32_t* d_na, const int32_t* d_nb,
+                        int32_t batch, int32_t seq_len, int64_t* d_input_ids,
+                        int64_t* d_token_type_ids, int64_t* d_attention_mask,
+                        int64_t* d_special_tokens_mask, const uint8_t* d_lab_bytes,
+                        const int64_t* d_lab_off, const uint16_t* d_pos, const int64_t* d_pos_off,
+                        int64_t* d_labels, int64_t ignore_index);
+
+/* ---------------------------------------------------------------------------------------------
+ * Dynamic masking (lddl/torch/bert.py:152-196 `_mask_tokens`) in place on d_input_ids
+ * [batch, seq_len] int64; writes d_labels. Special slots come from d_special_tokens_mask, or,
+ * if NULL, from the lengths (positions 0, na+1 and >= na+nb+2, as _to_encoded_inputs sets them).
+ * Native mode: Philox4x32-10 keyed by (seed, counter) — call with a fresh counter per batch.
+ * Replay mode (all four d_r_* non-NULL): apply captured torch draws (masked_indices,
+ * indices_replaced, indices_random as uint8, random_words int64) bit for bit.
+ * ------------------------------------------------------------------------------------------- */
+int lddl_mask_dynamic(lddl_ctx* ctx, void* stream, int64_t* d_input_ids, int64_t* d_labels,
+                      const int64_t* d_special_tokens_mask, const int32_t* d_na, const int32_t* d_nb,
+                      int64_t batch, int64_t seq_len, float mlm_probability, int64_t ignore_index,
+                      int64_t vocab_len, uint64_t seed, uint64_t counter,
+                      const uint8_t* d_r_masked, const uint8_t* d_r_replaced,
+                      const uint8_t* d_r_random, const int64_t* d_r_words);
+
 #ifdef __cplusplus
 }
 #endif

@@ -25,7 +25,27 @@ SIGNATURES = {
     'lddl_ctx_info': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
     'lddl_ctx_render_table': (ctypes.c_int, [c_vp, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp)]),
     'lddl_tokenize': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    'lddl_pairs_plan': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                       c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),
+    'lddl_pairs_emit': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'lddl_pairs_destroy': (ctypes.c_int, [c_vp, c_vp]),
+    'lddl_collate_encode': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
+                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                           c_i64]),
+    'lddl_mask_dynamic': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                         ctypes.c_float, c_i64, c_i64, c_u64, c_u64, c_vp, c_vp,
+                                         c_vp, c_vp]),
 }
+
+
+class PairParams(ctypes.Structure):
+    """lddl_pair_params (include/lddl_amd.h)."""
+    _fields_ = [('seq', ctypes.c_int32), ('dup', ctypes.c_int32), ('masking', ctypes.c_int32),
+                ('rng', ctypes.c_int32), ('short_seq_prob', ctypes.c_double),
+                ('masked_lm_ratio', ctypes.c_double), ('native_seed', ctypes.c_uint64)]
+
+
+RNG_REPLAY, RNG_NATIVE = 0, 1
 
 
 class NativeError(RuntimeError):

@@ -1,0 +1,19 @@
+#include "scan.h"
+
+namespace lddl {
+
+__global__ void __launch_bounds__(kScanThreads) scan_sums_kernel(int64_t* sums, int64_t nb) {
+  int64_t carry = 0;
+  for (int64_t b0 = 0; b0 < nb; b0 += kScanThreads) {
+    const int64_t i = b0 + threadIdx.x;
+    const int64_t v = i < nb ? sums[i] : 0;
+    int64_t tot;
+    const int64_t ex = block_excl_scan(v, &tot);
+    if (i < nb) sums[i] = carry + ex;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sums[nb] = carry;
+}
+
+}  // namespace lddl

@@ -1,0 +1,87 @@
+"""NSP pairs + static masking on the GPU — the device-resident replacement of
+`_to_partition_pairs` / `create_pairs_from_document` / `create_masked_lm_predictions`
+(lddl/dask/bert/pretrain.py:386-402, 241-365, 182-238).
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ._native import lib, check, PairParams, RNG_REPLAY, RNG_NATIVE
+from .context import _ptr, _stream
+
+
+@dataclass
+class PairBatch:
+    """Pairs of one batch of partitions, in output order (partition order, then the reference's
+    per-partition shuffle). Pair q: tokens[tok_off[q]:tok_off[q]+len_a[q]] is A (after masking),
+    the rest up to tok_off[q+1] is B. With static masking, pos[pos_off[q]:pos_off[q+1]] are the
+    masked positions in [CLS] A [SEP] B [SEP] coordinates (sorted) and labels the original ids."""
+    tokens: torch.Tensor
+    tok_off: torch.Tensor
+    len_a: torch.Tensor
+    is_random_next: torch.Tensor
+    pos: torch.Tensor = None      # int16 storage of uint16 positions
+    labels: torch.Tensor = None
+    pos_off: torch.Tensor = None
+    n_kept_sentences: int = 0
+    n_kept_documents: int = 0
+
+    @property
+    def n_pairs(self):
+        return self.len_a.numel()
+
+    @property
+    def num_tokens(self):
+        """len(A) + len(B) + 3 per pair (pretrain.py:352)."""
+        return (self.tok_off[1:] - self.tok_off[:-1]) + 3
+
+    def to_host(self):
+        out = dict(tokens=self.tokens.cpu().numpy(), tok_off=self.tok_off.cpu().numpy(),
+                   len_a=self.len_a.cpu().numpy(),
+                   is_random_next=self.is_random_next.cpu().numpy().astype(bool))
+        out['num_tokens'] = np.diff(out['tok_off']) + 3
+        if self.pos is not None:
+            out['pos'] = self.pos.cpu().numpy().view(np.uint16)
+            out['labels'] = self.labels.cpu().numpy()
+            out['pos_off'] = self.pos_off.cpu().numpy()
+        return out
+
+
+def make_pairs(ctx, sent_off, ids, sent_len, doc_sent_off, part_doc_off, part_seed, seq=128,
+               dup=5, masking=False, short_seq_prob=0.1, masked_lm_ratio=0.15, rng='replay',
+               native_seed=12345):
+    """All inputs are cuda tensors (int64 offsets / seeds; tokenizer output from Context.tokenize).
+
+    rng='replay' reproduces CPython `random` after random.seed(part_seed[p]) per partition.
+    """
+    dev = ctx.device
+    prm = PairParams(seq, dup, int(bool(masking)), RNG_REPLAY if rng == 'replay' else RNG_NATIVE,
+                     short_seq_prob, masked_lm_ratio, native_seed)
+    n_sent = sent_off.numel() - 1
+    n_doc = doc_sent_off.numel() - 1
+    n_part = part_doc_off.numel() - 1
+    h = ctypes.c_void_p()
+    counts = np.zeros(5, np.int64)
+    st = _stream()
+    check(lib.lddl_pairs_plan(ctx.handle, st, ctypes.byref(prm), _ptr(sent_off), _ptr(ids),
+                              _ptr(sent_len), n_sent, _ptr(doc_sent_off), n_doc, _ptr(part_doc_off),
+                              _ptr(part_seed), n_part, ctypes.byref(h), counts.ctypes.data))
+    try:
+        n_pairs, n_tok, n_mask = int(counts[0]), int(counts[1]), int(counts[2])
+        tokens = torch.empty(max(n_tok, 1), dtype=torch.int32, device=dev)[:n_tok]
+        tok_off = torch.empty(n_pairs + 1, dtype=torch.int64, device=dev)
+        len_a = torch.empty(n_pairs, dtype=torch.int32, device=dev)
+        is_rn = torch.empty(n_pairs, dtype=torch.uint8, device=dev)
+        pos = labels = pos_off = None
+        if masking:
+            pos = torch.empty(max(n_mask, 1), dtype=torch.int16, device=dev)[:n_mask]
+            labels = torch.empty(max(n_mask, 1), dtype=torch.int32, device=dev)[:n_mask]
+            pos_off = torch.empty(n_pairs + 1, dtype=torch.int64, device=dev)
+        check(lib.lddl_pairs_emit(h, st, _ptr(tokens), _ptr(tok_off), _ptr(len_a), _ptr(is_rn),
+                                  _ptr(pos), _ptr(labels), _ptr(pos_off)))
+    finally:
+        lib.lddl_pairs_destroy(h, st)
+    return PairBatch(tokens, tok_off, len_a, is_rn, pos, labels, pos_off, int(counts[3]),
+                     int(counts[4]))

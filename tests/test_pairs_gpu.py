@@ -1,0 +1,73 @@
+"""GPU pair construction + static masking (replay RNG) vs the reference goldens, starting from
+the raw Punkt sentences: tokenize -> drop empty sentences/docs -> plan -> gather."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, VOCAB_UNCASED
+
+pytestmark = pytest.mark.gpu
+
+PAIR_CASES = ['s128_mask', 's128_nomask', 's512_mask', 's512_nomask_short', 's64_mask_ratio']
+
+
+def load(name):
+    with np.load(os.path.join(GOLDEN, name)) as z:
+        return dict(z)
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    from lddl_amd.context import Context
+    return Context(VOCAB_UNCASED, True)
+
+
+@pytest.fixture(scope='module')
+def docs_dev(ctx):
+    g = load('documents_uncased.npz')
+    text = torch.from_numpy(g['text'].copy()).cuda()
+    sent_off = torch.from_numpy(g['sent_off']).cuda()
+    ids, sent_len = ctx.tokenize(text, sent_off)
+    line_off = g['line_sent_off']
+    # original line index of every kept document (a line whose sentences all normalise away is
+    # dropped by the reference before partitioning)
+    lens = (sent_len.cpu().numpy() & ((1 << 30) - 1))
+    kept_lines = [i for i in range(len(line_off) - 1) if lens[line_off[i]:line_off[i + 1]].sum() > 0]
+    return dict(sent_off=sent_off, ids=ids, sent_len=sent_len,
+                doc_sent_off=torch.from_numpy(line_off).cuda(), kept_lines=kept_lines,
+                n_lines=len(line_off) - 1)
+
+
+def part_doc_off_for(sizes, kept_lines, n_lines):
+    bounds = np.concatenate([[0], np.cumsum(sizes)])
+    return np.asarray([kept_lines[b] if b < len(kept_lines) else n_lines for b in bounds], np.int64)
+
+
+@pytest.mark.parametrize('name', PAIR_CASES)
+def test_pairs_golden_gpu(name, ctx, docs_dev):
+    from lddl_amd.pairs import make_pairs
+    g = load('pairs_{}.npz'.format(name))
+    dup, seq, masking = g['params'].tolist()
+    pdo = part_doc_off_for(g['part_doc_sizes'], docs_dev['kept_lines'], docs_dev['n_lines'])
+    if pdo[-1] < docs_dev['n_lines']:  # docs after the last golden partition are not used
+        pass
+    out = make_pairs(ctx, docs_dev['sent_off'], docs_dev['ids'], docs_dev['sent_len'],
+                     docs_dev['doc_sent_off'], torch.from_numpy(pdo).cuda(),
+                     torch.from_numpy(g['seeds'].astype(np.int64)).cuda(), seq=seq, dup=dup,
+                     masking=bool(masking), short_seq_prob=float(g['short_seq_prob']),
+                     masked_lm_ratio=float(g['ratio'])).to_host()
+    n = len(g['num_tokens'])
+    assert len(out['len_a']) == n
+    np.testing.assert_array_equal(out['is_random_next'], g['is_random_next'])
+    np.testing.assert_array_equal(out['num_tokens'], g['num_tokens'])
+    np.testing.assert_array_equal(np.diff(g['a_off']), out['len_a'])
+    exp_tok = np.concatenate([np.concatenate([g['a'][g['a_off'][q]:g['a_off'][q + 1]],
+                                              g['b'][g['b_off'][q]:g['b_off'][q + 1]]])
+                              for q in range(n)])
+    np.testing.assert_array_equal(out['tokens'], exp_tok)
+    if masking:
+        np.testing.assert_array_equal(out['pos_off'], g['pos_off'])
+        np.testing.assert_array_equal(out['pos'], g['pos'])
+        np.testing.assert_array_equal(out['labels'], g['labels'])
