@@ -1,0 +1,215 @@
+"""Benchmark of the hot path on BASELINE.json's metric config (configs[1], "C2"):
+synthetic English-like corpus, seq 128, static masking, no binning, on MI355X.
+
+One step = one pass of the hot path over one batch of synthetic input already resident in HBM:
+WordPiece tokenization of the batch's (Punkt-segmented) sentences, then NSP pair construction with
+duplicate_factor 5 and static MLM masking (CPython-exact `random` replay per partition), producing
+the device-resident sample table (A/B token ids, num_tokens, is_random_next, masked positions and
+labels). Every step recomputes everything from the text; nothing is cached between steps.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+Multi-GPU: documents are sharded across ranks (each rank owns disjoint documents of the corpus and
+its own partitions); the path has no data-path collective for C2, so `scaling` is "weak".
+value = sum over ranks of output tokens (sum of num_tokens, [CLS]/[SEP] included) / max rank time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+VOCAB = os.path.join(REPO, 'lddl_amd', 'assets', 'vocab_synth_uncased_30522.txt')
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def partition_docs(corp, partition_bytes):
+    """Group consecutive documents into partitions of ~partition_bytes of text (the reference's
+    Dask blocks, readers.py:48-67)."""
+    doc_bytes = corp.sent_off[corp.doc_sent_off]
+    cuts = np.searchsorted(doc_bytes, np.arange(0, doc_bytes[-1], partition_bytes), 'left')
+    cuts = np.unique(np.concatenate([cuts, [corp.n_doc]]))
+    if cuts[0] != 0:
+        cuts = np.concatenate([[0], cuts])
+    return cuts.astype(np.int64)
+
+
+def make_batch(rank, args):
+    from lddl_amd import synth
+    corp = synth.generate(seed=args.seed, n_bytes=args.batch_bytes, doc_begin=rank * 50_000_000,
+                          nonascii_frac=0.01, threads=args.gen_threads)
+    part = partition_docs(corp, args.partition_bytes)
+    # per-partition seeds for random.seed(); the reference leaves the worker RNG unseeded (H1)
+    seeds = (np.arange(len(part) - 1, dtype=np.int64) + rank * 10_000_000) * 7919 + args.seed
+    return corp, part, seeds
+
+
+def cpu_baseline(corp, part, seeds, args):
+    """The oracle (C restatement of the reference algorithm, one core) on a bounded sample of the
+    same workload: the first partitions of the batch, up to ~cpu_sample_bytes of text."""
+    from oracle import oracle as O
+    tok = O.Tokenizer(VOCAB, lowercase=True)
+    cls_id, sep_id, mask_id = (tok.token_id(t) for t in ('[CLS]', '[SEP]', '[MASK]'))
+    doc_bytes = corp.sent_off[corp.doc_sent_off]
+    n_part = max(1, int(np.searchsorted(doc_bytes[part], args.cpu_sample_bytes)))
+    d1 = part[n_part]
+    s1 = corp.doc_sent_off[d1]
+    b1 = corp.sent_off[s1]
+    t0 = time.perf_counter()
+    ids, off = tok.tokenize(corp.text[:b1], corp.sent_off[:s1 + 1])
+    lens = np.diff(off)
+    keep = lens > 0  # drop empty sentences, then empty documents (pretrain.py:89-97)
+    k_off = np.concatenate([[0], np.cumsum(lens[keep])])  # ids is already compact
+    kept_pos = np.concatenate([[0], np.cumsum(keep)])
+    n_out = 0
+    for p in range(n_part):
+        kd = kept_pos[corp.doc_sent_off[part[p]:part[p + 1] + 1]]
+        kd = np.concatenate([kd[:1], kd[1:][np.diff(kd) > 0]])
+        out = O.partition_pairs(kd, k_off, ids, int(seeds[p]), 5, args.seq, True,
+                                tok.vocab_size, cls_id, sep_id, mask_id)
+        n_out += int(out['num_tokens'].sum())
+    dt = time.perf_counter() - t0
+    return {'value': n_out / dt, 'unit': 'output tokens/s', 'cores': 1, 'kind': 'port',
+            'sample': '{} partitions = {:.1f} MB of the same synthetic batch (tokenize + pairs + '
+                      'static masking, oracle/lddl_oracle.c, 1 thread), {:.1f} s'.format(
+                          n_part, b1 / 1e6, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--batch-bytes', type=int, default=1 << 30)
+    ap.add_argument('--partition-bytes', type=int, default=1 << 20)
+    ap.add_argument('--seq', type=int, default=128)
+    ap.add_argument('--seed', type=int, default=1234)
+    ap.add_argument('--gen-threads', type=int, default=16)
+    ap.add_argument('--cpu-sample-bytes', type=int, default=48 << 20)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    from lddl_amd.context import Context
+    from lddl_amd.pairs import make_pairs
+
+    corp, part, seeds = make_batch(rank, args)
+    ctx = Context(VOCAB, do_lower_case=True)
+    dev = ctx.device
+    text = torch.from_numpy(corp.text).to(dev)
+    sent_off = torch.from_numpy(corp.sent_off).to(dev)
+    doc_off = torch.from_numpy(corp.doc_sent_off).to(dev)
+    part_off = torch.from_numpy(part).to(dev)
+    part_seed = torch.from_numpy(seeds).to(dev)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        ids, sent_len = ctx.tokenize(text, sent_off)
+        if ev is not None:
+            ev[1].record()
+        pb = make_pairs(ctx, sent_off, ids, sent_len, doc_off, part_off, part_seed, seq=args.seq,
+                        dup=5, masking=True, short_seq_prob=0.1, masked_lm_ratio=0.15)
+        if ev is not None:
+            ev[2].record()
+        n_tok = int(pb.tokens.numel()) + 3 * pb.n_pairs
+        return n_tok, pb, sent_len
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out_tokens = 0
+    last = None
+    for k in range(args.steps):
+        n, pb, sent_len = step(evs[k])
+        out_tokens += n
+        last = (pb, sent_len)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tok_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    pair_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    pb, sent_len = last
+    pieces = int((sent_len & ((1 << 30) - 1)).sum())
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        n = torch.tensor([out_tokens], dtype=torch.float64, device=dev)
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        out_tokens = int(n.item())
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    # roofline of the dominant kernel (tokenizer): algorithmic bytes per launch =
+    # text bytes read + sentence offsets read (8 B each) + ids written (4 B / piece) + sent_len (4 B)
+    n_bytes, n_sent = corp.text.size, corp.n_sent
+    tok_bytes = n_bytes + 8 * (n_sent + 1) + 4 * pieces + 4 * n_sent
+    achieved = tok_bytes / (tok_ms * 1e-3) / 1e9
+    prof_traffic = None
+    pmc = os.path.join(REPO, 'profiles', 'tokenize_pmc.json')
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                rec = json.load(f)
+            if rec.get('batch_bytes') == args.batch_bytes:
+                prof_traffic = rec.get('hbm_bytes_per_launch')
+        except Exception:
+            prof_traffic = None
+    res = {
+        'metric': 'WordPiece+MLM tokens/sec (1/2/4/8 MI355X) and % of HBM roofline',
+        'value': out_tokens / dt,
+        'unit': 'output tokens/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': dt * 1e3 / args.steps,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'int32',
+        'data': 'synthetic',
+        'config': {
+            'workload': 'C2: synthetic English-like corpus (SURVEY 8d generator, seed {}), '
+                        'seq 128, static masking, duplicate_factor 5, no binning; {} MiB of '
+                        'sentence text per GPU per step, {} KiB partitions'.format(
+                            args.seed, args.batch_bytes >> 20, args.partition_bytes >> 10),
+            'seq_len': args.seq, 'masking': 'static', 'duplicate_factor': 5,
+            'rng': 'replay (CPython MT19937, random.seed per partition)',
+            'batch_bytes': int(n_bytes), 'sentences': int(n_sent), 'documents': int(corp.n_doc),
+            'partitions': int(len(part) - 1), 'wordpieces': pieces, 'pairs': int(pb.n_pairs),
+            'vocab': os.path.basename(VOCAB), 'parallelism': 'dp{} (document shards)'.format(world),
+        },
+        'stages_ms': {'tokenize': tok_ms, 'pairs_plan_and_gather': pair_ms},
+        'roofline': {'kernel': 'tokenize_lane_kernel', 'bound': 'hbm', 'achieved': achieved,
+                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
+                     'traffic': prof_traffic, 'algorithmic_bytes_per_launch': tok_bytes},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        res['cpu_baseline'] = cpu_baseline(corp, part, seeds, args)
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()
