@@ -25,7 +25,7 @@ def main(src, dst):
         f.write('{:>10} {:>6} {:>14} {:>14} {:>7}  kernel\n'.format('total_ms', 'calls', 'avg_us',
                                                                     'max_us', '%'))
         for r in rows:
-            name = r[0].split('(')[0].replace('lddl::(anonymous namespace)::', '')
+            name = r[0].replace('(anonymous namespace)::', '').split('(')[0]
             f.write('{:10.3f} {:6d} {:14.1f} {:14.1f} {:7.2f}  {}\n'.format(
                 r[2] / 1e6, r[1], r[3] / 1e3, r[5] / 1e3, 100.0 * r[2] / total, name[:110]))
     print(open(dst + '.txt').read())
