@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, '_lib', 'liblddl_amd.so')
+LIB_PATH = os.environ.get('LDDL_AMD_LIB') or os.path.join(_HERE, '_lib', 'liblddl_amd.so')
 
 c_i64, c_u64, c_i32, c_u32, c_dbl, c_vp = (ctypes.c_int64, ctypes.c_uint64, ctypes.c_int32,
                                            ctypes.c_uint32, ctypes.c_double, ctypes.c_void_p)

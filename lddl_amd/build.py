@@ -40,16 +40,21 @@ def _run(cmd):
     return r.stdout
 
 
-def build_product(verbose=False, jobs=8):
-    os.makedirs(LIBDIR, exist_ok=True)
-    os.makedirs(OBJDIR, exist_ok=True)
+def build_product(verbose=False, jobs=8, diag=False):
+    """diag=True builds the stamp-instrumented diagnostic library into lddl_amd/_lib_diag
+    (timing shares only; never the shipped library)."""
+    libdir = LIBDIR + ('_diag' if diag else '')
+    objdir = OBJDIR + ('_diag' if diag else '')
+    lib = os.path.join(libdir, 'liblddl_amd.so')
+    os.makedirs(libdir, exist_ok=True)
+    os.makedirs(objdir, exist_ok=True)
     headers = glob.glob(os.path.join(ROOT, 'include', '*.h')) + glob.glob(os.path.join(CSRC, '*.h'))
     srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')) + glob.glob(os.path.join(CSRC, '*.cpp')))
     flags = ['-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function',
-             '-I' + os.path.join(ROOT, 'include'), '-I' + CSRC]
+             '-I' + os.path.join(ROOT, 'include'), '-I' + CSRC] + (['-DLDDL_STAMPS'] if diag else [])
     objs, jobs_list = [], []
     for s in srcs:
-        o = os.path.join(OBJDIR, os.path.basename(s) + '.o')
+        o = os.path.join(objdir, os.path.basename(s) + '.o')
         objs.append(o)
         if _newer(o, [s] + headers):
             if s.endswith('.hip'):
@@ -61,10 +66,10 @@ def build_product(verbose=False, jobs=8):
         for out in ex.map(_run, jobs_list):
             if verbose and out:
                 print(out)
-    if _newer(LIB, objs):
-        _run([HIPCC, '-shared', '-fPIC', '--offload-arch=' + ARCH, '-o', LIB] + objs +
+    if _newer(lib, objs):
+        _run([HIPCC, '-shared', '-fPIC', '--offload-arch=' + ARCH, '-o', lib] + objs +
              ['-lpthread'])
-    return LIB
+    return lib
 
 
 def build_oracle():
@@ -84,4 +89,7 @@ def build_all(verbose=False):
 
 
 if __name__ == '__main__':
-    print(build_all(verbose=True))
+    if '--diag' in sys.argv:
+        print(build_product(verbose=True, diag=True))
+    else:
+        print(build_all(verbose=True))

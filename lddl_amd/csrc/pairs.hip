@@ -19,6 +19,7 @@
 //           the partition shuffle of pretrain.py:401).
 //   gather  one wave per pair: coalesced copy of A and B token spans from the tokenizer output,
 //           applying the mask decisions and emitting positions + labels.
+#include <cstdio>
 #include <vector>
 
 #include "common.h"
@@ -40,6 +41,21 @@ struct alignas(16) PairDesc {
 };
 
 constexpr int32_t kKeep = -1;  // mask decision "keep the original token" (pretrain.py:215-216)
+
+// Diagnostic build only (-DLDDL_STAMPS): per-region s_memtime sums of the planner.
+#ifdef LDDL_STAMPS
+constexpr int kStampRegions = 8;
+#define STAMP_T() __builtin_amdgcn_s_memtime()
+#define STAMP_ADD(r, t0)                   \
+  do {                                     \
+    const uint64_t t1_ = STAMP_T();        \
+    st_acc[r] += t1_ - (t0);               \
+    t0 = t1_;                              \
+  } while (0)
+#else
+#define STAMP_T() 0ull
+#define STAMP_ADD(r, t0) ((void)0)
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Compaction (pretrain.py:89-97): drop sentences with no pieces, then documents with no sentences
@@ -83,13 +99,64 @@ __global__ void part_offsets_kernel(const int64_t* part_doc_off, int64_t n_part,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Wave-uniform CPython MT19937 (Modules/_randommodule.c) with the state in LDS.
+// Wave-uniform CPython MT19937 (Modules/_randommodule.c).
+// Raw state and the tempered 624-word block live in LDS; draws are served from a register
+// window (lane l holds word wbase+l) through readlane, so a draw costs a few instructions.
+// Every lane executes the same sequential algorithm with identical scalars (uniform control
+// flow); only parallel phases (twist, temper, speculative shuffle draws) use the lanes.
 // ---------------------------------------------------------------------------------------------
 constexpr int kN = 624, kM = 397;
 
-struct WaveMT {
-  uint32_t* mt;  // LDS [624]
-  int mti;
+__device__ inline int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ inline uint32_t rdlane(uint32_t v, int idx) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, uni(idx));
+}
+__device__ inline uint32_t temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+struct WaveRng {
+  uint32_t* mt;  // LDS raw state [624]
+  uint32_t* tw;  // LDS tempered block [624]
+  int mti;       // next word of the block (uniform)
+  int wbase;     // window base (uniform)
+  uint32_t win;  // this lane's word tw[wbase + lane]
+
+  __device__ static uint32_t twist1(uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  }
+
+  // regenerate + temper the block with all 64 lanes: three dependency-free phases
+  __device__ void twist() {
+    const int l = threadIdx.x;
+    for (int i = l; i < kN - kM; i += 64) {  // [0,227): old[i], old[i+1], old[i+397]
+      const uint32_t v = twist1(mt[i], mt[i + 1], mt[i + kM]);
+      mt[i] = v;
+    }
+    __syncthreads();
+    for (int i = kN - kM + l; i < 2 * (kN - kM); i += 64) {  // [227,454): new[i-227]
+      const uint32_t v = twist1(mt[i], mt[i + 1], mt[i - (kN - kM)]);
+      mt[i] = v;
+    }
+    __syncthreads();
+    for (int i = 2 * (kN - kM) + l; i < kN - 1; i += 64) {  // [454,623): new[i-227]
+      const uint32_t v = twist1(mt[i], mt[i + 1], mt[i - (kN - kM)]);
+      mt[i] = v;
+    }
+    __syncthreads();
+    if (l == 0) mt[kN - 1] = twist1(mt[kN - 1], mt[0], mt[kM - 1]);
+    __syncthreads();
+    for (int i = l; i < kN; i += 64) tw[i] = temper(mt[i]);
+    __syncthreads();
+    mti = 0;
+    wbase = 0;
+    win = tw[l];
+  }
 
   __device__ void seed_i64(int64_t seed) {  // random.seed(int): init_by_array(abs(seed) limbs)
     if (threadIdx.x == 0) {
@@ -123,51 +190,80 @@ struct WaveMT {
       mt[0] = 0x80000000u;
     }
     __syncthreads();
-    mti = kN;
+    twist();  // CPython leaves index = N after seeding: the first draw twists
   }
 
-  __device__ static uint32_t twist1(uint32_t a, uint32_t b, uint32_t c) {
-    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-  }
-
-  // all 64 lanes: regenerate the 624-word block in three dependency-free phases
-  __device__ void twist() {
-    const int l = threadIdx.x;
-    for (int i = l; i < kN - kM; i += 64) {  // [0,227): old[i], old[i+1], old[i+397]
-      const uint32_t v = twist1(mt[i], mt[i + 1], mt[i + kM]);
-      mt[i] = v;
-    }
-    __syncthreads();
-    for (int i = kN - kM + l; i < 2 * (kN - kM); i += 64) {  // [227,454): new[i-227]
-      const uint32_t v = twist1(mt[i], mt[i + 1], mt[i - (kN - kM)]);
-      mt[i] = v;
-    }
-    __syncthreads();
-    for (int i = 2 * (kN - kM) + l; i < kN - 1; i += 64) {  // [454,623): new[i-227]
-      const uint32_t v = twist1(mt[i], mt[i + 1], mt[i - (kN - kM)]);
-      mt[i] = v;
-    }
-    __syncthreads();
-    if (l == 0) mt[kN - 1] = twist1(mt[kN - 1], mt[0], mt[kM - 1]);
-    __syncthreads();
-  }
-
-  __device__ uint32_t u32() {
+  // out of line: runs once per 64 draws (window load) or per 624 draws (twist)
+  __device__ void refill() {
     if (mti >= kN) {
       twist();
-      mti = 0;
+    } else {
+      wbase = uni(mti);
+      const int k = mti + (int)threadIdx.x;
+      win = k < kN ? tw[k] : 0u;
     }
-    uint32_t y = mt[mti++];
-    y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= (y >> 18);
-    return y;
   }
-  __device__ double random() {
+  __device__ uint32_t u32() {
+    if (mti >= wbase + 64 || mti >= kN) refill();
+    const uint32_t v = rdlane(win, mti - wbase);
+    mti = uni(mti + 1);
+    return v;
+  }
+  // Fisher-Yates draws of random.shuffle over n items: j_i = _randbelow(i+1), i = n-1 .. 1,
+  // delivered as sink(i, j_i). Wave-parallel over 64 words at a time: while k = bit_length(s+1)
+  // is fixed, word t is rejected iff R_t < c_t with c_t = (w_t >> (32-k)) - s0 + t and R_t the
+  // rejections before t. The sets {t : c_t > m} are nested, so the m-th rejection is the first
+  // lane after the (m-1)-th with c_t > m: one compare (= ballot) and a few scalar ops each.
+  template <typename Sink>
+  __device__ void fy_draws(int64_t n, Sink sink) {
+    constexpr int kHyp = 24;  // rejections resolved per 64-word window (expected ~16)
+    const int lane = threadIdx.x;
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    int64_t s0 = n - 1;  // next step (uniform)
+    while (s0 >= 1) {
+      if (mti >= kN) twist();
+      const int k = 32 - __clz((uint32_t)(s0 + 1));
+      const int64_t s_lo = (1ll << (k - 1)) - 1 > 1 ? (1ll << (k - 1)) - 1 : 1;
+      const int64_t need = s0 - s_lo + 1;  // steps served by this k
+      const int L = min(64, kN - mti);
+      const uint32_t w = lane < L ? tw[mti + lane] : 0u;
+      const int64_t x = (int64_t)(w >> (32 - k));
+      const int64_t c = x - s0 + lane;
+      uint64_t rej = 0;
+      int U = L;  // lanes [0, U) resolved
+      int pos = 0;
+      for (int m = 0; m < kHyp; ++m) {
+        const uint64_t bm = __ballot(lane < L && c > m) & (pos < 64 ? (~0ull << pos) : 0ull);
+        if (!bm) break;
+        const int r = __ffsll((unsigned long long)bm) - 1;
+        rej |= 1ull << r;
+        pos = r + 1;
+        if (m == kHyp - 1) U = pos;  // more rejections may follow: stop after the last known
+      }
+      const int64_t R = __popcll(rej & lt_mask);
+      const int64_t rank = lane - R;  // accepted words before this lane
+      const uint64_t consumed = __ballot(lane < U && rank < need);
+      const int E = __popcll(consumed);
+      const bool accepted = lane < E && !((rej >> lane) & 1ull);
+      if (accepted) sink(s0 - rank, (uint32_t)x);
+      mti += E;
+      s0 -= E - __popcll(rej & (E >= 64 ? ~0ull : ((1ull << E) - 1)));
+      s0 = (int64_t)uni((int)s0);
+      mti = uni(mti);
+    }
+    __syncthreads();
+    wbase = -1024;  // the register window is stale
+  }
+  // random() = N / 2^53 with N = (w1 >> 5) * 2^26 + (w2 >> 6). `random() < p` is decided exactly
+  // on N: N < ceil(p * 2^53) (see k_short / kLt08), so no floating point is needed.
+  __device__ uint64_t rand53() {
     const uint32_t a = u32() >> 5, b = u32() >> 6;
-    return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
+    return ((uint64_t)a << 26) | b;
+  }
+  __device__ bool below_half() {  // random() < 0.5  <=>  N < 2^52  <=>  w1 < 2^31
+    const uint32_t a = u32();
+    (void)u32();
+    return a < 0x80000000u;
   }
   __device__ uint32_t randbelow(uint32_t n) {
     const int k = 32 - __clz(n);
@@ -176,6 +272,7 @@ struct WaveMT {
     return r;
   }
   __device__ int64_t randint(int64_t a, int64_t b) { return a + randbelow((uint32_t)(b - a + 1)); }
+
 };
 
 struct PlanArgs {
@@ -189,21 +286,41 @@ struct PlanArgs {
   // params
   int32_t seq, dup, masking, vocab_size, cls_id, sep_id, mask_id, max_pred;
   double short_seq_prob, ratio;
+  uint64_t k_short;  // random() < short_seq_prob  <=>  N < k_short = ceil(short_seq_prob * 2^53)
+  int32_t seq_r64;   // seq rounded up to a multiple of 64
   // outputs, slot base of partition p = dup * kd_off[kp_off[p]]
   PairDesc* desc;
-  int32_t* order;      // per slot: creation index at final position
+  int32_t* jseq;       // per slot: j_i draws of the final partition shuffle
   int32_t* nmask;      // per slot
   uint16_t* mpos;      // per slot * max_pred
   int32_t* mtok;       // per slot * max_pred
   int64_t* part_npairs;
+  uint64_t* stamps;  // diagnostic build: [n_part][8]
 };
 
-__device__ inline int32_t slen(const PlanArgs& A, int64_t k) { return A.ks_len[k] & kLenMask; }
+constexpr int kDocLds = 2048;
+constexpr uint64_t kLt08 = 7205759403792794ull;  // 0.8 (binary64) * 2^53, exact  // partitions with <= this many documents cache offsets in LDS
+
+// Sentence lengths of one document through a 64-entry register window.
+struct LenWin {
+  const int32_t* len;  // ks_len + first kept sentence of the doc
+  int n, wbase;
+  int32_t win;
+  __device__ void reset(const int32_t* p, int nn) { len = p; n = nn; wbase = -1024; }
+  __device__ int32_t at(int j) {  // raw length word (flags included)
+    if (j < wbase || j >= wbase + 64) {
+      wbase = j;
+      const int k = j + (int)threadIdx.x;
+      win = k < n ? len[k] : 0;
+    }
+    return (int32_t)rdlane((uint32_t)win, j - wbase);
+  }
+};
 
 // token j (0-based) of the span that starts at kept sentence k0 (sequential walk; slow path only)
 __device__ int32_t span_token(const PlanArgs& A, int64_t k0, int64_t j) {
   for (int64_t k = k0;; ++k) {
-    const int32_t l = slen(A, k);
+    const int32_t l = A.ks_len[k] & kLenMask;
     if (j < l) return A.ids[A.ks_start[k] + j];
     j -= l;
   }
@@ -211,39 +328,60 @@ __device__ int32_t span_token(const PlanArgs& A, int64_t k0, int64_t j) {
 
 __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  WaveMT rng{reinterpret_cast<uint32_t*>(smem), kN};
-  uint16_t* cand = reinterpret_cast<uint16_t*>(smem + 4 * kN);              // [seq]
-  uint16_t* tpos = cand + ((A.seq + 7) & ~7);                                // [max_pred]
-  int32_t* ttok = reinterpret_cast<int32_t*>(tpos + ((A.max_pred + 7) & ~7));  // [max_pred]
+  uint32_t* s_mt = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* s_tw = s_mt + kN;
+  int32_t* s_doc = reinterpret_cast<int32_t*>(s_tw + kN);                 // [kDocLds + 1]
+  uint16_t* jarr = reinterpret_cast<uint16_t*>(s_doc + kDocLds + 4);     // [seq rounded to 64]
+  uint16_t* cand = jarr + A.seq_r64;                                       // [seq] (slow path)
+  uint16_t* tpos = cand + A.seq_r64;                                       // [max_pred]
+  int32_t* ttok = reinterpret_cast<int32_t*>(tpos + ((A.max_pred + 7) & ~7));
   const int p = blockIdx.x;
   const int lane = threadIdx.x;
   const bool leader = lane == 0;
+#ifdef LDDL_STAMPS
+  uint64_t st_acc[kStampRegions] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  uint64_t st_t = STAMP_T();
+  WaveRng rng{s_mt, s_tw, 0, 0, 0u};
   rng.seed_i64(A.part_seed[p]);
   const int64_t d0 = A.kp_off[p], nd = A.kp_off[p + 1] - d0;
-  const int64_t base = (int64_t)A.dup * A.kd_off[d0];
+  const int64_t kbase = A.kd_off[d0];
+  const bool doc_lds = nd + 1 <= kDocLds;
+  if (doc_lds)
+    for (int64_t d = lane; d <= nd; d += 64) s_doc[d] = (int32_t)(A.kd_off[d0 + d] - kbase);
+  __syncthreads();
+  auto doc_off = [&](int64_t d) -> int64_t {  // kept-sentence index of document d (partition-local)
+    return doc_lds ? kbase + uni(s_doc[d]) : A.kd_off[d0 + d];
+  };
+  const int64_t base = (int64_t)A.dup * kbase;
   const int32_t max_num = A.seq - 3;
+  LenWin La, Lb;
   int64_t np = 0;
   for (int dp = 0; dp < A.dup; ++dp) {
     for (int64_t di = 0; di < nd; ++di) {
-      const int64_t s0 = A.kd_off[d0 + di], ns = A.kd_off[d0 + di + 1] - s0;
+      const int64_t s0 = doc_off(di);
+      const int ns = (int)(doc_off(di + 1) - s0);
+      La.reset(A.ks_len + s0, ns);
       int32_t target = max_num;
-      if (rng.random() < A.short_seq_prob) target = (int32_t)rng.randint(2, max_num);
-      int64_t chunk0 = 0, chunk_n = 0, cur_len = 0;
-      for (int64_t i = 0; i < ns; ++i) {
+      if (rng.rand53() < A.k_short) target = (int32_t)rng.randint(2, max_num);
+      int chunk0 = 0, chunk_n = 0;
+      int64_t cur_len = 0;
+      for (int i = 0; i < ns; ++i) {
         if (chunk_n == 0) chunk0 = i;
         ++chunk_n;
-        cur_len += slen(A, s0 + i);
+        cur_len += La.at(i) & kLenMask;
         if (!(i == ns - 1 || cur_len >= target)) continue;
-        const int64_t a_end = chunk_n >= 2 ? rng.randint(1, chunk_n - 1) : 1;
+        const int a_end = chunk_n >= 2 ? (int)rng.randint(1, chunk_n - 1) : 1;
         int64_t la = 0;
         int32_t flags = 0;
-        for (int64_t j = chunk0; j < chunk0 + a_end; ++j) {
-          la += slen(A, s0 + j);
-          flags |= A.ks_len[s0 + j];
+        for (int j = chunk0; j < chunk0 + a_end; ++j) {
+          const int32_t w = La.at(j);
+          la += w & kLenMask;
+          flags |= w;
         }
         int64_t lb = 0, b_ks;
         int32_t rn = 0;
-        if (chunk_n == 1 || rng.random() < 0.5) {
+        if (chunk_n == 1 || rng.below_half()) {
           rn = 1;
           const int64_t target_b = target - la;
           int64_t rd = 0;
@@ -252,71 +390,98 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
             if (rd != di) break;
           }
           if (rd == di) rn = 0;
-          const int64_t r0 = A.kd_off[d0 + rd], rns = A.kd_off[d0 + rd + 1] - r0;
-          const int64_t rstart = rng.randint(0, rns - 1);
+          const int64_t r0 = doc_off(rd);
+          const int rns = (int)(doc_off(rd + 1) - r0);
+          const int rstart = (int)rng.randint(0, rns - 1);
           b_ks = r0 + rstart;
-          for (int64_t j = rstart; j < rns; ++j) {
-            lb += slen(A, r0 + j);
-            flags |= A.ks_len[r0 + j];
+          Lb.reset(A.ks_len + r0, rns);
+          for (int j = rstart; j < rns; ++j) {
+            const int32_t w = Lb.at(j);
+            lb += w & kLenMask;
+            flags |= w;
             if (lb >= target_b) break;
           }
           i -= chunk_n - a_end;
         } else {
           b_ks = s0 + chunk0 + a_end;
-          for (int64_t j = chunk0 + a_end; j < chunk0 + chunk_n; ++j) {
-            lb += slen(A, s0 + j);
-            flags |= A.ks_len[s0 + j];
+          for (int j = chunk0 + a_end; j < chunk0 + chunk_n; ++j) {
+            const int32_t w = La.at(j);
+            lb += w & kLenMask;
+            flags |= w;
           }
         }
         // _truncate_seq_pair
         int32_t a_front = 0, b_front = 0, na = (int32_t)la, nb = (int32_t)lb;
         while (na + nb > max_num) {
-          const bool front = rng.random() < 0.5;
+          const int32_t front = rng.below_half() ? 1 : 0;
           if (na > nb) { a_front += front; --na; }
           else { b_front += front; --nb; }
         }
+        STAMP_ADD(0, st_t);
         const int64_t slot = base + np;
         if (leader) A.desc[slot] = PairDesc{s0 + chunk0, b_ks, a_front, na, b_front,
                                             nb | (int32_t)((uint32_t)rn << 31)};
         if (A.masking) {
-          // candidates: every position of [CLS] A [SEP] B [SEP] whose token is not [CLS]/[SEP]
+          // candidates = positions of [CLS] A [SEP] B [SEP] whose token is not [CLS]/[SEP]
           int32_t nc = na + nb;
-          if (flags & kLenHasClsSep) {  // literal [CLS]/[SEP] inside A or B: inspect tokens
+          const bool slow = (flags & kLenHasClsSep) != 0;
+          if (slow) {  // literal [CLS]/[SEP] inside A or B: inspect the tokens
             int32_t c = 0;
             for (int32_t t = 0; t < na + nb; ++t) {
-              const int32_t tok = t < na ? span_token(A, s0 + chunk0, a_front + t)
-                                         : span_token(A, b_ks, b_front + (t - na));
+              const int32_t tok = uni(t < na ? span_token(A, s0 + chunk0, a_front + t)
+                                             : span_token(A, b_ks, b_front + (t - na)));
               if (tok != A.cls_id && tok != A.sep_id) {
                 if (leader) cand[c] = (uint16_t)(t < na ? t + 1 : t + 2);
                 ++c;
               }
             }
-            nc = c;
-          } else {
-            for (int32_t k = lane; k < nc; k += 64) cand[k] = (uint16_t)(k < na ? k + 1 : k + 2);
+            nc = uni(c);
+            __syncthreads();
           }
-          __syncthreads();
-          for (int32_t k = nc - 1; k > 0; --k) {  // random.shuffle(cand_indexes)
-            const uint32_t j = rng.randbelow((uint32_t)k + 1);
-            if (leader) {
-              const uint16_t t = cand[k];
-              cand[k] = cand[j];
-              cand[j] = t;
-            }
-          }
-          const double prod = (double)(na + nb + 3) * A.ratio;
-          int32_t num = (int32_t)rint(prod);  // Python round(): half to even
+          STAMP_ADD(1, st_t);
+          // random.shuffle(cand_indexes): draws j_i (i = nc-1 .. 1) into jarr
+          rng.fy_draws(nc, [&](int64_t i, uint32_t j) { jarr[i] = (uint16_t)j; });
+          STAMP_ADD(2, st_t);
+          int32_t num = (int32_t)rint((double)(na + nb + 3) * A.ratio);  // round(): half-even
           if (num < 1) num = 1;
           if (num > nc) num = nc;
-          for (int32_t c = 0; c < num; ++c) {
-            int32_t tok;
-            if (rng.random() < 0.8) tok = A.mask_id;
-            else if (rng.random() < 0.5) tok = kKeep;
-            else tok = (int32_t)rng.randint(0, A.vocab_size - 1);
-            if (leader) {
-              tpos[c] = cand[c];
-              ttok[c] = tok;
+          // the j draws in registers: jr[k] holds j_{64k + lane}
+          uint32_t jr[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) jr[k] = (64 * k + lane < nc) ? jarr[64 * k + lane] : 0u;
+          for (int32_t c0 = 0; c0 < num; c0 += 64) {
+            // final slot pp (< num) of the shuffled candidates: undo the transpositions
+            // i = pp+1 .. nc-1 to find its original index y
+            const int pp = c0 + lane;
+            int y = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if ((pp >> 6) == k) y = pp == 0 ? 0 : (int)jr[k];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const int i_lo = max(64 * k, c0 + 1), i_hi = min(64 * k + 64, nc);
+              for (int i2 = i_lo; i2 < i_hi; ++i2) {
+                // going backwards y < i2 always holds, so only j_i == y moves it (to i)
+                const int ji = (int)rdlane(jr[k], i2 - 64 * k);
+                y = (ji == y && i2 > pp) ? i2 : y;
+              }
             }
+            const int cval = slow ? (int)cand[y < nc ? y : 0] : (y < na ? y + 1 : y + 2);
+            STAMP_ADD(3, st_t);
+            const int cmax = min(64, num - c0);
+            int32_t mytok = 0;
+            for (int c = 0; c < cmax; ++c) {
+              int32_t tok;
+              if (rng.rand53() < kLt08) tok = A.mask_id;
+              else if (rng.below_half()) tok = kKeep;
+              else tok = (int32_t)rng.randint(0, A.vocab_size - 1);
+              mytok = lane == c ? tok : mytok;  // writelane
+            }
+            if (lane < cmax) {
+              tpos[c0 + lane] = (uint16_t)cval;
+              ttok[c0 + lane] = mytok;
+            }
+            STAMP_ADD(4, st_t);
           }
           __syncthreads();
           // sorted(masked_lms, key=index): rank sort (positions are distinct)
@@ -329,6 +494,7 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
           }
           if (leader) A.nmask[slot] = num;
           __syncthreads();
+          STAMP_ADD(5, st_t);
         }
         ++np;
         chunk_n = 0;
@@ -336,21 +502,56 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
       }
     }
   }
-  // random.shuffle(partition_pairs): order[base + k] = creation index of the pair at position k
-  if (leader) {
-    int32_t* ord = A.order + base;
-    for (int64_t k = 0; k < np; ++k) ord[k] = (int32_t)k;
+  // random.shuffle(partition_pairs) (pretrain.py:401): record the draws j_i, i = np-1 .. 1
+  // (64 at a time through writelane); apply_shuffle_kernel performs the swaps.
+  STAMP_ADD(0, st_t);
+  {
+    int32_t* js = A.jseq + base;
+    rng.fy_draws(np, [&](int64_t i, uint32_t j) { js[i] = (int32_t)j; });
   }
-  for (int64_t k = np - 1; k > 0; --k) {
-    const uint32_t j = rng.randbelow((uint32_t)k + 1);
-    if (leader) {
-      int32_t* ord = A.order + base;
-      const int32_t t = ord[k];
-      ord[k] = ord[j];
+  STAMP_ADD(6, st_t);
+#ifdef LDDL_STAMPS
+  if (leader && A.stamps)
+    for (int r = 0; r < kStampRegions; ++r) A.stamps[(int64_t)p * kStampRegions + r] = st_acc[r];
+#endif
+  if (leader) A.part_npairs[p] = np;
+}
+
+// Perform the final per-partition Fisher-Yates swaps (draws from plan_replay_kernel). One
+// workgroup per partition; the permutation lives in LDS when it fits, else in global memory.
+constexpr int kShufLds = 32768;
+
+__global__ void __launch_bounds__(64) apply_shuffle_kernel(const int64_t* kd_off, const int64_t* kp_off,
+                                                          int32_t dup, const int64_t* part_npairs,
+                                                          const int32_t* jseq, int32_t* order) {
+  extern __shared__ __attribute__((aligned(16))) int32_t s_ord[];
+  const int p = blockIdx.x;
+  const int64_t base = (int64_t)dup * kd_off[kp_off[p]];
+  const int64_t np = part_npairs[p];
+  const int32_t* js = jseq + base;
+  int32_t* ord = order + base;
+  if (np <= kShufLds) {
+    for (int64_t k = threadIdx.x; k < np; k += 64) s_ord[k] = (int32_t)k;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int64_t i = np - 1; i > 0; --i) {
+        const int32_t j = js[i];
+        const int32_t t = s_ord[i];
+        s_ord[i] = s_ord[j];
+        s_ord[j] = t;
+      }
+    }
+    __syncthreads();
+    for (int64_t k = threadIdx.x; k < np; k += 64) ord[k] = s_ord[k];
+  } else if (threadIdx.x == 0) {
+    for (int64_t k = 0; k < np; ++k) ord[k] = (int32_t)k;
+    for (int64_t i = np - 1; i > 0; --i) {
+      const int32_t j = js[i];
+      const int32_t t = ord[i];
+      ord[i] = ord[j];
       ord[j] = t;
     }
   }
-  if (leader) A.part_npairs[p] = np;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -512,6 +713,13 @@ struct lddl_pairs {
     }                              \
   } while (0)
 
+// ceil(p * 2^53): random() < p  <=>  N < this (N = 53-bit integer behind random())
+static uint64_t short_threshold(double p) {
+  if (!(p > 0)) return 0;
+  if (p >= 1) return 1ull << 53;
+  return (uint64_t)ceil(ldexp(p, 53));
+}
+
 extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params* prm,
                                const int64_t* d_sent_off, const int32_t* d_ids,
                                const int32_t* d_sent_len, int64_t n_sent,
@@ -571,8 +779,10 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     if (max_pred > kMaxPredLds) TRY((set_error("masked_lm_ratio * seq too large"), -1));
   }
   P->max_pred = max_pred;
+  int32_t* jseq;
   TRY(P->alloc(&P->desc, slots, st));
   TRY(P->alloc(&P->order, slots, st));
+  TRY(P->alloc(&jseq, slots, st));
   TRY(P->alloc(&part_npairs, n_part + 1, st));
   if (prm->masking) {
     TRY(P->alloc(&P->nmask, slots, st));
@@ -581,12 +791,42 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   }
   PlanArgs A{P->ks_start, P->ks_len, P->kd_off, P->kp_off, d_ids, d_part_seed,
              prm->seq, prm->dup, prm->masking, c->vocab_size, cls, sep, msk, max_pred,
-             prm->short_seq_prob, prm->masked_lm_ratio,
-             P->desc, P->order, P->nmask, P->mpos, P->mtok, part_npairs};
-  const size_t lds = 4 * kN + 2 * ((prm->seq + 7) & ~7) + 2 * ((max_pred + 7) & ~7) + 4 * max_pred + 16;
-  if (n_part)
+             prm->short_seq_prob, prm->masked_lm_ratio, short_threshold(prm->short_seq_prob),
+             ((prm->seq + 63) / 64) * 64, P->desc, jseq, P->nmask, P->mpos, P->mtok, part_npairs, nullptr};
+#ifdef LDDL_STAMPS
+  uint64_t* d_stamps;
+  TRY(P->alloc(&d_stamps, n_part * kStampRegions, st));
+  LDDL_HIP(hipMemsetAsync(d_stamps, 0, 8 * n_part * kStampRegions, st));
+  A.stamps = d_stamps;
+#endif
+  if (prm->seq > 512) TRY((set_error("replay planner supports target_seq_length <= 512"), -1));
+  const size_t lds = 8 * kN + 4 * (kDocLds + 4) + 4 * (size_t)A.seq_r64 +
+                     2 * ((max_pred + 7) & ~7) + 4 * max_pred + 16;
+  if (n_part) {
     hipLaunchKernelGGL(plan_replay_kernel, dim3((unsigned)n_part), dim3(64), lds, st, A);
+    hipLaunchKernelGGL(apply_shuffle_kernel, dim3((unsigned)n_part), dim3(64),
+                       sizeof(int32_t) * kShufLds, st, P->kd_off, P->kp_off, prm->dup,
+                       part_npairs, jseq, P->order);
+  }
   LDDL_HIP(hipGetLastError());
+#ifdef LDDL_STAMPS
+  {
+    std::vector<uint64_t> h(n_part * kStampRegions);
+    LDDL_HIP(hipMemcpyAsync(h.data(), d_stamps, 8 * h.size(), hipMemcpyDeviceToHost, st));
+    LDDL_HIP(hipStreamSynchronize(st));
+    double tot[kStampRegions] = {0};
+    for (int64_t q = 0; q < n_part; ++q)
+      for (int r = 0; r < kStampRegions; ++r) tot[r] += (double)h[q * kStampRegions + r];
+    const char* names[kStampRegions] = {"plan", "cand", "shuffle_draws", "traceback", "decisions",
+                                        "sort_write", "final_shuffle_draws", "-"};
+    double all = 0;
+    for (double t : tot) all += t;
+    fprintf(stderr, "[stamps] plan_replay_kernel mean cycles per partition:");
+    for (int r = 0; r < kStampRegions; ++r)
+      fprintf(stderr, " %s=%.3g (%.1f%%)", names[r], tot[r] / n_part, 100.0 * tot[r] / (all + 1e-9));
+    fprintf(stderr, "\n");
+  }
+#endif
   // layout
   TRY(P->alloc(&part_base, n_part + 1, st));
   if (scan_exclusive(Identity{part_npairs}, n_part, part_base, scratch, st) != hipSuccess) TRY(-100);
