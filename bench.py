@@ -88,7 +88,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--batch-bytes', type=int, default=1 << 30)
+    ap.add_argument('--batch-bytes', type=int, default=4 << 30)
     ap.add_argument('--partition-bytes', type=int, default=1 << 20)
     ap.add_argument('--seq', type=int, default=128)
     ap.add_argument('--seed', type=int, default=1234)
@@ -200,7 +200,7 @@ def main():
             'vocab': os.path.basename(VOCAB), 'parallelism': 'dp{} (document shards)'.format(world),
         },
         'stages_ms': {'tokenize': tok_ms, 'pairs_plan_and_gather': pair_ms},
-        'roofline': {'kernel': 'tokenize_lane_kernel', 'bound': 'hbm', 'achieved': achieved,
+        'roofline': {'kernel': 'tokenize_wave_kernel', 'bound': 'hbm', 'achieved': achieved,
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                      'traffic': prof_traffic, 'algorithmic_bytes_per_launch': tok_bytes},
     }

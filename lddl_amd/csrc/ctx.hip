@@ -135,6 +135,21 @@ extern "C" int lddl_ctx_create(int device, const uint8_t* norm_table, int64_t ta
     for (int32_t i = 0; i < V; ++i)
       if (c->tokens[i] == kSpecial[k]) { T.special_id[k] = i; break; }
   }
+  // classify the ASCII page for the wave tokenizer's register fast path
+  {
+    const uint16_t* l1p = reinterpret_cast<const uint16_t*>(l1);
+    const uint32_t* pg = reinterpret_cast<const uint32_t*>(pages) + 256 * (size_t)l1p[0];
+    bool lower_ok = true, ident_ok = true;
+    for (uint32_t cp = 0; cp < 128; ++cp) {
+      const uint32_t e = pg[cp];
+      if ((e >> 30) != kWord) continue;
+      const uint32_t outc = (e & kIdent) ? cp : (e & kMulti) ? 0xFFFFFFFFu : (e & 0x1FFFFFu);
+      const uint32_t want_lower = (cp >= 'A' && cp <= 'Z') ? cp + 32 : cp;
+      lower_ok &= outc == want_lower;
+      ident_ok &= outc == cp;
+    }
+    T.ascii_mode = ident_ok ? 2 : lower_ok ? 1 : 0;
+  }
   if (T.special_id[kUnk] < 0) { lddl_ctx_destroy(c); LDDL_FAIL(-1, "vocab has no [UNK]"); }
   *out = c;
   return 0;

@@ -52,6 +52,9 @@ struct Tables {
   uint32_t vmask;
   int32_t max_piece_bytes;
   int32_t special_id[kNumSpecial];
+  // ASCII fast path of the wave tokenizer: 1 = ASCII WORD chars map to themselves except A-Z ->
+  // a-z (uncased table), 2 = all map to themselves (cased), 0 = neither (fast path disabled)
+  int32_t ascii_mode;
 };
 
 // sent_len flag: the kept pieces contain a literal [CLS] or [SEP] (matters for static masking

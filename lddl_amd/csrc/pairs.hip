@@ -121,10 +121,10 @@ __device__ inline uint32_t temper(uint32_t y) {
 
 struct WaveRng {
   uint32_t* mt;  // LDS raw state [624]
-  uint32_t* tw;  // LDS tempered block [624]
+  uint32_t* tw;  // unused (the block is tempered on read; keeps LDS at one 624-word state)
   int mti;       // next word of the block (uniform)
   int wbase;     // window base (uniform)
-  uint32_t win;  // this lane's word tw[wbase + lane]
+  uint32_t win;  // this lane's tempered word temper(mt[wbase + lane])
 
   __device__ static uint32_t twist1(uint32_t a, uint32_t b, uint32_t c) {
     const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
@@ -151,11 +151,9 @@ struct WaveRng {
     __syncthreads();
     if (l == 0) mt[kN - 1] = twist1(mt[kN - 1], mt[0], mt[kM - 1]);
     __syncthreads();
-    for (int i = l; i < kN; i += 64) tw[i] = temper(mt[i]);
-    __syncthreads();
     mti = 0;
     wbase = 0;
-    win = tw[l];
+    win = temper(mt[l]);
   }
 
   __device__ void seed_i64(int64_t seed) {  // random.seed(int): init_by_array(abs(seed) limbs)
@@ -200,7 +198,7 @@ struct WaveRng {
     } else {
       wbase = uni(mti);
       const int k = mti + (int)threadIdx.x;
-      win = k < kN ? tw[k] : 0u;
+      win = k < kN ? temper(mt[k]) : 0u;
     }
   }
   __device__ uint32_t u32() {
@@ -216,39 +214,48 @@ struct WaveRng {
   // lane after the (m-1)-th with c_t > m: one compare (= ballot) and a few scalar ops each.
   template <typename Sink>
   __device__ void fy_draws(int64_t n, Sink sink) {
-    constexpr int kHyp = 24;  // rejections resolved per 64-word window (expected ~16)
     const int lane = threadIdx.x;
     const uint64_t lt_mask = (1ull << lane) - 1;
-    int64_t s0 = n - 1;  // next step (uniform)
+    int32_t s0 = (int32_t)(n - 1);  // next step (uniform); n < 2^30 (host-checked)
     while (s0 >= 1) {
       if (mti >= kN) twist();
       const int k = 32 - __clz((uint32_t)(s0 + 1));
-      const int64_t s_lo = (1ll << (k - 1)) - 1 > 1 ? (1ll << (k - 1)) - 1 : 1;
-      const int64_t need = s0 - s_lo + 1;  // steps served by this k
+      const int32_t s_lo = (1 << (k - 1)) - 1 > 1 ? (1 << (k - 1)) - 1 : 1;
+      const int32_t need = s0 - s_lo + 1;  // steps served by this k
       const int L = min(64, kN - mti);
-      const uint32_t w = lane < L ? tw[mti + lane] : 0u;
-      const int64_t x = (int64_t)(w >> (32 - k));
-      const int64_t c = x - s0 + lane;
+      const uint32_t w = lane < L ? temper(mt[mti + lane]) : 0u;
+      const int32_t x = (int32_t)(w >> (32 - k));
+      // word t is rejected iff c_t > R_t (R_t = rejections before t); clamp keeps it in int range
+      const int32_t c = lane < L ? min(max(x - s0 + lane, -1), 127) : -1;
+      // the m-th rejection is the first lane after the (m-1)-th with c > m. The nested sets
+      // {c > m} are ballotted 8 at a time by independent compares, then resolved by a pure
+      // scalar chain (no VALU->SALU round trip per rejection).
       uint64_t rej = 0;
-      int U = L;  // lanes [0, U) resolved
       int pos = 0;
-      for (int m = 0; m < kHyp; ++m) {
-        const uint64_t bm = __ballot(lane < L && c > m) & (pos < 64 ? (~0ull << pos) : 0ull);
-        if (!bm) break;
-        const int r = __ffsll((unsigned long long)bm) - 1;
-        rej |= 1ull << r;
-        pos = r + 1;
-        if (m == kHyp - 1) U = pos;  // more rejections may follow: stop after the last known
+      for (int m0 = 0; m0 < 64; m0 += 8) {
+        uint64_t B[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) B[q] = __ballot(c > m0 + q);
+        bool done = false;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint64_t bm = B[q] & (pos < 64 ? (~0ull << pos) : 0ull);
+          if (!bm) { done = true; break; }
+          const int r = __ffsll((unsigned long long)bm) - 1;
+          rej |= 1ull << r;
+          pos = r + 1;
+        }
+        if (done || pos >= L) break;
       }
-      const int64_t R = __popcll(rej & lt_mask);
-      const int64_t rank = lane - R;  // accepted words before this lane
-      const uint64_t consumed = __ballot(lane < U && rank < need);
+      const int32_t R = __popcll(rej & lt_mask);
+      const int32_t rank = lane - R;  // accepted words before this lane
+      const uint64_t consumed = __ballot(lane < L && rank < need);
       const int E = __popcll(consumed);
       const bool accepted = lane < E && !((rej >> lane) & 1ull);
-      if (accepted) sink(s0 - rank, (uint32_t)x);
+      if (accepted) sink((int64_t)(s0 - rank), (uint32_t)x);
       mti += E;
       s0 -= E - __popcll(rej & (E >= 64 ? ~0ull : ((1ull << E) - 1)));
-      s0 = (int64_t)uni((int)s0);
+      s0 = uni(s0);
       mti = uni(mti);
     }
     __syncthreads();
@@ -298,7 +305,7 @@ struct PlanArgs {
   uint64_t* stamps;  // diagnostic build: [n_part][8]
 };
 
-constexpr int kDocLds = 2048;
+constexpr int kDocLds = 512;
 constexpr uint64_t kLt08 = 7205759403792794ull;  // 0.8 (binary64) * 2^53, exact  // partitions with <= this many documents cache offsets in LDS
 
 // Sentence lengths of one document through a 64-entry register window.
@@ -329,8 +336,8 @@ __device__ int32_t span_token(const PlanArgs& A, int64_t k0, int64_t j) {
 __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* s_mt = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* s_tw = s_mt + kN;
-  int32_t* s_doc = reinterpret_cast<int32_t*>(s_tw + kN);                 // [kDocLds + 1]
+  uint32_t* s_tw = nullptr;
+  int32_t* s_doc = reinterpret_cast<int32_t*>(s_mt + kN);                 // [kDocLds + 1]
   uint16_t* jarr = reinterpret_cast<uint16_t*>(s_doc + kDocLds + 4);     // [seq rounded to 64]
   uint16_t* cand = jarr + A.seq_r64;                                       // [seq] (slow path)
   uint16_t* tpos = cand + A.seq_r64;                                       // [max_pred]
@@ -800,7 +807,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   A.stamps = d_stamps;
 #endif
   if (prm->seq > 512) TRY((set_error("replay planner supports target_seq_length <= 512"), -1));
-  const size_t lds = 8 * kN + 4 * (kDocLds + 4) + 4 * (size_t)A.seq_r64 +
+  const size_t lds = 4 * kN + 4 * (kDocLds + 4) + 4 * (size_t)A.seq_r64 +
                      2 * ((max_pred + 7) & ~7) + 4 * max_pred + 16;
   if (n_part) {
     hipLaunchKernelGGL(plan_replay_kernel, dim3((unsigned)n_part), dim3(64), lds, st, A);

@@ -60,3 +60,56 @@ def test_tokenize_max_pieces_gpu(ctxs):
         ids, o = ctxs['uncased'].tokenize_host(text, off, max_pieces=mp)
         e, eo = tok.tokenize(text, off, max_pieces=mp)
         np.testing.assert_array_equal(ids, e)
+
+
+def _adversarial_corpus(seed=7, n=6000):
+    """Sentences built to hit every branch of the wave tokenizer: literal special tokens and
+    multi-byte code points straddling 64-byte windows, invalid UTF-8, control chars inside words,
+    words of 16/17/64/65/150/500 bytes, many-piece words, CJK, separator code points beyond ASCII,
+    empty and whitespace-only sentences."""
+    rng = np.random.default_rng(seed)
+    frags = [b'the', b'Strommeth', b'[MASK]', b'[CLS]', b'[SEP]', b'[PAD]', b'[UNK]', b'[MAS', b'[[SEP]]',
+             b'x[MASK]y', 'café'.encode(), 'ÉCOLE'.encode(), '中文'.encode(),
+             '　'.encode(), ' '.encode(), ' '.encode(), b'\x01', b'ab\x00cd', b'\x7f',
+             b'\xe2\x82', b'\xff', b'\xc3', b'\x80\x80', '𝐀'.encode('utf-8', 'surrogatepass'),
+             '\U0001d400\U0001d401'.encode(), 'ﬃn'.encode(), 'İstanbul'.encode(),
+             'ȺȺ'.encode(), b'1234567890123456789012345', b'a' * 16, b'b' * 17, b'c' * 63,
+             b'd' * 64, b'e' * 65, b'f' * 150, b'g' * 500, ('hé' * 40).encode(), b'(', b')', b'...', b"don't", b'U.S.A.', b'\t', b'\n', b'  ',
+             ('ß' * 30).encode(), ('ΑΒ' * 12).encode()]
+    sents = []
+    for _ in range(n):
+        k = int(rng.integers(0, 24))
+        parts = []
+        for _ in range(k):
+            f = frags[int(rng.integers(0, len(frags)))]
+            sep = [b' ', b'', b'  ', b'-', b'\t'][int(rng.integers(0, 5))]
+            parts.append(f + sep)
+        sents.append(b''.join(parts))
+    text = np.frombuffer(b''.join(sents), np.uint8).copy()
+    off = np.zeros(len(sents) + 1, np.int64)
+    off[1:] = np.cumsum([len(x) for x in sents])
+    return text, off
+
+
+@pytest.mark.parametrize('case', ['uncased', 'cased'])
+def test_tokenize_adversarial_vs_oracle(case, ctxs):
+    from oracle import oracle as O
+    text, off = _adversarial_corpus()
+    vocab = VOCAB_UNCASED if case == 'uncased' else VOCAB_CASED
+    tok = O.Tokenizer(vocab, lowercase=case == 'uncased')
+    for mp in (512, 9):
+        ids, o = ctxs[case].tokenize_host(text, off, max_pieces=mp)
+        e, eo = tok.tokenize(text, off, max_pieces=mp)
+        np.testing.assert_array_equal(o, eo)
+        np.testing.assert_array_equal(ids, e)
+
+
+def test_tokenize_lane_path_matches_wave_path(ctxs, monkeypatch):
+    """The fallback (lane per sentence) kernel alone gives the same result as the wave kernel."""
+    from lddl_amd import synth
+    corp = synth.generate(seed=99, n_bytes=1 << 20, nonascii_frac=0.05)
+    a = ctxs['uncased'].tokenize_host(corp.text, corp.sent_off)
+    monkeypatch.setenv('LDDL_TOKENIZE_PATH', 'lane')
+    b = ctxs['uncased'].tokenize_host(corp.text, corp.sent_off)
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[0], b[0])

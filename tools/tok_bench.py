@@ -27,5 +27,7 @@ ev1.record()
 torch.cuda.synchronize()
 ms = ev0.elapsed_time(ev1) / n
 pieces = int((sl & ((1 << 30) - 1)).sum())
-print('tokenize: {:.3f} ms/iter, {:.2f} GB/s text, {:.3f} G pieces/s, pieces={}'.format(
-    ms, len(corp.text) / ms / 1e6, pieces / ms / 1e6, pieces), flush=True)
+import os
+fb = os.environ.get('LDDL_TOKENIZE_PATH', 'wave')
+print('[{}] tokenize: {:.3f} ms/iter, {:.2f} GB/s text, {:.3f} G pieces/s, pieces={}'.format(
+    fb, ms, len(corp.text) / ms / 1e6, pieces / ms / 1e6, pieces), flush=True)
