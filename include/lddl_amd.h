@@ -113,6 +113,43 @@ int lddl_pairs_emit(lddl_pairs* plan, void* stream, int32_t* d_tokens, int64_t* 
                     int32_t* d_len_a, uint8_t* d_is_rn, uint16_t* d_pos, int32_t* d_lab,
                     int64_t* d_pos_off);
 int lddl_pairs_destroy(lddl_pairs* plan, void* stream);
+/* d_part_pair_off[n_part + 1]: first output pair of each partition (pairs are emitted in
+ * partition order), i.e. the row ranges of the reference's per-partition outputs. */
+int lddl_pairs_part_offsets(lddl_pairs* plan, void* stream, int64_t* d_part_pair_off);
+
+/* ---------------------------------------------------------------------------------------------
+ * Per-partition sequence-length binning.
+ * Replaces _to_dataframe_binned (lddl/dask/bert/binning.py:63-93) applied per partition:
+ *   bin_id = min((num_tokens - 1) // bin_size, nbins - 1), rows regrouped by bin, stable.
+ * Rows of partition p are d_part_off[p] .. d_part_off[p+1]. Outputs (device): d_perm[r] = input
+ * row of output row r (partition order kept, bins ascending inside a partition), d_bin_id[r] its
+ * bin, d_counts[p * nbins + b] = rows of partition p in bin b. nbins <= 8192.
+ * ------------------------------------------------------------------------------------------- */
+int lddl_bin_partitions(lddl_ctx* ctx, void* stream, const int32_t* d_num_tokens, int64_t n_rows,
+                        const int64_t* d_part_off, int64_t n_part, int32_t bin_size, int32_t nbins,
+                        int64_t* d_perm, int64_t* d_bin_id, int64_t* d_counts);
+
+/* ---------------------------------------------------------------------------------------------
+ * Rendering of the parquet columns (lddl/dask/bert/pretrain.py:345-358):
+ *   A, B = ' '.join(tokens), masked_lm_labels = ' '.join(labels) (vocab strings of the ids),
+ *   masked_lm_positions = np.save bytes of uint16[k] (lddl/utils.py:98-102; 128 + 2k bytes).
+ * Output row r renders pair d_rows[r] (d_rows NULL = identity) of a lddl_pairs_emit table.
+ * lddl_render_lengths writes per-row byte lengths; the caller scans them (lddl_scan_i64) into
+ * offsets and calls lddl_render_write. Label / position arguments may be NULL (no masking).
+ * ------------------------------------------------------------------------------------------- */
+int lddl_render_lengths(lddl_ctx* ctx, void* stream, const int32_t* d_tokens,
+                        const int64_t* d_tok_off, const int32_t* d_len_a, const int32_t* d_lab,
+                        const int64_t* d_pos_off, const int64_t* d_rows, int64_t n_rows,
+                        int64_t* d_a_len, int64_t* d_b_len, int64_t* d_l_len, int64_t* d_npy_len);
+int lddl_render_write(lddl_ctx* ctx, void* stream, const int32_t* d_tokens,
+                      const int64_t* d_tok_off, const int32_t* d_len_a, const uint16_t* d_pos,
+                      const int32_t* d_lab, const int64_t* d_pos_off, const int64_t* d_rows,
+                      int64_t n_rows, const int64_t* d_a_off, const int64_t* d_b_off,
+                      const int64_t* d_l_off, const int64_t* d_npy_off, uint8_t* d_a_bytes,
+                      uint8_t* d_b_bytes, uint8_t* d_l_bytes, uint8_t* d_npy_bytes);
+
+/* Exclusive prefix sum: d_out[0..n] (d_out[n] = total) of d_in[0..n). */
+int lddl_scan_i64(void* stream, const int64_t* d_in, int64_t n, int64_t* d_out);
 
 /* ---------------------------------------------------------------------------------------------
  * Loader collate (lddl/torch/bert.py:69-149 `_to_encoded_inputs`), one batch, device in/out.

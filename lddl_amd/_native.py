@@ -29,6 +29,14 @@ SIGNATURES = {
                                        c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),
     'lddl_pairs_emit': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'lddl_pairs_destroy': (ctypes.c_int, [c_vp, c_vp]),
+    'lddl_pairs_part_offsets': (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    'lddl_bin_partitions': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp,
+                                           c_vp, c_vp]),
+    'lddl_render_lengths': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                           c_vp, c_vp, c_vp, c_vp]),
+    'lddl_render_write': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                         c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'lddl_scan_i64': (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),
     'lddl_collate_encode': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_i64]),

@@ -348,7 +348,7 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
 #ifdef LDDL_STAMPS
   uint64_t st_acc[kStampRegions] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-  uint64_t st_t = STAMP_T();
+  [[maybe_unused]] uint64_t st_t = STAMP_T();
   WaveRng rng{s_mt, s_tw, 0, 0, 0u};
   rng.seed_i64(A.part_seed[p]);
   const int64_t d0 = A.kp_off[p], nd = A.kp_off[p + 1] - d0;
@@ -697,6 +697,7 @@ struct lddl_pairs {
   int32_t *order = nullptr, *nmask = nullptr, *mtok = nullptr;
   uint16_t* mpos = nullptr;
   int64_t *src = nullptr, *tok_off = nullptr, *pos_off = nullptr;
+  int64_t* part_base = nullptr;  // [n_part + 1] first output pair of each partition
 
   template <typename T>
   int alloc(T** p, int64_t n, hipStream_t st) {
@@ -836,6 +837,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
 #endif
   // layout
   TRY(P->alloc(&part_base, n_part + 1, st));
+  P->part_base = part_base;
   if (scan_exclusive(Identity{part_npairs}, n_part, part_base, scratch, st) != hipSuccess) TRY(-100);
   LDDL_HIP(hipMemcpyAsync(&P->n_pairs, part_base + n_part, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
@@ -891,5 +893,12 @@ extern "C" int lddl_pairs_destroy(lddl_pairs* P, void* stream) {
   if (!P) return 0;
   P->release(as_stream(stream));
   delete P;
+  return 0;
+}
+
+extern "C" int lddl_pairs_part_offsets(lddl_pairs* P, void* stream, int64_t* d_part_pair_off) {
+  if (!P || !d_part_pair_off) LDDL_FAIL(-1, "null argument");
+  LDDL_HIP(hipMemcpyAsync(d_part_pair_off, P->part_base, 8 * (P->n_part + 1),
+                          hipMemcpyDeviceToDevice, as_stream(stream)));
   return 0;
 }

@@ -1,0 +1,118 @@
+"""Input side of the preprocessor: the reference's lddl/dask/readers.py semantics without Dask.
+
+* files: every `*.txt` under the source directory, sorted (readers.py:35-41); Wikipedia adds
+  `/<lang>` (readers.py:81-82);
+* blocks: `dask.bag.read_text(files, blocksize)` cuts each file into byte blocks of `blocksize`,
+  moved forward to the next line start (dask.bytes.read_block with delimiter b'\\n'); no
+  blocksize = one block per file; a block is one partition;
+* lines are `strip()`ed and empty ones dropped (readers.py:31-32);
+* `random_sample(sample_ratio, seed)` keeps a line iff random() < ratio, with the per-partition
+  MT states of dask 2021.10's `random_state_data_python` (624 words of randint(0, 2**32) each
+  drawn from Random(seed), in partition order).
+"""
+import os
+import random
+
+
+def find_files_under(path, extensions=('.txt',)):
+    out = []
+    for cur, _, names in os.walk(path):
+        for n in names:
+            if os.path.splitext(n)[1] in extensions:
+                out.append(os.path.join(cur, n))
+    return sorted(out)
+
+
+def total_bytes_of(files):
+    return sum(map(os.path.getsize, files))
+
+
+def estimate_block_size(paths, num_blocks):
+    """readers.py:48-57."""
+    total = sum(total_bytes_of(find_files_under(p)) for p in paths if p is not None)
+    print('total_bytes = {}, num_blocks = {}'.format(total, num_blocks))
+    bs = round(total / num_blocks)
+    print('block_size = {} bytes'.format(bs))
+    return bs
+
+
+def _block_starts(data, blocksize):
+    """Start offsets of dask read_block blocks of `data` (bytes)."""
+    n = len(data)
+    if not blocksize or n == 0:
+        return [0, n]
+    starts = [0]
+    for off in range(blocksize, n, blocksize):
+        j = data.find(b'\n', off - 1)
+        s = n if j < 0 else j + 1
+        starts.append(s)
+    starts.append(n)
+    return starts
+
+
+def read_blocks(files, blocksize=None):
+    """List of blocks; each block is a list of raw lines (bytes, without the delimiter)."""
+    blocks = []
+    for fn in files:
+        with open(fn, 'rb') as f:
+            data = f.read()
+        st = _block_starts(data, blocksize)
+        for a, b in zip(st[:-1], st[1:]):
+            if b <= a and len(st) > 2:
+                blocks.append([])
+                continue
+            blocks.append(data[a:b].split(b'\n'))
+    return blocks
+
+
+def random_state_data_python(n, seed):
+    r = random.Random(seed)
+    m = 1 << 32
+    return [(3, tuple(r.randint(0, m) for _ in range(624)) + (624,), None) for _ in range(n)]
+
+
+def _filter(block):
+    out = []
+    for raw in block:
+        s = raw.decode('utf-8').strip()
+        if s:
+            out.append(s)
+    return out
+
+
+def read_bag_of_text(path, blocksize=None, sample_ratio=1.0, sample_seed=12345):
+    """readers.py:60-71: partitions of stripped, non-empty lines, optionally sampled."""
+    blocks = [_filter(b) for b in read_blocks(find_files_under(path), blocksize)]
+    if sample_ratio < 1.0:
+        states = random_state_data_python(len(blocks), sample_seed)
+        out = []
+        for b, st in zip(blocks, states):
+            r = random.Random()
+            r.setstate(st)
+            out.append([x for x in b if r.random() < sample_ratio])
+        blocks = out
+    return blocks
+
+
+def read_wikipedia(path, lang='en', blocksize=None, sample_ratio=1.0, sample_seed=12345):
+    return read_bag_of_text(os.path.join(path, lang), blocksize, sample_ratio, sample_seed)
+
+
+def read_books(path, blocksize=None, sample_ratio=1.0, sample_seed=12345):
+    return read_bag_of_text(path, blocksize, sample_ratio, sample_seed)
+
+
+def read_common_crawl(path, blocksize=None, sample_ratio=1.0, sample_seed=12345):
+    return read_bag_of_text(path, blocksize, sample_ratio, sample_seed)
+
+
+def read_open_webtext(path, blocksize=None, sample_ratio=1.0, sample_seed=12345):
+    return read_bag_of_text(path, blocksize, sample_ratio, sample_seed)
+
+
+def split_id_text(raw_text):
+    """readers.py:131-136: id = chars up to the first whitespace char; text = the rest after it."""
+    i = 0
+    while i < len(raw_text) and not raw_text[i].isspace():
+        i += 1
+    return raw_text[:i], raw_text[i + 1:]

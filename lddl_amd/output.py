@@ -1,0 +1,192 @@
+"""Device-resident sample table -> the reference's parquet layout.
+
+Counterparts of the reference's output stage:
+  * `_to_dataframe_binned` (lddl/dask/bert/binning.py:63-93) -> `bin_partitions` (HIP kernel
+    lddl_bin_partitions: per-partition stable regroup by bin_id = min((n-1)//bin_size, nbins-1));
+  * the instance dict of `create_pairs_from_document` (lddl/dask/bert/pretrain.py:345-358) ->
+    `render` (HIP kernels lddl_render_lengths / lddl_render_write: ' '.join of vocab strings and
+    the np.save bytes of masked_lm_positions, lddl/utils.py:98-102);
+  * `_save_parquet` / `write_partition_binned` (pretrain.py:444-498, binning.py:353-431) ->
+    `write_parquet` (pyarrow, zero-copy Arrow arrays over the rendered buffers; file names
+    `part.<i>.parquet` or `part.<i>.parquet_<b>`, one file per (partition, bin) even if empty).
+
+Everything up to the host copy of the rendered bytes runs on the GPU; pyarrow only frames and
+writes the buffers.
+"""
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.parquet as pq
+import torch
+
+from ._native import lib, check
+from .context import _ptr, _stream
+
+try:  # the reference compresses with snappy iff python-snappy is importable (binning.py:42-47)
+    import snappy  # noqa: F401
+    DEFAULT_COMPRESSION = 'snappy'
+except ImportError:
+    DEFAULT_COMPRESSION = None
+
+
+def bin_partitions(ctx, num_tokens, part_off, bin_size, nbins):
+    """num_tokens: int32 cuda [n]; part_off: int64 cuda [n_part+1].
+    Returns (perm int64 [n], bin_id int64 [n], counts int64 [n_part, nbins]) on the device."""
+    n = num_tokens.numel()
+    n_part = part_off.numel() - 1
+    dev = num_tokens.device
+    perm = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
+    bin_id = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
+    counts = torch.zeros(max(n_part * nbins, 1), dtype=torch.int64, device=dev)[:n_part * nbins]
+    check(lib.lddl_bin_partitions(ctx.handle, _stream(), _ptr(num_tokens), n, _ptr(part_off),
+                                  n_part, bin_size, nbins, _ptr(perm), _ptr(bin_id), _ptr(counts)))
+    return perm, bin_id, counts.view(n_part, nbins)
+
+
+def _scan(x):
+    out = torch.empty(x.numel() + 1, dtype=torch.int64, device=x.device)
+    check(lib.lddl_scan_i64(_stream(), _ptr(x), x.numel(), _ptr(out)))
+    return out
+
+
+@dataclass
+class Rendered:
+    """Host buffers of the parquet columns of rows 0..n-1 (offsets are int64, global)."""
+    a_off: np.ndarray
+    a_bytes: np.ndarray
+    b_off: np.ndarray
+    b_bytes: np.ndarray
+    is_random_next: np.ndarray
+    num_tokens: np.ndarray
+    l_off: np.ndarray = None
+    l_bytes: np.ndarray = None
+    npy_off: np.ndarray = None
+    npy_bytes: np.ndarray = None
+    bin_id: np.ndarray = None
+
+    @property
+    def n(self):
+        return len(self.num_tokens)
+
+    def row(self, r):
+        """Python dict of row r, as the reference's instance (for tests / txt output)."""
+        d = {'A': bytes(self.a_bytes[self.a_off[r]:self.a_off[r + 1]]).decode('utf-8'),
+             'B': bytes(self.b_bytes[self.b_off[r]:self.b_off[r + 1]]).decode('utf-8'),
+             'is_random_next': bool(self.is_random_next[r]),
+             'num_tokens': int(self.num_tokens[r])}
+        if self.l_off is not None:
+            d['masked_lm_positions'] = bytes(self.npy_bytes[self.npy_off[r]:self.npy_off[r + 1]])
+            d['masked_lm_labels'] = bytes(self.l_bytes[self.l_off[r]:self.l_off[r + 1]]).decode(
+                'utf-8')
+        if self.bin_id is not None:
+            d['bin_id'] = int(self.bin_id[r])
+        return d
+
+
+def render(ctx, pb, rows=None, bin_id=None):
+    """Render the parquet columns of PairBatch `pb` for output rows `rows` (int64 cuda tensor of
+    pair indices, None = all pairs in order). Returns a host `Rendered`."""
+    dev = ctx.device
+    n = pb.n_pairs if rows is None else rows.numel()
+    masking = pb.pos is not None
+    st = _stream()
+    a_len = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
+    b_len = torch.empty_like(a_len)
+    l_len = torch.empty_like(a_len) if masking else None
+    npy_len = torch.empty_like(a_len) if masking else None
+    lab = pb.labels if masking else None
+    pos_off = pb.pos_off if masking else None
+    check(lib.lddl_render_lengths(ctx.handle, st, _ptr(pb.tokens), _ptr(pb.tok_off), _ptr(pb.len_a),
+                                  _ptr(lab), _ptr(pos_off), _ptr(rows), n, _ptr(a_len), _ptr(b_len),
+                                  _ptr(l_len), _ptr(npy_len)))
+    a_off, b_off = _scan(a_len), _scan(b_len)
+    l_off = _scan(l_len) if masking else None
+    npy_off = _scan(npy_len) if masking else None
+    tot = [int(x[-1].item()) if x is not None else 0 for x in (a_off, b_off, l_off, npy_off)]
+    bufs = [torch.empty(max(t, 1), dtype=torch.uint8, device=dev) for t in tot]
+    check(lib.lddl_render_write(ctx.handle, st, _ptr(pb.tokens), _ptr(pb.tok_off), _ptr(pb.len_a),
+                                _ptr(pb.pos) if masking else None, _ptr(lab), _ptr(pos_off),
+                                _ptr(rows), n, _ptr(a_off), _ptr(b_off), _ptr(l_off),
+                                _ptr(npy_off), _ptr(bufs[0]), _ptr(bufs[1]),
+                                _ptr(bufs[2]) if masking else None,
+                                _ptr(bufs[3]) if masking else None))
+    sel = (lambda x: x) if rows is None else (lambda x: x.index_select(0, rows))
+    num_tokens = sel((pb.tok_off[1:] - pb.tok_off[:-1]) + 3)
+    is_rn = sel(pb.is_random_next)
+
+    def host(t, k):
+        return t[:k].cpu().numpy()
+
+    out = Rendered(a_off.cpu().numpy(), host(bufs[0], tot[0]), b_off.cpu().numpy(),
+                   host(bufs[1], tot[1]), is_rn.cpu().numpy().astype(bool),
+                   num_tokens.cpu().numpy().astype(np.uint16))
+    if masking:
+        out.l_off, out.l_bytes = l_off.cpu().numpy(), host(bufs[2], tot[2])
+        out.npy_off, out.npy_bytes = npy_off.cpu().numpy(), host(bufs[3], tot[3])
+    if bin_id is not None:
+        out.bin_id = bin_id.cpu().numpy().astype(np.int64)
+    return out
+
+
+def schema(masking, binned):
+    """The reference's parquet schema (pretrain.py:450-468, + bin_id int64 when binned, 496)."""
+    fields = [('A', pa.string()), ('B', pa.string()), ('is_random_next', pa.bool_()),
+              ('num_tokens', pa.uint16())]
+    if masking:
+        fields += [('masked_lm_positions', pa.binary()), ('masked_lm_labels', pa.string())]
+    if binned:
+        fields.append(('bin_id', pa.int64()))
+    return pa.schema(fields)
+
+
+def _var(typ, off, data, r0, r1):
+    o = off[r0:r1 + 1]
+    b0, b1 = int(o[0]), int(o[-1])
+    if b1 - b0 >= (1 << 31):
+        raise ValueError('a parquet file would hold >= 2 GiB in one string column; use more '
+                         'partitions (--num-blocks / --block-size)')
+    rel = (o - b0).astype(np.int32)
+    return pa.Array.from_buffers(typ, r1 - r0, [None, pa.py_buffer(rel),
+                                                pa.py_buffer(data[b0:b1])])
+
+
+def table(rd, r0, r1, masking, binned):
+    cols = [_var(pa.string(), rd.a_off, rd.a_bytes, r0, r1),
+            _var(pa.string(), rd.b_off, rd.b_bytes, r0, r1),
+            pa.array(rd.is_random_next[r0:r1], pa.bool_()),
+            pa.array(rd.num_tokens[r0:r1], pa.uint16())]
+    if masking:
+        cols += [_var(pa.binary(), rd.npy_off, rd.npy_bytes, r0, r1),
+                 _var(pa.string(), rd.l_off, rd.l_bytes, r0, r1)]
+    if binned:
+        cols.append(pa.array(rd.bin_id[r0:r1], pa.int64()))
+    return pa.Table.from_arrays(cols, schema=schema(masking, binned))
+
+
+def write_parquet(outdir, rd, part_rows, part_index, masking, nbins=None, bin_counts=None,
+                  compression=DEFAULT_COMPRESSION):
+    """Write the reference's files for a group of partitions.
+
+    part_rows: int64 [n_part + 1] row ranges of the partitions inside `rd`; part_index: global
+    partition number of each (file name part.<i>.parquet); when binned, bin_counts[p, b] are the
+    rows of (p, b), laid out bin after bin inside the partition's range."""
+    paths = []
+    for p in range(len(part_rows) - 1):
+        r0, r1 = int(part_rows[p]), int(part_rows[p + 1])
+        name = os.path.join(outdir, 'part.{}.parquet'.format(part_index[p]))
+        if nbins is None:
+            pq.write_table(table(rd, r0, r1, masking, False), name, compression=compression)
+            paths.append(name)
+            continue
+        b0 = r0
+        for b in range(nbins):
+            b1 = b0 + int(bin_counts[p, b])
+            fn = '{}_{}'.format(name, b)
+            pq.write_table(table(rd, b0, b1, masking, True), fn, compression=compression)
+            paths.append(fn)
+            b0 = b1
+        assert b0 == r1
+    return paths

@@ -27,6 +27,7 @@ class PairBatch:
     pos_off: torch.Tensor = None
     n_kept_sentences: int = 0
     n_kept_documents: int = 0
+    part_off: torch.Tensor = None  # int64 [n_part + 1]: pair range of each partition
 
     @property
     def n_pairs(self):
@@ -42,6 +43,8 @@ class PairBatch:
                    len_a=self.len_a.cpu().numpy(),
                    is_random_next=self.is_random_next.cpu().numpy().astype(bool))
         out['num_tokens'] = np.diff(out['tok_off']) + 3
+        if self.part_off is not None:
+            out['part_off'] = self.part_off.cpu().numpy()
         if self.pos is not None:
             out['pos'] = self.pos.cpu().numpy().view(np.uint16)
             out['labels'] = self.labels.cpu().numpy()
@@ -81,7 +84,9 @@ def make_pairs(ctx, sent_off, ids, sent_len, doc_sent_off, part_doc_off, part_se
             pos_off = torch.empty(n_pairs + 1, dtype=torch.int64, device=dev)
         check(lib.lddl_pairs_emit(h, st, _ptr(tokens), _ptr(tok_off), _ptr(len_a), _ptr(is_rn),
                                   _ptr(pos), _ptr(labels), _ptr(pos_off)))
+        part_off = torch.empty(n_part + 1, dtype=torch.int64, device=dev)
+        check(lib.lddl_pairs_part_offsets(h, st, _ptr(part_off)))
     finally:
         lib.lddl_pairs_destroy(h, st)
     return PairBatch(tokens, tok_off, len_a, is_rn, pos, labels, pos_off, int(counts[3]),
-                     int(counts[4]))
+                     int(counts[4]), part_off)

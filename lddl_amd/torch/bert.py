@@ -1,21 +1,48 @@
-"""GPU collate for the BERT loader — counterparts of lddl/torch/bert.py:69-196.
+"""BERT pretraining loader — drop-in for lddl/torch/bert.py (`get_bert_pretrain_data_loader`,
+199-413) with the collate on the GPU.
 
 `_to_encoded_inputs` and `_mask_tokens` keep the reference's names, arguments and outputs, but
 run as HIP kernels (lddl_collate_encode / lddl_mask_dynamic) and return cuda tensors (the
 reference returns CPU tensors that the training loop then moves with `.to(device)`; on a cuda
 tensor that call is a no-op).
 
-HIP must not be initialised in forked DataLoader workers ("Fork + HIP"): these functions
-run in the process that owns the GPU; the loader's workers only decode parquet into raw samples.
+Process split (SURVEY §7 "Fork + HIP"): the reference runs the whole collate inside forked
+DataLoader workers. HIP must not be used there, so the workers only decode parquet record
+batches, run the shuffle buffer and pack each batch into flat numpy buffers (`_pack_batch`);
+the process that owns the GPU uploads the packed batch, runs the encode + masking kernels and
+then the user's extra collate_fn. Sample order, bin choice and epoch logic are the reference's.
 """
 import ctypes
 import io
+import logging
+import os
 
 import numpy as np
 import torch
 
 from .._native import lib, check
-from ..context import _ptr, _stream
+from ..context import Context, _ptr, _stream
+from ..utils import get_all_bin_ids, get_all_parquets_under, get_file_paths_for_bin_id
+from .dataloader import Binned, DataLoader
+from .datasets import ParquetDataset
+from .log import DatasetLogger
+from .utils import get_node_rank, get_nproc_per_node, get_rank
+
+
+def _decode_record_batch(b):
+    """lddl/torch/bert.py:42-54: (A, B, is_random_next[, masked_lm_positions, labels])."""
+    b = b.to_pydict()
+    if 'masked_lm_positions' in b:
+        assert 'masked_lm_labels' in b
+    cols = tuple(b[k] for k in ('A', 'B', 'is_random_next', 'masked_lm_positions',
+                                'masked_lm_labels') if k in b)
+    for s in zip(*cols):
+        yield s
+
+
+class BertPretrainDataset(ParquetDataset):
+    def _decode_record_batch(self, b):
+        return _decode_record_batch(b)
 
 
 def _npy_u16(b):
@@ -60,39 +87,9 @@ def _dev(a, device):
 
 def _to_encoded_inputs(batch, tokenizer, sequence_length_alignment=8, ignore_index=-1):
     """lddl/torch/bert.py:69-149. `tokenizer` is a lddl_amd.context.Context."""
-    ctx = tokenizer
-    dev = ctx.device
-    B = len(batch)
-    static = len(batch[0]) > 3
-    if static:
+    if len(batch[0]) > 3:
         assert len(batch[0]) == 5
-    blob, a_off, b_off, na, nb, extra = _pack(batch, static)
-    seq = int((na + nb).max()) + 3
-    L = ((seq - 1) // sequence_length_alignment + 1) * sequence_length_alignment
-    d_blob = _dev(blob, dev) if len(blob) else torch.zeros(1, dtype=torch.uint8, device=dev)
-    d_a, d_b, d_na, d_nb = (_dev(x, dev) for x in (a_off, b_off, na, nb))
-    out = {k: torch.empty(B, L, dtype=torch.long, device=dev)
-           for k in ('input_ids', 'token_type_ids', 'attention_mask')}
-    stm = labels = d_lab_off = d_pos = d_pos_off = None
-    if static:
-        lab_off, pos, pos_off = extra
-        d_lab_off, d_pos_off = _dev(lab_off, dev), _dev(pos_off, dev)
-        d_pos = _dev(pos.view(np.int16), dev) if len(pos) else torch.zeros(1, dtype=torch.int16,
-                                                                           device=dev)
-        labels = torch.empty(B, L, dtype=torch.long, device=dev)
-    else:
-        stm = torch.empty(B, L, dtype=torch.long, device=dev)
-    check(lib.lddl_collate_encode(ctx.handle, _stream(), _ptr(d_blob), _ptr(d_a), _ptr(d_b),
-                                  _ptr(d_na), _ptr(d_nb), B, L, _ptr(out['input_ids']),
-                                  _ptr(out['token_type_ids']), _ptr(out['attention_mask']),
-                                  _ptr(stm), _ptr(d_blob) if static else None, _ptr(d_lab_off),
-                                  _ptr(d_pos), _ptr(d_pos_off), _ptr(labels), ignore_index))
-    out['next_sentence_labels'] = torch.as_tensor([s[2] for s in batch], dtype=torch.long).to(dev)
-    if static:
-        out['labels'] = labels
-    else:
-        out['special_tokens_mask'] = stm
-    return out
+    return encode_packed(PackedBatch(batch), tokenizer, sequence_length_alignment, ignore_index)
 
 
 def _mask_tokens(inputs, special_tokens_mask=None, tokenizer=None, mlm_probability=0.15,
@@ -121,3 +118,158 @@ def _mask_tokens(inputs, special_tokens_mask=None, tokenizer=None, mlm_probabili
                                 None, B, L, float(mlm_probability), ignore_index, len(ctx), seed,
                                 counter, *[_ptr(x) for x in r]))
     return inputs, labels
+
+
+class PackedBatch:
+    """A collated batch as flat host buffers (built in a DataLoader worker, picklable)."""
+
+    def __init__(self, batch):
+        self.static = len(batch[0]) > 3
+        self.blob, self.a_off, self.b_off, self.na, self.nb, self.extra = _pack(batch, self.static)
+        self.nsl = np.asarray([s[2] for s in batch], np.int64)
+
+    def __len__(self):
+        return len(self.nsl)
+
+
+def _pack_batch(batch):
+    return PackedBatch(batch)
+
+
+def encode_packed(pk, ctx, sequence_length_alignment=8, ignore_index=-1):
+    """`_to_encoded_inputs` on an already packed batch (main process, GPU)."""
+    dev = ctx.device
+    B = len(pk)
+    seq = int((pk.na + pk.nb).max()) + 3
+    L = ((seq - 1) // sequence_length_alignment + 1) * sequence_length_alignment
+    d_blob = _dev(pk.blob, dev) if len(pk.blob) else torch.zeros(1, dtype=torch.uint8, device=dev)
+    d_a, d_b, d_na, d_nb = (_dev(x, dev) for x in (pk.a_off, pk.b_off, pk.na, pk.nb))
+    out = {k: torch.empty(B, L, dtype=torch.long, device=dev)
+           for k in ('input_ids', 'token_type_ids', 'attention_mask')}
+    stm = labels = d_lab_off = d_pos = d_pos_off = None
+    if pk.static:
+        lab_off, pos, pos_off = pk.extra
+        d_lab_off, d_pos_off = _dev(lab_off, dev), _dev(pos_off, dev)
+        d_pos = _dev(pos.view(np.int16), dev) if len(pos) else torch.zeros(1, dtype=torch.int16,
+                                                                           device=dev)
+        labels = torch.empty(B, L, dtype=torch.long, device=dev)
+    else:
+        stm = torch.empty(B, L, dtype=torch.long, device=dev)
+    check(lib.lddl_collate_encode(ctx.handle, _stream(), _ptr(d_blob), _ptr(d_a), _ptr(d_b),
+                                  _ptr(d_na), _ptr(d_nb), B, L, _ptr(out['input_ids']),
+                                  _ptr(out['token_type_ids']), _ptr(out['attention_mask']),
+                                  _ptr(stm), _ptr(d_blob) if pk.static else None, _ptr(d_lab_off),
+                                  _ptr(d_pos), _ptr(d_pos_off), _ptr(labels), ignore_index))
+    out['next_sentence_labels'] = _dev(pk.nsl, dev)
+    if pk.static:
+        out['labels'] = labels
+    else:
+        out['special_tokens_mask'] = stm
+    return out
+
+
+class GPUCollateLoader:
+    """Iterates a torch DataLoader of PackedBatch and finishes the collate on the GPU."""
+
+    def __init__(self, loader, ctx, mlm_probability, ignore_index, sequence_length_alignment,
+                 extra_collate, seed):
+        self._loader = loader
+        self._ctx = ctx
+        self._mlm = mlm_probability
+        self._ignore = ignore_index
+        self._align = sequence_length_alignment
+        self._extra = extra_collate
+        self._seed = seed
+        self._counter = 0
+
+    @property
+    def dataset(self):
+        return self._loader.dataset
+
+    def __len__(self):
+        return len(self._loader)
+
+    def __getattr__(self, k):
+        return getattr(self._loader, k)
+
+    def __iter__(self):
+        for pk in self._loader:
+            with torch.no_grad():
+                enc = encode_packed(pk, self._ctx, self._align, self._ignore)
+                if 'special_tokens_mask' in enc:  # dynamic masking
+                    stm = enc.pop('special_tokens_mask')
+                    enc['input_ids'], enc['labels'] = _mask_tokens(
+                        enc['input_ids'], special_tokens_mask=stm, tokenizer=self._ctx,
+                        mlm_probability=self._mlm, ignore_index=self._ignore, seed=self._seed,
+                        counter=self._counter)
+                    self._counter += 1
+            yield self._extra(enc)
+
+
+class BertPretrainBinned(Binned):
+    def _get_batch_size(self, batch):
+        if isinstance(batch, dict):
+            return batch['input_ids'].size(0)
+        return len(batch[0]) if isinstance(batch, (list, tuple)) else len(batch)
+
+
+def get_bert_pretrain_data_loader(path, local_rank=0, shuffle_buffer_size=16384,
+                                  shuffle_buffer_warmup_factor=16, tokenizer_class=None,
+                                  vocab_file=None, tokenizer_kwargs={}, data_loader_class=DataLoader,
+                                  data_loader_kwargs={}, mlm_probability=0.15, base_seed=12345,
+                                  log_dir=None, log_level=logging.INFO, return_raw_samples=False,
+                                  start_epoch=0, sequence_length_alignment=8, ignore_index=-1):
+    """Same signature, arguments and yielded dicts as lddl.torch.get_bert_pretrain_data_loader
+    (lddl/torch/bert.py:199-413); the tensors are on the current cuda device.
+
+    tokenizer_class is accepted for compatibility (BertTokenizerFast / BertTokenizer or None):
+    the vocab file is loaded into a lddl_amd Context (vocab hash in HBM). vocab_file must be a
+    local path (no model-name download offline)."""
+    assert isinstance(path, str)
+    assert isinstance(local_rank, int) and local_rank >= 0
+    assert isinstance(shuffle_buffer_size, int) and shuffle_buffer_size > 0
+    assert isinstance(shuffle_buffer_warmup_factor, int) and shuffle_buffer_warmup_factor > 0
+    if tokenizer_class is not None:
+        assert getattr(tokenizer_class, '__name__', '') in {'BertTokenizerFast', 'BertTokenizer'}
+    assert isinstance(vocab_file, str)
+    assert isinstance(tokenizer_kwargs, dict)
+    assert data_loader_class in {DataLoader}
+    assert isinstance(data_loader_kwargs, dict)
+    assert isinstance(mlm_probability, (int, float)) and 0 <= mlm_probability <= 1
+    assert isinstance(base_seed, int)
+    assert log_dir is None or isinstance(log_dir, str)
+    assert log_level in {logging.NOTSET, logging.DEBUG, logging.INFO, logging.WARNING,
+                         logging.ERROR, logging.CRITICAL}
+    assert isinstance(return_raw_samples, bool)
+    assert isinstance(start_epoch, int)
+    if not os.path.isfile(vocab_file):
+        raise FileNotFoundError('vocab_file {!r}: a local vocab.txt is required (offline)'.format(
+            vocab_file))
+    data_loader_kwargs = dict(data_loader_kwargs)
+    logger = DatasetLogger(log_dir=log_dir,
+                           node_rank=get_node_rank(nproc_per_node=get_nproc_per_node(local_rank)),
+                           local_rank=local_rank, log_level=log_level)
+    dataset_kwargs = dict(local_rank=local_rank, shuffle_buffer_size=shuffle_buffer_size,
+                          shuffle_buffer_warmup_factor=shuffle_buffer_warmup_factor,
+                          base_seed=base_seed, logger=logger, start_epoch=start_epoch)
+    extra_collate = data_loader_kwargs.get('collate_fn', lambda x: x)
+    ctx = None
+    if not return_raw_samples:
+        ctx = Context(vocab_file, do_lower_case=tokenizer_kwargs.get('do_lower_case', True))
+        data_loader_kwargs['collate_fn'] = _pack_batch
+    data_loader_kwargs['persistent_workers'] = True
+
+    def make(paths):
+        dl = data_loader_class(BertPretrainDataset(paths, **dataset_kwargs), **data_loader_kwargs)
+        if return_raw_samples:
+            return dl
+        return GPUCollateLoader(dl, ctx, mlm_probability, ignore_index,
+                                sequence_length_alignment, extra_collate,
+                                base_seed * 1000003 + get_rank())
+
+    paths = get_all_parquets_under(path)
+    bin_ids = get_all_bin_ids(paths)
+    if bin_ids:
+        return BertPretrainBinned([make(get_file_paths_for_bin_id(paths, b)) for b in bin_ids],
+                                  base_seed=base_seed, start_epoch=start_epoch, logger=logger)
+    return make(paths)

@@ -1,0 +1,104 @@
+"""Host-side pieces that need no GPU: readers, layout utils, sentence segmentation fallback,
+CLI flag parity."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from lddl_amd import utils as U
+from lddl_amd.dask import readers as R
+
+
+def test_parse_str_of_num_bytes():
+    assert U.parse_str_of_num_bytes('1k') == 1024
+    assert U.parse_str_of_num_bytes('1.5M') == int(1.5 * 1024 ** 2)
+    assert U.parse_str_of_num_bytes('2g') == 2 * 1024 ** 3
+    assert U.parse_str_of_num_bytes('1024') == 102  # reference quirk kept
+    assert U.parse_str_of_num_bytes('8K', return_str=True) == '8K'
+    with pytest.raises(ValueError):
+        U.parse_str_of_num_bytes('xk')
+
+
+def test_bin_ids_and_paths():
+    paths = ['/a/part.0.parquet_0', '/a/part.0.parquet_1', '/a/part.1.parquet_1']
+    assert U.get_all_bin_ids(paths) == [0, 1]
+    assert U.get_file_paths_for_bin_id(paths, 1) == paths[1:]
+    with pytest.raises(ValueError):
+        U.get_all_bin_ids(['/a/part.0.parquet_1'])
+    assert U.get_all_bin_ids(['/a/part.0.parquet']) == []
+
+
+def test_serialize_np_array_roundtrip():
+    a = np.asarray([3, 1, 4, 159], np.uint16)
+    b = U.serialize_np_array(a)
+    assert len(b) == 128 + 8
+    np.testing.assert_array_equal(U.deserialize_np_array(b), a)
+
+
+def test_split_id_text():
+    assert R.split_id_text('wiki-1 hello world') == ('wiki-1', 'hello world')
+    assert R.split_id_text('wiki-2\tx') == ('wiki-2', 'x')
+    assert R.split_id_text('alone') == ('alone', '')
+
+
+def test_blocks_follow_dask_read_block(tmp_path):
+    data = b''.join(b'line%03d xx\n' % i for i in range(50))
+    f = tmp_path / 'a.txt'
+    f.write_bytes(data)
+    for bs in (7, 12, 13, 64, 1000):
+        blocks = R.read_blocks([str(f)], bs)
+        lines = [l for b in blocks for l in b if l]
+        assert lines == data.split(b'\n')[:-1]
+        # dask: block k (k > 0) starts after the first newline at or after offset k*bs - 1
+        starts = R._block_starts(data, bs)
+        for k, s in enumerate(starts[1:-1], 1):
+            j = data.find(b'\n', k * bs - 1)
+            assert s == j + 1
+
+
+def test_random_sample_is_dask_semantics(tmp_path):
+    d = tmp_path / 'src'
+    d.mkdir()
+    (d / 'x.txt').write_text(''.join('doc{} text\n'.format(i) for i in range(200)))
+    a = R.read_bag_of_text(str(d), None, 0.5, 42)
+    b = R.read_bag_of_text(str(d), None, 0.5, 42)
+    assert a == b and 60 < len(a[0]) < 140
+    # partition 0 state: 624 words of randint(0, 2**32) from Random(42), then random() < p
+    r0 = random.Random(42)
+    st = (3, tuple(r0.randint(0, 1 << 32) for _ in range(624)) + (624,), None)
+    r = random.Random()
+    r.setstate(st)
+    assert a[0] == ['doc{} text'.format(i) for i in range(200) if r.random() < 0.5]
+
+
+def test_rule_sentence_splitter():
+    from lddl_amd.dask.bert import segment as S
+    out = S._rule_split('One here. Two is J. Smith! Three... still three? Four.')
+    assert [s.strip() for s in out] == ['One here.', 'Two is J. Smith!',
+                                         'Three... still three?', 'Four.']
+
+
+def test_pretrain_flags_match_reference_surface():
+    from lddl_amd.dask.bert import pretrain as P
+    ap = P.attach_args()
+    flags = {a for act in ap._actions for a in act.option_strings}
+    want = {'--schedule', '--local-n-workers', '--local-threads-per-worker', '--wikipedia',
+            '--books', '--common-crawl', '--sink', '--output-format', '--wikipedia-lang',
+            '--target-seq-length', '--short-seq-prob', '--block-size', '--num-blocks',
+            '--bin-size', '--sample-ratio', '--seed', '--duplicate-factor', '--vocab-file',
+            '--masking', '--no-masking', '--masked-lm-ratio'}
+    assert want <= flags
+    a = ap.parse_args(['--sink', '/tmp/x'])
+    assert (a.target_seq_length, a.short_seq_prob, a.sample_ratio, a.seed, a.duplicate_factor,
+            a.masking, a.masked_lm_ratio, a.output_format) == (128, 0.1, 0.9, 12345, 5, False,
+                                                               0.15, 'parquet')
+    with pytest.raises(ValueError):
+        P.main(ap.parse_args(['--sink', '/tmp/x', '--bin-size', '48']))
+
+
+def test_load_balance_flags():
+    from lddl_amd.dask import load_balance as LB
+    a = LB.attach_args().parse_args(['--indir', 'x', '--num-shards', '4', '--bin-ids', '0', '2'])
+    assert (a.indir, a.outdir, a.num_shards, a.bin_ids, a.keep_orig) == ('x', None, 4, [0, 2],
+                                                                          False)

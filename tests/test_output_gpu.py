@@ -1,0 +1,156 @@
+"""Output stage on the GPU: per-partition binning (vs the reference's _to_dataframe_binned
+goldens and the oracle), string/npy rendering (vs Python ' '.join / np.save) and the
+`preprocess_bert_pretrain` CLI end to end (parquet files vs the oracle replay)."""
+import io
+import json
+import os
+
+import numpy as np
+import pyarrow.parquet as pq
+import pytest
+
+from conftest import GOLDEN, VOCAB_UNCASED
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    from lddl_amd.context import Context
+    return Context(VOCAB_UNCASED, True)
+
+
+def test_bin_golden(ctx):
+    import torch
+    from lddl_amd.output import bin_partitions
+    with open(os.path.join(GOLDEN, 'binning.json')) as f:
+        cases = json.load(f)
+    for c in cases:
+        nt = np.asarray(c['num_tokens'], np.int32)
+        nbins = c['seq'] // c['bin_size']
+        d_nt = torch.from_numpy(nt).cuda()
+        off = torch.tensor([0, len(nt)], dtype=torch.int64).cuda()
+        perm, bin_id, counts = bin_partitions(ctx, d_nt, off, c['bin_size'], nbins)
+        assert perm.cpu().tolist() == c['uid_order']
+        assert bin_id.cpu().tolist() == c['bin_id']
+        assert counts.cpu().numpy().sum() == len(nt)
+
+
+def test_bin_many_partitions_vs_oracle(ctx):
+    import torch
+    from oracle import oracle as O
+    from lddl_amd.output import bin_partitions
+    rng = np.random.default_rng(3)
+    sizes = rng.integers(0, 3000, 40)
+    sizes[5] = 0
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    for seq, bs in ((512, 8), (128, 32), (512, 1)):
+        nb = seq // bs
+        nt = rng.integers(5, seq + 1, off[-1]).astype(np.int32)
+        perm, bin_id, counts = bin_partitions(ctx, torch.from_numpy(nt).cuda(),
+                                              torch.from_numpy(off).cuda(), bs, nb)
+        perm, bin_id, counts = perm.cpu().numpy(), bin_id.cpu().numpy(), counts.cpu().numpy()
+        for p in range(len(sizes)):
+            a, z = off[p], off[p + 1]
+            eb, eo, ec = O.bin_samples(nt[a:z], bs, nb)
+            np.testing.assert_array_equal(perm[a:z] - a, eo)
+            np.testing.assert_array_equal(bin_id[a:z], eb[eo])
+            np.testing.assert_array_equal(counts[p], ec)
+
+
+def _py_rows(pairs, vocab, order=None):
+    """The reference's instance dicts (pretrain.py:345-358) from oracle/GPU pair arrays."""
+    rows = []
+    n = len(pairs['len_a'])
+    for q in (range(n) if order is None else order):
+        t = pairs['tokens'][pairs['tok_off'][q]:pairs['tok_off'][q + 1]]
+        na = pairs['len_a'][q]
+        d = {'A': ' '.join(vocab[i] for i in t[:na]), 'B': ' '.join(vocab[i] for i in t[na:]),
+             'is_random_next': bool(pairs['is_random_next'][q]),
+             'num_tokens': int(len(t) + 3)}
+        if 'pos' in pairs:
+            p0, p1 = pairs['pos_off'][q], pairs['pos_off'][q + 1]
+            buf = io.BytesIO()
+            np.save(buf, np.asarray(pairs['pos'][p0:p1], np.uint16))
+            d['masked_lm_positions'] = buf.getvalue()
+            d['masked_lm_labels'] = ' '.join(vocab[i] for i in pairs['labels'][p0:p1])
+        rows.append(d)
+    return rows
+
+
+def test_render_matches_python(ctx):
+    import torch
+    from lddl_amd import synth
+    from lddl_amd.pairs import make_pairs
+    from lddl_amd.output import render
+    corp = synth.generate(seed=5, n_bytes=200_000, nonascii_frac=0.05)
+    text = torch.from_numpy(corp.text).cuda()
+    so = torch.from_numpy(corp.sent_off).cuda()
+    ids, sl = ctx.tokenize(text, so)
+    part = torch.tensor([0, corp.n_doc], dtype=torch.int64).cuda()
+    for masking in (True, False):
+        pb = make_pairs(ctx, so, ids, sl, torch.from_numpy(corp.doc_sent_off).cuda(), part,
+                        torch.tensor([9], dtype=torch.int64).cuda(), seq=128, dup=2,
+                        masking=masking)
+        h = pb.to_host()
+        order = np.random.default_rng(1).permutation(pb.n_pairs)
+        rd = render(ctx, pb, torch.from_numpy(order).cuda())
+        exp = _py_rows(h, ctx.tokens, order)
+        for r in range(0, pb.n_pairs, 7):
+            assert rd.row(r) == exp[r]
+
+
+def _write_source(root, n_docs=300, seed=11):
+    from lddl_amd import synth
+    corp = synth.generate(seed=seed, n_bytes=n_docs * 3000, nonascii_frac=0.02)
+    docs = corp.documents()
+    os.makedirs(os.path.join(root, 'en'))
+    lines = ['wiki-{} {}'.format(i, ' '.join(d)) for i, d in enumerate(docs)]
+    half = len(lines) // 2
+    for k, chunk in enumerate((lines[:half], lines[half:])):
+        with open(os.path.join(root, 'en', 'wiki_{}.txt'.format(k)), 'w') as f:
+            f.write('\n'.join(chunk) + '\n\n')
+
+
+@pytest.mark.parametrize('binned', [False, True])
+def test_pretrain_cli_vs_oracle(tmp_path, binned):
+    from lddl_amd.dask.bert import pretrain as P
+    from oracle import oracle as O
+    src = tmp_path / 'source'
+    _write_source(str(src))
+    sink = tmp_path / 'out'
+    argv = ['--schedule', 'local', '--wikipedia', str(src), '--sink', str(sink), '--masking',
+            '--target-seq-length', '128', '--num-blocks', '4', '--seed', '7',
+            '--vocab-file', VOCAB_UNCASED, '--local-n-workers', '1', '--duplicate-factor', '2']
+    if binned:
+        argv += ['--bin-size', '32']
+    args = P.attach_args().parse_args(argv)
+    P.main(args)
+    # CPU replay: the same host partitions, the oracle tokenizer + pair/mask replay
+    args = P.attach_args().parse_args(argv)
+    parts = P.get_partitions(args)
+    tok = O.Tokenizer(VOCAB_UNCASED, lowercase=True)
+    vocab = [l.rstrip('\n') for l in open(VOCAB_UNCASED, encoding='utf-8')]
+    cls, sep, msk = (tok.token_id(t) for t in ('[CLS]', '[SEP]', '[MASK]'))
+    for p, lines in parts:
+        text, so, dso, pdo = P.build_corpus([(p, lines)])
+        ids, off = tok.tokenize(text, so)
+        lens = np.diff(off)
+        keep = lens > 0
+        kpos = np.concatenate([[0], np.cumsum(keep)])
+        kd = kpos[dso]
+        kd = np.concatenate([kd[:1], kd[1:][np.diff(kd) > 0]])
+        k_off = np.concatenate([[0], np.cumsum(lens[keep])])
+        out = O.partition_pairs(kd, k_off, ids, P.partition_seed(7, p), 2, 128, True,
+                                tok.vocab_size, cls, sep, msk)
+        rows = _py_rows(out, vocab)
+        if not binned:
+            t = pq.read_table(sink / 'part.{}.parquet'.format(p)).to_pylist()
+            assert t == rows
+        else:
+            nt = np.asarray([r['num_tokens'] for r in rows])
+            bins = np.minimum((nt - 1) // 32, 3)
+            for b in range(4):
+                t = pq.read_table(sink / 'part.{}.parquet_{}'.format(p, b)).to_pylist()
+                exp = [dict(r, bin_id=b) for r, bb in zip(rows, bins) if bb == b]
+                assert t == exp
