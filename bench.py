@@ -1,5 +1,8 @@
 """Benchmark of the hot path on BASELINE.json's metric config (configs[1], "C2"):
 synthetic English-like corpus, seq 128, static masking, no binning, on MI355X.
+`--workload c4` runs configs[2]/[3] instead (seq 512 phase 2, static masking, 64 bins of 8
+tokens, HBM load balance: at N > 1 an RCCL all-gather of per-bin counts and an all-to-all-v
+sample exchange over xGMI, lddl_amd/balance.py).
 
 One step = one pass of the hot path over one batch of synthetic input already resident in HBM:
 WordPiece tokenization of the batch's (Punkt-segmented) sentences, then NSP pair construction with
@@ -90,12 +93,15 @@ def main():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--batch-bytes', type=int, default=4 << 30)
     ap.add_argument('--partition-bytes', type=int, default=1 << 20)
-    ap.add_argument('--seq', type=int, default=128)
+    ap.add_argument('--seq', type=int, default=None)
+    ap.add_argument('--workload', choices=['c2', 'c4'], default='c2')
     ap.add_argument('--seed', type=int, default=1234)
     ap.add_argument('--gen-threads', type=int, default=16)
     ap.add_argument('--cpu-sample-bytes', type=int, default=48 << 20)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
+    if args.seq is None:
+        args.seq = 128 if args.workload == 'c2' else 512
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -105,6 +111,7 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     from lddl_amd.context import Context
     from lddl_amd.pairs import make_pairs
+    from lddl_amd.balance import balance
 
     corp, part, seeds = make_batch(rank, args)
     ctx = Context(VOCAB, do_lower_case=True)
@@ -123,9 +130,13 @@ def main():
             ev[1].record()
         pb = make_pairs(ctx, sent_off, ids, sent_len, doc_off, part_off, part_seed, seq=args.seq,
                         dup=5, masking=True, short_seq_prob=0.1, masked_lm_ratio=0.15)
+        if args.workload == 'c4':
+            bb = balance(ctx, pb, 8, args.seq // 8)
+            n_tok = int(bb.tokens.numel()) + 3 * bb.n_rows
+        else:
+            n_tok = int(pb.tokens.numel()) + 3 * pb.n_pairs
         if ev is not None:
             ev[2].record()
-        n_tok = int(pb.tokens.numel()) + 3 * pb.n_pairs
         return n_tok, pb, sent_len
 
     for _ in range(args.warmup):
@@ -189,17 +200,23 @@ def main():
         'dtype': 'int32',
         'data': 'synthetic',
         'config': {
-            'workload': 'C2: synthetic English-like corpus (SURVEY 8d generator, seed {}), '
-                        'seq 128, static masking, duplicate_factor 5, no binning; {} MiB of '
-                        'sentence text per GPU per step, {} KiB partitions'.format(
-                            args.seed, args.batch_bytes >> 20, args.partition_bytes >> 10),
+            'workload': ('C2: synthetic English-like corpus (SURVEY 8d generator, seed {}), '
+                         'seq {}, static masking, duplicate_factor 5, no binning; {} MiB of '
+                         'sentence text per GPU per step, {} KiB partitions' if args.workload == 'c2'
+                         else 'C3/C4: synthetic English-like corpus (SURVEY 8d generator, seed {}), '
+                         'seq {} phase 2, static masking, duplicate_factor 5, 64 bins of 8 tokens + '
+                         'HBM load balance (RCCL count all-gather + all-to-all-v exchange when N > 1)'
+                         '; {} MiB of sentence text per GPU per step, {} KiB partitions').format(
+                             args.seed, args.seq, args.batch_bytes >> 20, args.partition_bytes >> 10),
             'seq_len': args.seq, 'masking': 'static', 'duplicate_factor': 5,
             'rng': 'replay (CPython MT19937, random.seed per partition)',
             'batch_bytes': int(n_bytes), 'sentences': int(n_sent), 'documents': int(corp.n_doc),
             'partitions': int(len(part) - 1), 'wordpieces': pieces, 'pairs': int(pb.n_pairs),
             'vocab': os.path.basename(VOCAB), 'parallelism': 'dp{} (document shards)'.format(world),
         },
-        'stages_ms': {'tokenize': tok_ms, 'pairs_plan_and_gather': pair_ms},
+        'stages_ms': {'tokenize': tok_ms,
+                      ('pairs_plan_and_gather' if args.workload == 'c2' else
+                       'pairs_bin_and_balance'): pair_ms},
         'roofline': {'kernel': 'tokenize_wave_kernel', 'bound': 'hbm', 'achieved': achieved,
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                      'traffic': prof_traffic, 'algorithmic_bytes_per_launch': tok_bytes},

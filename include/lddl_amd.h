@@ -148,6 +148,12 @@ int lddl_render_write(lddl_ctx* ctx, void* stream, const int32_t* d_tokens,
                       const int64_t* d_l_off, const int64_t* d_npy_off, uint8_t* d_a_bytes,
                       uint8_t* d_b_bytes, uint8_t* d_l_bytes, uint8_t* d_npy_bytes);
 
+/* Ragged row gather (packing of the load-balance sample exchange): output row i is source row
+ * d_rows[i] (NULL = i), elements d_src[d_src_off[r] .. d_src_off[r+1]) copied to
+ * d_dst[d_dst_off[i] ...]. elem_bytes in {1, 2, 4, 8}; offsets count elements. */
+int lddl_gather_ragged(void* stream, const void* d_src, const int64_t* d_src_off, int32_t elem_bytes,
+                       const int64_t* d_rows, int64_t n_rows, const int64_t* d_dst_off, void* d_dst);
+
 /* Exclusive prefix sum: d_out[0..n] (d_out[n] = total) of d_in[0..n). */
 int lddl_scan_i64(void* stream, const int64_t* d_in, int64_t n, int64_t* d_out);
 

@@ -37,6 +37,7 @@ SIGNATURES = {
     'lddl_render_write': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                          c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'lddl_scan_i64': (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),
+    'lddl_gather_ragged': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp]),
     'lddl_collate_encode': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_i64]),

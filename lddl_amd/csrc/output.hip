@@ -213,10 +213,56 @@ __global__ void __launch_bounds__(256) render_write_kernel(RenderArgs R, const i
   }
 }
 
+// ---- ragged row gather (sample exchange packing) ---------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) gather_ragged_kernel(const T* __restrict__ src,
+                                                            const int64_t* __restrict__ src_off,
+                                                            const int64_t* __restrict__ rows,
+                                                            int64_t n_rows,
+                                                            const int64_t* __restrict__ dst_off,
+                                                            T* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n_rows) return;
+  const int64_t r = rows ? rows[i] : i;
+  const int64_t a = src_off[r], n = src_off[r + 1] - a, o = dst_off[i];
+  for (int64_t j = lane_id(); j < n; j += 64) dst[o + j] = src[a + j];
+}
+
 }  // namespace
 }  // namespace lddl
 
 using namespace lddl;
+
+extern "C" int lddl_gather_ragged(void* stream, const void* d_src, const int64_t* d_src_off,
+                                  int32_t elem_bytes, const int64_t* d_rows, int64_t n_rows,
+                                  const int64_t* d_dst_off, void* d_dst) {
+  if (n_rows < 0) LDDL_FAIL(-1, "bad size");
+  if (n_rows == 0) return 0;
+  const dim3 grid((unsigned)((n_rows + 3) / 4)), block(256);
+  hipStream_t st = as_stream(stream);
+  switch (elem_bytes) {
+    case 1:
+      hipLaunchKernelGGL(gather_ragged_kernel<uint8_t>, grid, block, 0, st,
+                         (const uint8_t*)d_src, d_src_off, d_rows, n_rows, d_dst_off, (uint8_t*)d_dst);
+      break;
+    case 2:
+      hipLaunchKernelGGL(gather_ragged_kernel<uint16_t>, grid, block, 0, st,
+                         (const uint16_t*)d_src, d_src_off, d_rows, n_rows, d_dst_off, (uint16_t*)d_dst);
+      break;
+    case 4:
+      hipLaunchKernelGGL(gather_ragged_kernel<uint32_t>, grid, block, 0, st,
+                         (const uint32_t*)d_src, d_src_off, d_rows, n_rows, d_dst_off, (uint32_t*)d_dst);
+      break;
+    case 8:
+      hipLaunchKernelGGL(gather_ragged_kernel<uint64_t>, grid, block, 0, st,
+                         (const uint64_t*)d_src, d_src_off, d_rows, n_rows, d_dst_off, (uint64_t*)d_dst);
+      break;
+    default:
+      LDDL_FAIL(-1, "elem_bytes %d unsupported", elem_bytes);
+  }
+  LDDL_HIP(hipGetLastError());
+  return 0;
+}
 
 extern "C" int lddl_bin_partitions(lddl_ctx* c, void* stream, const int32_t* d_num_tokens,
                                    int64_t n_rows, const int64_t* d_part_off, int64_t n_part,
