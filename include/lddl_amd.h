@@ -129,6 +129,12 @@ int lddl_bin_partitions(lddl_ctx* ctx, void* stream, const int32_t* d_num_tokens
                         const int64_t* d_part_off, int64_t n_part, int32_t bin_size, int32_t nbins,
                         int64_t* d_perm, int64_t* d_bin_id, int64_t* d_counts);
 
+/* The same regroup for ONE large segment (all rows of a rank before the load-balance exchange),
+ * spread over many workgroups: d_perm / d_bin_id as above, d_counts[b] rows per bin. */
+int lddl_bin_stable(lddl_ctx* ctx, void* stream, const int32_t* d_num_tokens, int64_t n_rows,
+                    int32_t bin_size, int32_t nbins, int64_t* d_perm, int64_t* d_bin_id,
+                    int64_t* d_counts);
+
 /* ---------------------------------------------------------------------------------------------
  * Rendering of the parquet columns (lddl/dask/bert/pretrain.py:345-358):
  *   A, B = ' '.join(tokens), masked_lm_labels = ' '.join(labels) (vocab strings of the ids),

@@ -32,6 +32,7 @@ SIGNATURES = {
     'lddl_pairs_part_offsets': (ctypes.c_int, [c_vp, c_vp, c_vp]),
     'lddl_bin_partitions': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp,
                                            c_vp, c_vp]),
+    'lddl_bin_stable': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),
     'lddl_render_lengths': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
                                            c_vp, c_vp, c_vp, c_vp]),
     'lddl_render_write': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -93,17 +93,26 @@ def _a2a(send, send_splits, recv_splits, group):
     return recv
 
 
-def balance(ctx, pb, bin_size, nbins, group=None):
-    """Balance the PairBatch `pb` of every rank into per-bin shards of N or N+1 samples."""
+def balance(ctx, pb, bin_size, nbins, group=None, timings=None):
+    """Balance the PairBatch `pb` of every rank into per-bin shards of N or N+1 samples.
+    timings: optional dict, filled with synchronised per-phase wall times (diagnostics)."""
+    import time
     dev = pb.tok_off.device
+
+    def mark(name):
+        if timings is not None:
+            torch.cuda.synchronize()
+            timings[name] = time.perf_counter()
+    mark('start')
     W = dist.get_world_size(group) if dist.is_initialized() else 1
     me = dist.get_rank(group) if dist.is_initialized() else 0
-    from .output import bin_partitions
+    from .output import bin_stable
     ntok = pb.tok_off[1:] - pb.tok_off[:-1]
-    one = torch.tensor([0, pb.n_pairs], dtype=torch.int64, device=dev)
-    perm, _, cnt = bin_partitions(ctx, (ntok + 3).to(torch.int32), one, bin_size, nbins)
+    perm, _, cnt = bin_stable(ctx, (ntok + 3).to(torch.int32), bin_size, nbins)
+    mark('bin')
     counts = gather_counts(cnt.reshape(-1), group)
     target, send, first = plan_exchange(counts)
+    mark('counts')
     bin0 = np.concatenate([[0], np.cumsum(counts[me])])
     # rows to send, dst-major then bin (slices of the local bin order)
     pieces, send_rows_per_dst = [], []
@@ -142,12 +151,14 @@ def balance(ctx, pb, bin_size, nbins, group=None):
             return r.view(buf.dtype)
         return _a2a(buf, ss, rs, group)
 
+    mark('meta')
     rtok = exchange(pb.tokens, pb.tok_off, rmeta[:, 0])
     rtok_off = _scan(rmeta[:, 0].contiguous())
     if masking:
         rpos = exchange(pb.pos, pb.pos_off, rmeta[:, 3])
         rlab = exchange(pb.labels, pb.pos_off, rmeta[:, 3])
         rpos_off = _scan(rmeta[:, 3].contiguous())
+    mark('exchange')
     # regroup received rows bin-major (src order inside a bin = global order)
     src0 = np.concatenate([[0], np.cumsum(recv_rows_per_src)])
     order, bin_off = [], [0]
@@ -171,4 +182,5 @@ def balance(ctx, pb, bin_size, nbins, group=None):
         out.pos = _gather(rpos, rpos_off, order, pos_off, int(pos_off[-1].item()))
         out.labels = _gather(rlab, rpos_off, order, pos_off, int(pos_off[-1].item()))
         out.pos_off = pos_off
+    mark('regroup')
     return out

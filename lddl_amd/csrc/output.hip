@@ -101,6 +101,67 @@ __global__ void __launch_bounds__(kBinThreads) bin_partitions_kernel(
   }
 }
 
+
+// ---- stable sort by bin of one large segment: tiles of kBinTile rows, one wavefront each ----
+constexpr int kBinTile = 2048;
+
+__global__ void __launch_bounds__(64) bin_tile_hist_kernel(const int32_t* __restrict__ num_tokens,
+                                                           int64_t n, int32_t bin_size,
+                                                           int32_t nbins, int64_t n_tiles,
+                                                           int64_t* __restrict__ tile_counts) {
+  __shared__ int32_t s_cnt[kMaxBinsLds];
+  const int64_t tile = blockIdx.x;
+  for (int b = threadIdx.x; b < nbins; b += 64) s_cnt[b] = 0;
+  __syncthreads();
+  const int64_t r0 = tile * kBinTile, r1 = min(n, r0 + kBinTile);
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += 64)
+    atomicAdd(&s_cnt[bin_of(num_tokens[r], bin_size, nbins)], 1);
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbins; b += 64) tile_counts[(int64_t)b * n_tiles + tile] = s_cnt[b];
+}
+
+__global__ void __launch_bounds__(64) bin_tile_scatter_kernel(
+    const int32_t* __restrict__ num_tokens, int64_t n, int32_t bin_size, int32_t nbins,
+    int32_t nbits, int64_t n_tiles, const int64_t* __restrict__ tile_base,
+    int64_t* __restrict__ perm, int64_t* __restrict__ bin_id) {
+  __shared__ int64_t s_run[kMaxBinsLds];
+  const int64_t tile = blockIdx.x;
+  for (int b = threadIdx.x; b < nbins; b += 64) s_run[b] = tile_base[(int64_t)b * n_tiles + tile];
+  __syncthreads();
+  const int lane = threadIdx.x;
+  const uint64_t below = (1ull << lane) - 1;
+  const int64_t r0 = tile * kBinTile, r1 = min(n, r0 + kBinTile);
+  for (int64_t c0 = r0; c0 < r1; c0 += 64) {
+    const int64_t r = c0 + lane;
+    const bool in = r < r1;
+    const int32_t b = in ? bin_of(num_tokens[r], bin_size, nbins) : -1;
+    uint64_t match = __ballot(in);
+    for (int k = 0; k < nbits; ++k) {
+      const uint64_t bk = __ballot(in && ((b >> k) & 1));
+      match &= ((b >> k) & 1) ? bk : ~bk;
+    }
+    int64_t base = 0;
+    if (in) base = s_run[b];
+    __builtin_amdgcn_wave_barrier();
+    if (in) {
+      const int64_t dst = base + __popcll(match & below);
+      perm[dst] = r;
+      bin_id[dst] = b;
+      if ((match & below) == 0) s_run[b] = base + __popcll(match);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// bin totals = column sums of the tile counts (bin b's tiles are contiguous after the scan)
+__global__ void bin_totals_kernel(const int64_t* __restrict__ tile_base, int64_t n_tiles,
+                                  int32_t nbins, int64_t* __restrict__ counts) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < nbins) counts[b] = tile_base[(int64_t)(b + 1) * n_tiles] - tile_base[(int64_t)b * n_tiles];
+}
+
 // ---- rendering --------------------------------------------------------------------------------
 struct RenderArgs {
   const uint8_t* rbytes;  // vocab render table
@@ -278,6 +339,44 @@ extern "C" int lddl_bin_partitions(lddl_ctx* c, void* stream, const int32_t* d_n
   hipLaunchKernelGGL(bin_partitions_kernel, dim3((unsigned)n_part), dim3(kBinThreads), 0,
                      as_stream(stream), d_num_tokens, d_part_off, bin_size, nbins, nbits, d_perm,
                      d_bin_id, d_counts);
+  LDDL_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int lddl_bin_stable(lddl_ctx* c, void* stream, const int32_t* d_num_tokens,
+                               int64_t n_rows, int32_t bin_size, int32_t nbins, int64_t* d_perm,
+                               int64_t* d_bin_id, int64_t* d_counts) {
+  (void)c;
+  if (bin_size < 1 || nbins < 1) LDDL_FAIL(-1, "bin_size and nbins must be >= 1");
+  if (nbins > kMaxBinsLds) LDDL_FAIL(-1, "nbins %d > %d unsupported", nbins, kMaxBinsLds);
+  if (n_rows < 0) LDDL_FAIL(-1, "bad sizes");
+  hipStream_t st = as_stream(stream);
+  if (n_rows == 0) {
+    LDDL_HIP(hipMemsetAsync(d_counts, 0, sizeof(int64_t) * nbins, st));
+    return 0;
+  }
+  int nbits = 0;
+  while ((1 << nbits) < nbins) ++nbits;
+  const int64_t n_tiles = (n_rows + kBinTile - 1) / kBinTile;
+  const int64_t m = n_tiles * nbins;
+  int64_t *tc, *scratch;
+  LDDL_HIP(hipMallocAsync((void**)&tc, sizeof(int64_t) * (2 * m + 1), st));
+  LDDL_HIP(hipMallocAsync((void**)&scratch, sizeof(int64_t) * scan_scratch_elems(m), st));
+  int64_t* base = tc + m;
+  hipLaunchKernelGGL(bin_tile_hist_kernel, dim3((unsigned)n_tiles), dim3(64), 0, st, d_num_tokens,
+                     n_rows, bin_size, nbins, n_tiles, tc);
+  struct In {
+    const int64_t* v;
+    __device__ int64_t operator()(int64_t i) const { return v[i]; }
+  };
+  const hipError_t e = scan_exclusive(In{tc}, m, base, scratch, st);
+  hipLaunchKernelGGL(bin_tile_scatter_kernel, dim3((unsigned)n_tiles), dim3(64), 0, st,
+                     d_num_tokens, n_rows, bin_size, nbins, nbits, n_tiles, base, d_perm, d_bin_id);
+  hipLaunchKernelGGL(bin_totals_kernel, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, st,
+                     base, n_tiles, nbins, d_counts);
+  LDDL_HIP(hipFreeAsync(scratch, st));
+  LDDL_HIP(hipFreeAsync(tc, st));
+  LDDL_HIP(e);
   LDDL_HIP(hipGetLastError());
   return 0;
 }

@@ -22,6 +22,8 @@
 #include <cstdio>
 #include <vector>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "ctx.h"
 #include "device.h"
@@ -106,6 +108,8 @@ __global__ void part_offsets_kernel(const int64_t* part_doc_off, int64_t n_part,
 // flow); only parallel phases (twist, temper, speculative shuffle draws) use the lanes.
 // ---------------------------------------------------------------------------------------------
 constexpr int kN = 624, kM = 397;
+constexpr int kFyTail = 16;           // fy_draws: steps i < kFyTail are drawn sequentially
+constexpr int64_t kPoolChunk = 4096;  // mask pool entries reserved per atomic
 
 __device__ inline int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ inline uint32_t rdlane(uint32_t v, int idx) {
@@ -218,6 +222,17 @@ struct WaveRng {
     const uint64_t lt_mask = (1ull << lane) - 1;
     int32_t s0 = (int32_t)(n - 1);  // next step (uniform); n < 2^30 (host-checked)
     while (s0 >= 1) {
+      if (s0 < kFyTail) {
+        // the last buckets (bit_length <= 4) are a handful of draws each: plain sequential
+        // draws cost less than one window pass per bucket
+        wbase = -1024;
+        while (s0 >= 1) {
+          const uint32_t j = randbelow((uint32_t)(s0 + 1));
+          if (lane == 0) sink((int64_t)s0, j);
+          --s0;
+        }
+        break;
+      }
       if (mti >= kN) twist();
       const int k = 32 - __clz((uint32_t)(s0 + 1));
       const int32_t s_lo = (1 << (k - 1)) - 1 > 1 ? (1 << (k - 1)) - 1 : 1;
@@ -261,6 +276,104 @@ struct WaveRng {
     __syncthreads();
     wbase = -1024;  // the register window is stale
   }
+  // _truncate_seq_pair draws (pretrain.py:161-176). T = na + nb - max_num trims; trim t hits A
+  // iff A is the longer side at that point, which has a closed form: with d = na - nb the first
+  // |d| trims hit the longer side, then B and A alternate starting with B (ties trim B). Each
+  // trim is from the front iff random() < 0.5, i.e. iff the first of its two words is < 2^31, so
+  // 64 trims resolve per wave pass with two ballots.
+  __device__ void trunc_draws(int32_t& na, int32_t& nb, int32_t max_num, int32_t& a_front,
+                              int32_t& b_front) {
+    const int32_t T = na + nb - max_num;
+    if (T <= 0) return;
+    const int32_t d = na - nb, ad = d < 0 ? -d : d;
+    const int lane = threadIdx.x;
+    int32_t done = 0;
+    while (done < T) {
+      if (mti >= kN) twist();
+      const int pairs = (kN - mti) >> 1;
+      if (pairs == 0) {  // the trim's two words straddle the block end
+        wbase = -1024;
+        const int32_t front = below_half() ? 1 : 0;
+        const bool sa = done < d || (done >= ad && ((done - ad) & 1));
+        if (sa) a_front += front;
+        else b_front += front;
+        ++done;
+        continue;
+      }
+      const int cnt = min(min(T - done, pairs), 64);
+      const int32_t t = done + lane;
+      const bool front = lane < cnt && temper(mt[mti + 2 * lane]) < 0x80000000u;
+      const bool sa = t < d || (t >= ad && ((t - ad) & 1));
+      a_front += __popcll(__ballot(front && sa));
+      b_front += __popcll(__ballot(front && !sa));
+      mti = uni(mti + 2 * cnt);
+      done += cnt;
+    }
+    wbase = -1024;
+    const int32_t nA = (d > 0 ? min(d, T) : 0) + (T > ad ? (T - ad) / 2 : 0);
+    na -= nA;
+    nb -= T - nA;
+  }
+
+  // Decisions of create_masked_lm_predictions (pretrain.py:208-221) for cnt masked tokens:
+  // random() < 0.8 -> [MASK]; else random() < 0.5 -> keep; else vocab_words[randint(0, V-1)].
+  // Lane t tabulates the decision and word count of a token whose first word is mti + t; the
+  // tokens then follow as a pointer chase through that table (two readlanes per token). A table
+  // entry that would read past the MT block is left empty and that token is drawn the scalar way.
+  template <typename Out>
+  __device__ void mask_decisions(int cnt, uint64_t lt08, int32_t V, int32_t mask_id, Out out) {
+    const int lane = threadIdx.x;
+    const int kV = 32 - __clz((uint32_t)V);
+    int c = 0;
+    while (c < cnt) {
+      if (mti >= kN) twist();
+      const int avail = kN - mti;
+      int len = 0;
+      int32_t tok = 0;
+      if (lane + 1 < avail) {
+        const uint32_t w0 = temper(mt[mti + lane]), w1 = temper(mt[mti + lane + 1]);
+        const uint64_t N = ((uint64_t)(w0 >> 5) << 26) | (w1 >> 6);
+        if (N < lt08) {
+          len = 2;
+          tok = mask_id;
+        } else if (lane + 3 < avail) {
+          if (temper(mt[mti + lane + 2]) < 0x80000000u) {
+            len = 4;
+            tok = kKeep;
+          } else {
+            for (int j = lane + 4; j < avail; ++j) {
+              const uint32_t r = temper(mt[mti + j]) >> (32 - kV);
+              if (r < (uint32_t)V) {
+                len = j + 1 - lane;
+                tok = (int32_t)r;
+                break;
+              }
+            }
+          }
+        }
+      }
+      int pos = 0;
+      while (c < cnt && pos < 64) {
+        const int l = (int)rdlane((uint32_t)len, pos);
+        if (l == 0) break;
+        out(c, (int32_t)rdlane((uint32_t)tok, pos));
+        pos = uni(pos + l);
+        ++c;
+      }
+      mti = uni(mti + pos);
+      wbase = -1024;
+      if (c < cnt && pos < 64) {
+        int32_t t2;
+        if (rand53() < lt08) t2 = mask_id;
+        else if (below_half()) t2 = kKeep;
+        else t2 = (int32_t)randint(0, V - 1);
+        out(c, t2);
+        ++c;
+        wbase = -1024;
+      }
+    }
+  }
+
   // random() = N / 2^53 with N = (w1 >> 5) * 2^26 + (w2 >> 6). `random() < p` is decided exactly
   // on N: N < ceil(p * 2^53) (see k_short / kLt08), so no floating point is needed.
   __device__ uint64_t rand53() {
@@ -299,14 +412,18 @@ struct PlanArgs {
   PairDesc* desc;
   int32_t* jseq;       // per slot: j_i draws of the final partition shuffle
   int32_t* nmask;      // per slot
-  uint16_t* mpos;      // per slot * max_pred
-  int32_t* mtok;       // per slot * max_pred
+  uint16_t* mpos;      // mask pool: positions of slot s at moff[s] .. + nmask[s]
+  int32_t* mtok;       // mask pool: replacement tokens (kKeep = keep)
+  int64_t* moff;       // per slot
+  unsigned long long* pool_used;
+  int64_t pool_cap;
+  int32_t* overflow;   // set when the pool is too small (the host re-plans with a larger one)
   int64_t* part_npairs;
   uint64_t* stamps;  // diagnostic build: [n_part][8]
 };
 
 constexpr int kDocLds = 512;
-constexpr uint64_t kLt08 = 7205759403792794ull;  // 0.8 (binary64) * 2^53, exact  // partitions with <= this many documents cache offsets in LDS
+constexpr uint64_t kLt08 = 7205759403792794ull;  // ceil(0.8 (binary64) * 2^53): random() < 0.8
 
 // Sentence lengths of one document through a 64-entry register window.
 struct LenWin {
@@ -362,6 +479,7 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
   };
   const int64_t base = (int64_t)A.dup * kbase;
   const int32_t max_num = A.seq - 3;
+  int64_t pool_cur = 0, pool_end = 0;  // this wave's current chunk of the mask pool
   LenWin La, Lb;
   int64_t np = 0;
   for (int dp = 0; dp < A.dup; ++dp) {
@@ -419,11 +537,7 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
         }
         // _truncate_seq_pair
         int32_t a_front = 0, b_front = 0, na = (int32_t)la, nb = (int32_t)lb;
-        while (na + nb > max_num) {
-          const int32_t front = rng.below_half() ? 1 : 0;
-          if (na > nb) { a_front += front; --na; }
-          else { b_front += front; --nb; }
-        }
+        rng.trunc_draws(na, nb, max_num, a_front, b_front);
         STAMP_ADD(0, st_t);
         const int64_t slot = base + np;
         if (leader) A.desc[slot] = PairDesc{s0 + chunk0, b_ks, a_front, na, b_front,
@@ -477,13 +591,8 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
             STAMP_ADD(3, st_t);
             const int cmax = min(64, num - c0);
             int32_t mytok = 0;
-            for (int c = 0; c < cmax; ++c) {
-              int32_t tok;
-              if (rng.rand53() < kLt08) tok = A.mask_id;
-              else if (rng.below_half()) tok = kKeep;
-              else tok = (int32_t)rng.randint(0, A.vocab_size - 1);
-              mytok = lane == c ? tok : mytok;  // writelane
-            }
+            rng.mask_decisions(cmax, kLt08, A.vocab_size, A.mask_id,
+                               [&](int c, int32_t tok) { mytok = lane == c ? tok : mytok; });
             if (lane < cmax) {
               tpos[c0 + lane] = (uint16_t)cval;
               ttok[c0 + lane] = mytok;
@@ -491,15 +600,36 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
             STAMP_ADD(4, st_t);
           }
           __syncthreads();
-          // sorted(masked_lms, key=index): rank sort (positions are distinct)
-          for (int32_t c = lane; c < num; c += 64) {
-            const uint16_t v = tpos[c];
-            int32_t r = 0;
-            for (int32_t o = 0; o < num; ++o) r += tpos[o] < v;
-            A.mpos[slot * A.max_pred + r] = v;
-            A.mtok[slot * A.max_pred + r] = ttok[c];
+          // pool space for this pair's masks (bump allocation; order of pairs is irrelevant since
+          // each slot records its own offset)
+          if (pool_cur + num > pool_end) {  // a new chunk: one atomic per kPoolChunk masks
+            const int64_t sz = num > kPoolChunk ? num : kPoolChunk;
+            int64_t nb0 = 0;
+            if (leader) nb0 = (int64_t)atomicAdd(A.pool_used, (unsigned long long)sz);
+            nb0 = ((int64_t)__shfl((int)(nb0 >> 32), 0, 64) << 32) |
+                  (uint32_t)__shfl((int)(uint32_t)nb0, 0, 64);
+            pool_cur = nb0;
+            pool_end = nb0 + sz;
           }
-          if (leader) A.nmask[slot] = num;
+          const int64_t mb = pool_cur;
+          pool_cur += num;
+          const bool fits = pool_end <= A.pool_cap;
+          // sorted(masked_lms, key=index): rank sort (positions are distinct)
+          if (fits) {
+            for (int32_t c = lane; c < num; c += 64) {
+              const uint16_t v = tpos[c];
+              int32_t r = 0;
+              for (int32_t o = 0; o < num; ++o) r += tpos[o] < v;
+              A.mpos[mb + r] = v;
+              A.mtok[mb + r] = ttok[c];
+            }
+          } else if (leader) {
+            *A.overflow = 1;
+          }
+          if (leader) {
+            A.nmask[slot] = num;
+            A.moff[slot] = mb;
+          }
           __syncthreads();
           STAMP_ADD(5, st_t);
         }
@@ -522,6 +652,16 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
     for (int r = 0; r < kStampRegions; ++r) A.stamps[(int64_t)p * kStampRegions + r] = st_acc[r];
 #endif
   if (leader) A.part_npairs[p] = np;
+}
+
+// total kept tokens (sizing of the mask pool)
+__global__ void __launch_bounds__(256) sum_tokens_kernel(const int32_t* __restrict__ sent_len,
+                                                        int64_t n, unsigned long long* out) {
+  int64_t acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    acc += sent_len[i] & kLenMask;
+  acc = wave_sum(acc);
+  if (lane_id() == 0) atomicAdd(out, (unsigned long long)acc);
 }
 
 // Perform the final per-partition Fisher-Yates swaps (draws from plan_replay_kernel). One
@@ -599,6 +739,7 @@ struct GatherArgs {
   const int32_t* nmask;
   const uint16_t* mpos;
   const int32_t* mtok;
+  const int64_t* moff;
   int32_t max_pred, masking;
   int64_t n_pairs;
   const int64_t* tok_off;
@@ -657,10 +798,11 @@ __global__ void __launch_bounds__(64 * kGatherWaves) gather_kernel(GatherArgs G)
   int32_t* lab = nullptr;
   if (G.masking && active) {
     nm = G.nmask[slot];
+    const int64_t mb = G.moff[slot];
     for (int j = lane; j < nm; j += 64) {
-      const uint16_t pv = G.mpos[slot * G.max_pred + j];
+      const uint16_t pv = G.mpos[mb + j];
       s_pos[w][j] = pv;
-      s_tok[w][j] = G.mtok[slot * G.max_pred + j];
+      s_tok[w][j] = G.mtok[mb + j];
       G.out_pos[G.pos_off[q] + j] = pv;
     }
     lab = G.out_lab + G.pos_off[q];
@@ -696,6 +838,7 @@ struct lddl_pairs {
   PairDesc* desc = nullptr;
   int32_t *order = nullptr, *nmask = nullptr, *mtok = nullptr;
   uint16_t* mpos = nullptr;
+  int64_t* moff = nullptr;
   int64_t *src = nullptr, *tok_off = nullptr, *pos_off = nullptr;
   int64_t* part_base = nullptr;  // [n_part + 1] first output pair of each partition
 
@@ -794,13 +937,32 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   TRY(P->alloc(&part_npairs, n_part + 1, st));
   if (prm->masking) {
     TRY(P->alloc(&P->nmask, slots, st));
-    TRY(P->alloc(&P->mpos, slots * max_pred, st));
-    TRY(P->alloc(&P->mtok, slots * max_pred, st));
+    TRY(P->alloc(&P->moff, slots, st));
   }
-  PlanArgs A{P->ks_start, P->ks_len, P->kd_off, P->kp_off, d_ids, d_part_seed,
-             prm->seq, prm->dup, prm->masking, c->vocab_size, cls, sep, msk, max_pred,
-             prm->short_seq_prob, prm->masked_lm_ratio, short_threshold(prm->short_seq_prob),
-             ((prm->seq + 63) / 64) * 64, P->desc, jseq, P->nmask, P->mpos, P->mtok, part_npairs, nullptr};
+  PlanArgs A{};
+  A.ks_start = P->ks_start;
+  A.ks_len = P->ks_len;
+  A.kd_off = P->kd_off;
+  A.kp_off = P->kp_off;
+  A.ids = d_ids;
+  A.part_seed = d_part_seed;
+  A.seq = prm->seq;
+  A.dup = prm->dup;
+  A.masking = prm->masking;
+  A.vocab_size = c->vocab_size;
+  A.cls_id = cls;
+  A.sep_id = sep;
+  A.mask_id = msk;
+  A.max_pred = max_pred;
+  A.short_seq_prob = prm->short_seq_prob;
+  A.ratio = prm->masked_lm_ratio;
+  A.k_short = short_threshold(prm->short_seq_prob);
+  A.seq_r64 = ((prm->seq + 63) / 64) * 64;
+  A.desc = P->desc;
+  A.jseq = jseq;
+  A.nmask = P->nmask;
+  A.moff = P->moff;
+  A.part_npairs = part_npairs;
 #ifdef LDDL_STAMPS
   uint64_t* d_stamps;
   TRY(P->alloc(&d_stamps, n_part * kStampRegions, st));
@@ -810,12 +972,57 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   if (prm->seq > 512) TRY((set_error("replay planner supports target_seq_length <= 512"), -1));
   const size_t lds = 4 * kN + 4 * (kDocLds + 4) + 4 * (size_t)A.seq_r64 +
                      2 * ((max_pred + 7) & ~7) + 4 * max_pred + 16;
-  if (n_part) {
+  // mask pool: sized from the kept tokens (expected use ~0.15 * 1.5 * dup * tokens + pairs); a
+  // plan that outgrows it reports the exact size and is planned again (deterministic replay)
+  unsigned long long* pool_ctl;  // [0] used, [1] overflow flag
+  TRY(P->alloc(&pool_ctl, 2, st));
+  int64_t cap = 0;
+  if (prm->masking && n_sent) {
+    LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 16, st));
+    hipLaunchKernelGGL(sum_tokens_kernel, dim3(1024), dim3(256), 0, st, d_sent_len, n_sent,
+                       pool_ctl);
+    unsigned long long kept_tokens = 0;
+    LDDL_HIP(hipMemcpyAsync(&kept_tokens, pool_ctl, 8, hipMemcpyDeviceToHost, st));
+    LDDL_HIP(hipStreamSynchronize(st));
+    cap = (int64_t)(2.0 * prm->masked_lm_ratio * prm->dup * (double)kept_tokens) +
+          (int64_t)prm->dup * P->n_kept_sent / 2 + kPoolChunk * (n_part + 16);
+    if (const char* e = getenv("LDDL_AMD_MASK_POOL")) cap = atoll(e);  // tests: force a re-plan
+  }
+  for (int attempt = 0; n_part; ++attempt) {
+    uint16_t* mpos = nullptr;
+    int32_t* mtok = nullptr;
+    if (prm->masking) {
+      LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 16, st));
+      LDDL_HIP(hipMallocAsync((void**)&mpos, 2 * (size_t)cap + 16, st));
+      LDDL_HIP(hipMallocAsync((void**)&mtok, 4 * (size_t)cap + 16, st));
+    }
+    A.mpos = mpos;
+    A.mtok = mtok;
+    A.pool_cap = cap;
+    A.pool_used = pool_ctl;
+    A.overflow = reinterpret_cast<int32_t*>(pool_ctl + 1);
     hipLaunchKernelGGL(plan_replay_kernel, dim3((unsigned)n_part), dim3(64), lds, st, A);
+    LDDL_HIP(hipGetLastError());
+    if (!prm->masking) break;
+    unsigned long long ctl[2];
+    LDDL_HIP(hipMemcpyAsync(ctl, pool_ctl, 16, hipMemcpyDeviceToHost, st));
+    LDDL_HIP(hipStreamSynchronize(st));
+    if (!ctl[1]) {
+      P->mpos = mpos;
+      P->mtok = mtok;
+      P->allocs.push_back(mpos);
+      P->allocs.push_back(mtok);
+      break;
+    }
+    (void)hipFreeAsync(mpos, st);
+    (void)hipFreeAsync(mtok, st);
+    if (attempt > 0) TRY((set_error("mask pool overflow after resize"), -1));
+    cap = (int64_t)ctl[0] + 1024;
+  }
+  if (n_part)
     hipLaunchKernelGGL(apply_shuffle_kernel, dim3((unsigned)n_part), dim3(64),
                        sizeof(int32_t) * kShufLds, st, P->kd_off, P->kp_off, prm->dup,
                        part_npairs, jseq, P->order);
-  }
   LDDL_HIP(hipGetLastError());
 #ifdef LDDL_STAMPS
   {
@@ -876,7 +1083,7 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
   if (!P) LDDL_FAIL(-1, "null plan");
   hipStream_t st = as_stream(stream);
   if (P->n_pairs == 0) return 0;
-  GatherArgs G{P->ks_start, P->ks_len, P->ids, P->src, P->desc, P->nmask, P->mpos, P->mtok,
+  GatherArgs G{P->ks_start, P->ks_len, P->ids, P->src, P->desc, P->nmask, P->mpos, P->mtok, P->moff,
                P->max_pred, P->masking, P->n_pairs, P->tok_off, P->pos_off, d_tokens, d_len_a,
                d_is_rn, d_pos, d_lab};
   const int64_t grid = (P->n_pairs + kGatherWaves - 1) / kGatherWaves;

@@ -46,6 +46,19 @@ def bin_partitions(ctx, num_tokens, part_off, bin_size, nbins):
     return perm, bin_id, counts.view(n_part, nbins)
 
 
+def bin_stable(ctx, num_tokens, bin_size, nbins):
+    """One segment (all rows): (perm, bin_id, counts[nbins]) — the tiled multi-workgroup regroup
+    used before the load-balance exchange."""
+    n = num_tokens.numel()
+    dev = num_tokens.device
+    perm = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
+    bin_id = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
+    counts = torch.empty(nbins, dtype=torch.int64, device=dev)
+    check(lib.lddl_bin_stable(ctx.handle, _stream(), _ptr(num_tokens), n, bin_size, nbins,
+                              _ptr(perm), _ptr(bin_id), _ptr(counts)))
+    return perm, bin_id, counts
+
+
 def _scan(x):
     out = torch.empty(x.numel() + 1, dtype=torch.int64, device=x.device)
     check(lib.lddl_scan_i64(_stream(), _ptr(x), x.numel(), _ptr(out)))

@@ -154,3 +154,19 @@ def test_pretrain_cli_vs_oracle(tmp_path, binned):
                 t = pq.read_table(sink / 'part.{}.parquet_{}'.format(p, b)).to_pylist()
                 exp = [dict(r, bin_id=b) for r, bb in zip(rows, bins) if bb == b]
                 assert t == exp
+
+
+def test_bin_stable_single_segment_vs_oracle(ctx):
+    import torch
+    from oracle import oracle as O
+    from lddl_amd.output import bin_stable
+    rng = np.random.default_rng(9)
+    for n, seq, bs in ((0, 512, 8), (1, 128, 32), (5000, 128, 32), (300_001, 512, 8),
+                       (70_000, 512, 1)):
+        nb = seq // bs
+        nt = rng.integers(5, seq + 1, n).astype(np.int32)
+        perm, bin_id, counts = bin_stable(ctx, torch.from_numpy(nt).cuda(), bs, nb)
+        eb, eo, ec = O.bin_samples(nt, bs, nb)
+        np.testing.assert_array_equal(perm.cpu().numpy(), eo)
+        np.testing.assert_array_equal(bin_id.cpu().numpy(), eb[eo])
+        np.testing.assert_array_equal(counts.cpu().numpy(), ec)

@@ -71,3 +71,10 @@ def test_pairs_golden_gpu(name, ctx, docs_dev):
         np.testing.assert_array_equal(out['pos_off'], g['pos_off'])
         np.testing.assert_array_equal(out['pos'], g['pos'])
         np.testing.assert_array_equal(out['labels'], g['labels'])
+
+
+def test_mask_pool_overflow_replans(ctx, docs_dev, monkeypatch):
+    """A mask pool that is too small makes the planner re-plan with the exact size: same output."""
+    name = 's128_mask'
+    monkeypatch.setenv('LDDL_AMD_MASK_POOL', '100')
+    test_pairs_golden_gpu(name, ctx, docs_dev)
