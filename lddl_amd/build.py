@@ -40,18 +40,21 @@ def _run(cmd):
     return r.stdout
 
 
-def build_product(verbose=False, jobs=8, diag=False):
+def build_product(verbose=False, jobs=8, diag=False, variant=None, defines=()):
     """diag=True builds the stamp-instrumented diagnostic library into lddl_amd/_lib_diag
-    (timing shares only; never the shipped library)."""
-    libdir = LIBDIR + ('_diag' if diag else '')
-    objdir = OBJDIR + ('_diag' if diag else '')
+    (timing shares only; never the shipped library). variant/defines build an experiment library
+    into lddl_amd/_lib_<variant> with extra -D flags (A/B measurements only)."""
+    suffix = '_diag' if diag else ('_' + variant if variant else '')
+    libdir = LIBDIR + suffix
+    objdir = OBJDIR + suffix
     lib = os.path.join(libdir, 'liblddl_amd.so')
     os.makedirs(libdir, exist_ok=True)
     os.makedirs(objdir, exist_ok=True)
     headers = glob.glob(os.path.join(ROOT, 'include', '*.h')) + glob.glob(os.path.join(CSRC, '*.h'))
     srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')) + glob.glob(os.path.join(CSRC, '*.cpp')))
     flags = ['-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function',
-             '-I' + os.path.join(ROOT, 'include'), '-I' + CSRC] + (['-DLDDL_STAMPS'] if diag else [])
+             '-I' + os.path.join(ROOT, 'include'), '-I' + CSRC] + (['-DLDDL_STAMPS'] if diag else []) + \
+        ['-D' + d for d in defines]
     objs, jobs_list = [], []
     for s in srcs:
         o = os.path.join(objdir, os.path.basename(s) + '.o')
@@ -91,5 +94,8 @@ def build_all(verbose=False):
 if __name__ == '__main__':
     if '--diag' in sys.argv:
         print(build_product(verbose=True, diag=True))
+    elif '--variant' in sys.argv:  # python -m lddl_amd.build --variant NAME DEF=VAL ...
+        i = sys.argv.index('--variant')
+        print(build_product(verbose=True, variant=sys.argv[i + 1], defines=sys.argv[i + 2:]))
     else:
         print(build_all(verbose=True))

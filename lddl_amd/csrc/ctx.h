@@ -18,6 +18,7 @@ struct lddl_ctx {
   int64_t* d_voff = nullptr;
   uint8_t* d_render = nullptr;      // full token strings (as in vocab.txt, "##" kept)
   int64_t* d_render_off = nullptr;  // token i = d_render[off[i] .. off[i+1])
+  uint32_t* d_bloom = nullptr;
   int32_t vocab_size = 0;
   std::vector<std::string> tokens;  // host copy of the vocab lines
 };

@@ -20,11 +20,13 @@ __host__ __device__ inline uint32_t meta_len(uint32_t m) { return (m >> 21) & 0x
 __host__ __device__ inline int32_t meta_id(uint32_t m) { return (int32_t)(m & 0x1FFFFF); }
 
 __host__ __device__ inline uint64_t vhash(uint64_t k0, uint32_t k1, uint32_t len, uint32_t cont) {
-  uint64_t h = k0 * 0x9E3779B97F4A7C15ull;
-  h ^= ((uint64_t)k1 << 17) ^ ((uint64_t)len << 3) ^ (uint64_t)cont;
-  h ^= h >> 29;
-  h *= 0xBF58476D1CE4E5B9ull;
-  h ^= h >> 32;
+  // 32-bit multiplies only (v_mul_lo_u32): a 64-bit multiply costs ~4 of them on CDNA
+  uint32_t h = (uint32_t)k0 * 0x9E3779B1u;
+  h ^= ((uint32_t)(k0 >> 32) + (len << 24) + cont) * 0x85EBCA77u;
+  h ^= k1 * 0xC2B2AE3Du;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 13;
   return h;
 }
 
@@ -55,7 +57,25 @@ struct Tables {
   // ASCII fast path of the wave tokenizer: 1 = ASCII WORD chars map to themselves except A-Z ->
   // a-z (uncased table), 2 = all map to themselves (cased), 0 = neither (fast path disabled)
   int32_t ascii_mode;
+  const uint32_t* bloom;  // kBloomWords words: Bloom filter of (continuation, piece bytes)
 };
+
+// Bloom filter over vocab pieces for the longest-match scan: a piece's prefix hash is a
+// polynomial over its bytes (h = h * P + b + 1 mod 2^32, so every prefix of a word comes from one
+// pass), mixed with its length and continuation flag; two bits in one 32-bit word.
+constexpr int kBloomWords = 8192;  // 32 KB
+constexpr uint32_t kBloomP = 0x01000193u;
+__host__ __device__ inline uint32_t bloom_mix(uint32_t h, uint32_t len, uint32_t cont) {
+  uint32_t x = h + len * 0x9E3779B9u + cont * 0x7F4A7C15u;
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  return x;
+}
+__host__ __device__ inline uint32_t bloom_word(uint32_t x) { return x >> 19; }
+__host__ __device__ inline uint32_t bloom_bits(uint32_t x) {
+  return (1u << (x & 31u)) | (1u << ((x >> 5) & 31u));
+}
 
 // sent_len flag: the kept pieces contain a literal [CLS] or [SEP] (matters for static masking
 // candidates, pretrain.py:189-192)

@@ -422,7 +422,7 @@ struct PlanArgs {
   uint64_t* stamps;  // diagnostic build: [n_part][8]
 };
 
-constexpr int kDocLds = 512;
+constexpr int kDocLds = 512;  // partitions with <= this many documents cache offsets in LDS
 constexpr uint64_t kLt08 = 7205759403792794ull;  // ceil(0.8 (binary64) * 2^53): random() < 0.8
 
 // Sentence lengths of one document through a 64-entry register window.

@@ -208,16 +208,15 @@ __global__ void __launch_bounds__(kBlock) tokenize_lane_kernel(
 // ---------------------------------------------------------------------------------------------
 constexpr int kTW = 4;     // waves per workgroup
 constexpr int kPcs = 8;    // pieces per unit held per lane (more -> fallback)
-constexpr int kNorm = 48;  // normalised bytes per unit on the generic path (more -> fallback)
+constexpr int kNorm = 32;  // normalised bytes per unit on the generic path (more -> fallback)
 
 // unit categories per byte position
 enum : uint32_t { kCatRun = 0, kCatSep = 1, kCatIso = 2, kCatSpecial = 3 };
 
 struct alignas(16) WaveLds {
-  uint8_t win[64 + 16];        // window bytes (+16 so 20-byte reads at any start stay inside)
   uint8_t us[64], ue[64], uk[64];  // unit k: first byte, last byte (window-relative), kind
-  int32_t pcs[kPcs * 64];      // lane l's pieces at pcs[j * 64 + l]
-  uint8_t nrm[64 * kNorm];     // lane l's normalised word (generic path)
+  int32_t pcs[kPcs * 64];          // lane l's pieces at pcs[64 q + l]
+  uint8_t nrm[64 * kNorm];         // lane l's normalised word (generic path)
 };
 
 // Order this wave's LDS writes before its later LDS reads of other lanes' data (the waves of a
@@ -243,6 +242,13 @@ __device__ inline void shr128(uint64_t lo, uint64_t hi, int sh, uint64_t& a, uin
   else { a = hi >> (8 * (sh - 8)); b = 0; }
 }
 
+// The pieces of one unit: the lane's column of an LDS buffer (lane l's piece q at b[64 q]).
+struct Pcs {
+  int32_t* b;
+  __device__ void put(int n, int32_t v) { b[64 * n] = v; }
+  __device__ int32_t get(int q) const { return b[64 * q]; }
+};
+
 // Vocab probe for a key held in registers: bytes [0,8) in a, [8,16) in b (len <= 16).
 __device__ inline int32_t probe_reg(const Tables& T, uint64_t a, uint64_t b, int len, uint32_t cont) {
   const uint64_t k0 = keep_bytes(a, len);
@@ -263,34 +269,58 @@ __device__ inline int32_t probe_reg(const Tables& T, uint64_t a, uint64_t b, int
   }
 }
 
+// Bloom candidates for the pieces starting at the word's first byte held in (a, b): bit L-1 of
+// the result is set iff the filter may contain (cont, bytes[0, L)), L = 1 .. maxl.
+__device__ inline uint32_t bloom_candidates(const uint32_t* bloom, uint64_t a, uint64_t b, int maxl,
+                                            uint32_t cont) {
+  uint32_t h = 0, cand = 0;
+  for (int L = 1; L <= maxl; ++L) {
+    const uint32_t byte = (uint32_t)((L <= 8 ? a >> (8 * (L - 1)) : b >> (8 * (L - 9))) & 0xFFu);
+    h = h * kBloomP + byte + 1u;
+    const uint32_t x = bloom_mix(h, (uint32_t)L, cont);
+    const uint32_t m = bloom_bits(x);
+    if ((bloom[bloom_word(x)] & m) == m) cand |= 1u << (L - 1);
+  }
+  return cand;
+}
+
 // Greedy longest-match WordPiece of an ASCII word of nb <= 16 bytes held in (lo, hi).
-// Returns the piece count written to pc[j * 64] (j < kPcs), or -1 if more than kPcs pieces.
-__device__ int wordpiece_reg(const Tables& T, uint64_t lo, uint64_t hi, int nb, int32_t* pc) {
+// Returns the piece count written to pc (< kPcs), or -1 if more than kPcs pieces. The longest
+// candidate is probed first (most words are one piece); when it misses, the Bloom filter (LDS)
+// rules out the shorter lengths that cannot be pieces, so only likely ones are probed.
+__device__ int wordpiece_reg(const Tables& T, const uint32_t* bloom, uint64_t lo, uint64_t hi,
+                             int nb, Pcs& pc) {
   int n = 0, start = 0;
   while (start < nb) {
     uint64_t a, b;
     shr128(lo, hi, start, a, b);
+    const uint32_t cont = start > 0;
     int len = nb - start < T.max_piece_bytes ? nb - start : T.max_piece_bytes;
-    int32_t id = -1;
-    for (; len > 0; --len) {
-      id = probe_reg(T, a, b, len, start > 0);
-      if (id >= 0) break;
+    int32_t id = probe_reg(T, a, b, len, cont);
+    if (id < 0) {
+      uint32_t cand = len > 1 ? bloom_candidates(bloom, a, b, len - 1, cont) : 0u;
+      while (cand) {
+        len = 32 - __clz(cand);
+        id = probe_reg(T, a, b, len, cont);
+        if (id >= 0) break;
+        cand &= ~(1u << (len - 1));
+      }
     }
     if (id < 0) {
-      pc[0] = T.special_id[kUnk];
+      pc.put(0, T.special_id[kUnk]);
       return 1;
     }
     if (n == kPcs) return -1;
-    pc[64 * n++] = id;
+    pc.put(n++, id);
     start += len;
   }
   return n;
 }
 
 // Greedy longest-match WordPiece of a normalised word in LDS (UTF-8, nb bytes, nc chars).
-__device__ int wordpiece_lds(const Tables& T, const uint8_t* w, int nb, int nc, int32_t* pc) {
+__device__ int wordpiece_lds(const Tables& T, const uint8_t* w, int nb, int nc, Pcs& pc) {
   if (nc == 0) return 0;
-  if (nc > 100) { pc[0] = T.special_id[kUnk]; return 1; }
+  if (nc > 100) { pc.put(0, T.special_id[kUnk]); return 1; }
   int n = 0, start = 0;
   while (start < nb) {
     int end = nb < start + T.max_piece_bytes ? nb : start + T.max_piece_bytes;
@@ -300,16 +330,197 @@ __device__ int wordpiece_lds(const Tables& T, const uint8_t* w, int nb, int nc, 
       found = lookup(T, w, start, end - start, start > 0);
       if (found >= 0) break;
     }
-    if (found < 0) { pc[0] = T.special_id[kUnk]; return 1; }
+    if (found < 0) { pc.put(0, T.special_id[kUnk]); return 1; }
     if (n == kPcs) return -1;
-    pc[64 * n++] = found;
+    pc.put(n++, found);
     start = end;
   }
   return n;
 }
 
+// Classification of one 64-byte window [pos, pos+64) of a sentence ending at b1 (one byte per
+// lane). Fills W.us / W.ue / W.uk with the window's complete units (first byte, last byte, kind:
+// 0 word run, 1 isolated char, 2 + k literal special token k) and returns their count, the start
+// of the next window and the mask of lanes holding a byte the register fast path cannot take.
+struct WinResult {
+  int n_units;
+  int64_t next;
+  uint64_t slow;
+  bool fallback;  // a unit of >= 64 bytes: the sentence goes to the lane kernel
+};
+
+// byte = text[pos + lane] (already loaded by the caller, which may prefetch it), any value when
+// pos + lane >= b1.
+template <typename WL>
+__device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
+                                     const uint8_t* __restrict__ text, int64_t pos, int64_t b1,
+                                     uint32_t byte, WL& W) {
+  const int lane = lane_id();
+  const uint64_t below = lanes_below();
+  const int64_t i = pos + lane;
+  const bool in = i < b1;
+  uint32_t cls = kSpace;  // beyond the sentence: a separator
+  int cplen = 1;          // bytes of the code point starting here (0: covered continuation)
+  int spk = -1;           // literal special token starting here
+  bool slow = false;      // non-ASCII or dropped char: not for the register fast path
+  bool cont = false;
+  if (in) {
+    if (byte < 0x80) {
+      cls = s_ascii[byte] >> 30;
+      slow = cls == kDrop;
+      if (byte == '[') spk = match_special_at(T, text, i, b1);
+    } else if (byte >= 0xC0) {
+      int64_t j = i;
+      const uint32_t cp = utf8_next(text, b1, j);
+      cplen = (int)(j - i);
+      cls = tab_entry(T, cp) >> 30;
+      slow = true;
+    } else {
+      cont = true;  // resolved below: covered by a valid lead, or a lone byte (U+FFFD, drop)
+      cls = kDrop;
+      slow = true;
+    }
+  }
+  const uint64_t V2 = __ballot(cplen == 2), V3 = __ballot(cplen == 3), V4 = __ballot(cplen == 4);
+  const uint64_t C1 = (V2 | V3 | V4) << 1, C2 = (V3 | V4) << 2, C3 = V4 << 3;
+  const bool covered = cont && (((C1 | C2 | C3) >> lane) & 1ull);
+  const int dist = !covered ? 0 : ((C1 >> lane) & 1ull) ? 1 : ((C2 >> lane) & 1ull) ? 2 : 3;
+  // a covered continuation inherits its lead's class; cp_last marks a code point's last byte
+  const int lead_len = __shfl((int)(cls | ((uint32_t)cplen << 4)), lane - dist, 64);
+  if (covered) {
+    cls = (uint32_t)lead_len & 3u;
+    cplen = 0;
+  }
+  const bool cp_last = covered ? (dist == (lead_len >> 4) - 1) : (cplen <= 1);
+  const uint64_t S = __ballot(spk >= 0), S6 = __ballot(spk == kMask);
+  const uint64_t inside = (S << 1) | (S << 2) | (S << 3) | (S << 4) | (S6 << 5);
+  const bool in_sp = ((S | inside) >> lane) & 1ull;
+  const uint32_t cat = in_sp ? kCatSpecial : cls == kSpace ? kCatSep : cls == kIso ? kCatIso : kCatRun;
+  const uint64_t RUN = __ballot(cat == kCatRun);
+  const uint64_t LEAD = __ballot(cplen > 0);
+  const uint64_t ISO = __ballot(cat == kCatIso);
+  const uint64_t CPL = __ballot(cp_last);
+  WinResult R;
+  R.slow = __ballot(slow);
+  R.fallback = false;
+  const bool tail_known = pos + 64 >= b1;  // position 64 is past the sentence end
+  const uint64_t US = S | (ISO & LEAD) | (RUN & ~(RUN << 1));
+  uint64_t RE = RUN & ~(RUN >> 1);
+  if (!tail_known) RE &= ~(1ull << 63);
+  const uint64_t UE = ((S & ~S6) << 4) | (S6 << 5) | (ISO & CPL & ~inside) | RE;
+  R.n_units = __popcll(UE);
+  const int n_starts = __popcll(US);
+  if (n_starts > R.n_units) {
+    const int last = 63 - __clzll(US);
+    if (last == 0) {  // a unit of >= 64 bytes
+      R.fallback = true;
+      R.next = b1;
+      return R;
+    }
+    R.next = pos + last;
+  } else if (tail_known) {
+    R.next = b1;
+  } else {
+    // a separator code point straddling the window end restarts the next window at its lead
+    const int hl = 63 - __clzll(LEAD);
+    const int hc = 63 - __clzll(CPL);
+    R.next = pos + (hl > hc ? hl : 64);
+  }
+  if ((US >> lane) & 1ull) {
+    const int k = __popcll(US & below);
+    W.us[k] = (uint8_t)lane;
+    W.uk[k] = (uint8_t)(spk >= 0 ? 2 + spk : cat == kCatIso ? 1 : 0);
+  }
+  if ((UE >> lane) & 1ull) W.ue[__popcll(UE & below)] = (uint8_t)lane;
+  wave_sync();
+  return R;
+}
+
+// 16 bytes of text from byte `start` (unaligned) as two little-endian 64-bit words; bytes at or
+// past `n_bytes` read as 0 and are never loaded.
+__device__ inline void load16(const uint8_t* __restrict__ text, int64_t n_bytes, int64_t start,
+                              uint64_t& lo, uint64_t& hi) {
+  const int64_t a = start & ~(int64_t)3;
+  const int r = (int)(start & 3);
+  uint32_t d[5];
+  if (a + 20 <= n_bytes) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(text + a);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) d[k] = p[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      uint32_t v = 0;
+      for (int q = 0; q < 4; ++q)
+        if (a + 4 * k + q < n_bytes) v |= (uint32_t)text[a + 4 * k + q] << (8 * q);
+      d[k] = v;
+    }
+  }
+  const uint32_t a0 = __builtin_amdgcn_alignbyte(d[1], d[0], r);
+  const uint32_t a1 = __builtin_amdgcn_alignbyte(d[2], d[1], r);
+  const uint32_t a2 = __builtin_amdgcn_alignbyte(d[3], d[2], r);
+  const uint32_t a3 = __builtin_amdgcn_alignbyte(d[4], d[3], r);
+  lo = (uint64_t)a0 | ((uint64_t)a1 << 32);
+  hi = (uint64_t)a2 | ((uint64_t)a3 << 32);
+}
+
+// Pieces of one pre-tokenizer unit (text[start, start+len), kind as classify_window): written to
+// pc[64 * q]; returns the count, or -1 when the unit needs the lane kernel (> kPcs pieces or a
+// normalised word > kNorm bytes). cs_flag: the unit is a literal [CLS] / [SEP].
+__device__ int unit_pieces(const Tables& T, const uint32_t* bloom,
+                           const uint8_t* __restrict__ text, int64_t n_bytes, int64_t start,
+                           int len, int kind, bool unit_slow, Pcs& pc, uint8_t* w,
+                           bool& cs_flag) {
+  cs_flag = false;
+#ifdef LDDL_TOK_NO_WP  // A/B experiment only: classification + placement without WordPiece
+  pc.put(0, (int32_t)len);
+  return 1;
+#endif
+  if (kind >= 2) {
+    pc.put(0, T.special_id[kind - 2]);
+    cs_flag = kind - 2 == kCls || kind - 2 == kSep;
+    return 1;
+  }
+  if (kind == 0 && !unit_slow && len <= 16 && T.ascii_mode != 0) {
+    uint64_t lo, hi;
+    load16(text, n_bytes, start, lo, hi);
+    lo = keep_bytes(lo, len);
+    hi = keep_bytes(hi, len - 8);
+    if (T.ascii_mode == 1) {  // SWAR A-Z -> a-z on ASCII bytes
+      const uint64_t k3f = 0x3f3f3f3f3f3f3f3full, k25 = 0x2525252525252525ull,
+                     k80 = 0x8080808080808080ull;
+      lo |= (((lo + k3f) & ~(lo + k25)) & k80) >> 2;
+      hi |= (((hi + k3f) & ~(hi + k25)) & k80) >> 2;
+    }
+    return wordpiece_reg(T, bloom, lo, hi, len, pc);
+  }
+  // generic (rare): normalise the unit's code points into the lane's LDS buffer
+  int nb = 0, nc = 0;
+  int64_t j = start;
+  const int64_t je = start + len;
+  while (j < je) {
+    const uint32_t cp = utf8_next(text, je, j);
+    const uint32_t e = tab_entry(T, cp);
+    if ((e >> 30) == kDrop) continue;
+    uint8_t ob[12];
+    int olen, ochars = 1;
+    if (e & kIdent) olen = put_utf8(ob, cp);
+    else if (e & kMulti) {
+      const uint8_t* p = T.pool + (e & 0xFFFFFFu);
+      olen = p[0];
+      ochars = p[1];
+      for (int q = 0; q < olen; ++q) ob[q] = p[2 + q];
+    } else olen = put_utf8(ob, e & 0x1FFFFFu);
+    if (nb + olen > kNorm) return -1;
+    for (int q = 0; q < olen; ++q) w[nb + q] = ob[q];
+    nb += olen;
+    nc += ochars;
+  }
+  return wordpiece_lds(T, w, nb, nc, pc);
+}
+
 __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
-    Tables T, const uint8_t* __restrict__ text, const int64_t* __restrict__ sent_off,
+    Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
     int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
     int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n) {
   __shared__ uint32_t s_ascii[128];
@@ -318,9 +529,6 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
   __syncthreads();
   const int lane = lane_id();
   WaveLds& W = s_w[threadIdx.x >> 6];
-  const uint64_t below = lanes_below();
-  const bool lower = T.ascii_mode == 1;
-  const bool fast_ok = T.ascii_mode != 0;
   const int64_t stride = (int64_t)gridDim.x * kTW;
   for (int64_t s = (int64_t)blockIdx.x * kTW + (threadIdx.x >> 6); s < n_sent; s += stride) {
     const int64_t b0 = sent_off[s], b1 = sent_off[s + 1];
@@ -328,150 +536,27 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
     int32_t emitted = 0, flags = 0;
     bool fallback = false;
     while (pos < b1 && emitted < max_pieces) {
-      const int64_t i = pos + lane;
-      const bool in = i < b1;
-      const uint32_t byte = in ? text[i] : 0x20u;
-      W.win[lane] = (uint8_t)byte;
-      // ---- classify this lane's byte -----------------------------------------------------
-      uint32_t cls = kSpace;  // beyond the sentence: a separator
-      int cplen = 1;          // bytes of the code point starting here (0: covered continuation)
-      int spk = -1;           // literal special token starting here
-      bool slow = false;      // non-ASCII or dropped char: not for the register fast path
-      bool cont = false;
-      if (in) {
-        if (byte < 0x80) {
-          cls = s_ascii[byte] >> 30;
-          slow = cls == kDrop;
-          if (byte == '[') spk = match_special_at(T, text, i, b1);
-        } else if (byte >= 0xC0) {
-          int64_t j = i;
-          const uint32_t cp = utf8_next(text, b1, j);
-          cplen = (int)(j - i);
-          cls = tab_entry(T, cp) >> 30;
-          slow = true;
-        } else {
-          cont = true;  // resolved below: covered by a valid lead, or a lone byte (U+FFFD, drop)
-          cls = kDrop;
-          slow = true;
-        }
-      }
-      const uint64_t V2 = __ballot(cplen == 2), V3 = __ballot(cplen == 3), V4 = __ballot(cplen == 4);
-      const uint64_t C1 = (V2 | V3 | V4) << 1, C2 = (V3 | V4) << 2, C3 = V4 << 3;
-      const bool covered = cont && (((C1 | C2 | C3) >> lane) & 1ull);
-      const int dist = !covered ? 0 : ((C1 >> lane) & 1ull) ? 1 : ((C2 >> lane) & 1ull) ? 2 : 3;
-      // a covered continuation inherits its lead's class; cp_last marks a code point's last byte
-      const int lead_len = __shfl((int)(cls | ((uint32_t)cplen << 4)), lane - dist, 64);
-      if (covered) {
-        cls = (uint32_t)lead_len & 3u;
-        cplen = 0;
-      }
-      const bool cp_last = covered ? (dist == (lead_len >> 4) - 1) : (cplen <= 1);
-      const uint64_t S = __ballot(spk >= 0), S6 = __ballot(spk == kMask);
-      const uint64_t inside = (S << 1) | (S << 2) | (S << 3) | (S << 4) | (S6 << 5);
-      const bool in_sp = ((S | inside) >> lane) & 1ull;
-      const uint32_t cat = in_sp ? kCatSpecial
-                                 : cls == kSpace ? kCatSep : cls == kIso ? kCatIso : kCatRun;
-      const uint64_t RUN = __ballot(cat == kCatRun);
-      const uint64_t LEAD = __ballot(cplen > 0);
-      const uint64_t ISO = __ballot(cat == kCatIso);
-      const uint64_t CPL = __ballot(cp_last);
-      const uint64_t SLOW = __ballot(slow);
-      const bool tail_known = pos + 64 >= b1;  // position 64 is past the sentence end
-      const uint64_t US = S | (ISO & LEAD) | (RUN & ~(RUN << 1));
-      uint64_t RE = RUN & ~(RUN >> 1);
-      if (!tail_known) RE &= ~(1ull << 63);
-      const uint64_t UE = ((S & ~S6) << 4) | (S6 << 5) | (ISO & CPL & ~inside) | RE;
-      const int n_units = __popcll(UE);
-      const int n_starts = __popcll(US);
-      int64_t next;
-      if (n_starts > n_units) {
-        const int last = 63 - __clzll(US);
-        if (last == 0) { fallback = true; break; }  // a unit of >= 64 bytes
-        next = pos + last;
-      } else if (tail_known) {
-        next = b1;
-      } else {
-        // a separator code point straddling the window end restarts the next window at its lead
-        const int hl = 63 - __clzll(LEAD);
-        const int hc = 63 - __clzll(CPL);
-        next = pos + (hl > hc ? hl : 64);
-      }
-      if ((US >> lane) & 1ull) {
-        const int k = __popcll(US & below);
-        W.us[k] = (uint8_t)lane;
-        W.uk[k] = (uint8_t)(spk >= 0 ? 2 + spk : cat == kCatIso ? 1 : 0);
-      }
-      if ((UE >> lane) & 1ull) W.ue[__popcll(UE & below)] = (uint8_t)lane;
-      wave_sync();
-      // ---- WordPiece: lane k takes unit k --------------------------------------------------
+      const uint32_t byte = pos + lane < b1 ? text[pos + lane] : 0x20u;
+      const WinResult R = classify_window(T, s_ascii, text, pos, b1, byte, W);
+      if (R.fallback) { fallback = true; break; }
       int npc = 0;
       bool cs_flag = false;
-      int32_t* pc = W.pcs + lane;
-      if (lane < n_units) {
+      Pcs pc{W.pcs + lane};
+      if (lane < R.n_units) {
         const int us = W.us[lane], ue = W.ue[lane], kind = W.uk[lane];
         const int ulen = ue - us + 1;
-        if (kind >= 2) {
-          pc[0] = T.special_id[kind - 2];
-          npc = 1;
-          cs_flag = kind - 2 == kCls || kind - 2 == kSep;
-        } else {
-          const bool unit_slow = ((SLOW >> us) & (ulen >= 64 ? ~0ull : ((1ull << ulen) - 1))) != 0;
-          if (kind == 0 && !unit_slow && ulen <= 16 && fast_ok) {
-            const uint32_t* wd = reinterpret_cast<const uint32_t*>(W.win) + (us >> 2);
-            const int r = us & 3;
-            const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3], d4 = wd[4];
-            const uint32_t a0 = __builtin_amdgcn_alignbyte(d1, d0, r);
-            const uint32_t a1 = __builtin_amdgcn_alignbyte(d2, d1, r);
-            const uint32_t a2 = __builtin_amdgcn_alignbyte(d3, d2, r);
-            const uint32_t a3 = __builtin_amdgcn_alignbyte(d4, d3, r);
-            uint64_t lo = keep_bytes((uint64_t)a0 | ((uint64_t)a1 << 32), ulen);
-            uint64_t hi = keep_bytes((uint64_t)a2 | ((uint64_t)a3 << 32), ulen - 8);
-            if (lower) {  // SWAR A-Z -> a-z on ASCII bytes
-              const uint64_t k3f = 0x3f3f3f3f3f3f3f3full, k25 = 0x2525252525252525ull,
-                             k80 = 0x8080808080808080ull;
-              lo |= (((lo + k3f) & ~(lo + k25)) & k80) >> 2;
-              hi |= (((hi + k3f) & ~(hi + k25)) & k80) >> 2;
-            }
-            npc = wordpiece_reg(T, lo, hi, ulen, pc);
-          } else {
-            // generic: normalise the unit's code points into the lane's LDS buffer
-            uint8_t* w = W.nrm + lane * kNorm;
-            int nb = 0, nc = 0;
-            int64_t j = pos + us;
-            const int64_t je = pos + ue + 1;
-            while (j < je && nb >= 0) {
-              const uint32_t cp = utf8_next(text, b1, j);
-              const uint32_t e = tab_entry(T, cp);
-              if ((e >> 30) == kDrop) continue;
-              uint8_t ob[12];
-              int olen, ochars = 1;
-              if (e & kIdent) olen = put_utf8(ob, cp);
-              else if (e & kMulti) {
-                const uint8_t* p = T.pool + (e & 0xFFFFFFu);
-                olen = p[0];
-                ochars = p[1];
-                for (int q = 0; q < olen; ++q) ob[q] = p[2 + q];
-              } else olen = put_utf8(ob, e & 0x1FFFFFu);
-              if (nb + olen > kNorm) { nb = -1; break; }
-              for (int q = 0; q < olen; ++q) w[nb + q] = ob[q];
-              nb += olen;
-              nc += ochars;
-            }
-            npc = nb < 0 ? -1 : wordpiece_lds(T, w, nb, nc, pc);
-          }
-        }
+        const bool unit_slow = ((R.slow >> us) & (ulen >= 64 ? ~0ull : ((1ull << ulen) - 1))) != 0;
+        npc = unit_pieces(T, T.bloom, text, n_bytes, pos + us, ulen, kind, unit_slow, pc,
+                          W.nrm + lane * kNorm, cs_flag);
       }
       if (__ballot(npc < 0)) { fallback = true; break; }
-      // ---- place the pieces ----------------------------------------------------------------
       const int incl = wave_incl_scan(npc);
-      const int excl = incl - npc;
-      const int total = __shfl(incl, 63, 64);
-      const int o = emitted + excl;
+      const int o = emitted + incl - npc;
       for (int q = 0; q < npc; ++q)
-        if (o + q < max_pieces) ids[b0 + o + q] = pc[64 * q];
+        if (o + q < max_pieces) ids[b0 + o + q] = pc.get(q);
       if (__ballot(cs_flag && o < max_pieces)) flags = kLenHasClsSep;
-      emitted += total;
-      pos = next;
+      emitted += __shfl(incl, 63, 64);
+      pos = R.next;
       wave_sync();
     }
     if (fallback) {
@@ -480,6 +565,216 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
       sent_len[s] = (emitted < max_pieces ? emitted : max_pieces) | flags;
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Batched wave tokenizer: classification per 64-byte window feeds an LDS queue of units that
+// spans sentences; WordPiece runs when 64 units are queued, so every lane has a word. Pieces are
+// placed by a segmented scan over the queue (units of one sentence are contiguous and ordered)
+// on top of each in-flight sentence's running count (a ring of kRing sentences).
+// ---------------------------------------------------------------------------------------------
+constexpr int kQ = 128;     // queued units (a window adds <= 64; flush at >= 64)
+constexpr int kRing = 64;   // sentences in flight per wave
+constexpr int kBW = 16;     // waves per workgroup (one workgroup per CU shares the Bloom filter)
+
+struct alignas(16) BatchLds {
+  uint8_t us[64], ue[64], uk[64];
+  int32_t q_rel[kQ];        // unit start relative to its sentence's first byte
+  uint8_t q_len[kQ], q_kind[kQ], q_slot[kQ], q_slow[kQ];
+  int64_t r_b0[kRing];
+  int32_t r_sent[kRing], r_count[kRing], r_flags[kRing], r_pending[kRing], r_state[kRing];
+  int32_t pcs[kPcs * 64];  // lane l's pieces at pcs[64 q + l]
+  uint8_t nrm[64 * kNorm];  // lane l's normalised word (generic path)
+};
+
+enum : int32_t { kClosed = 1, kFallback = 2 };
+
+#ifndef LDDL_TOK_MIN_WAVES
+#define LDDL_TOK_MIN_WAVES 1
+#endif
+__global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_kernel(
+    Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
+    int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
+    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n) {
+  __shared__ uint32_t s_ascii[128];
+  __shared__ uint32_t s_bloom[kBloomWords];
+  __shared__ BatchLds s_w[kBW];
+  for (int c = threadIdx.x; c < 128; c += blockDim.x) s_ascii[c] = tab_entry(T, (uint32_t)c);
+  for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
+  __syncthreads();
+  const int lane = lane_id();
+  BatchLds& W = s_w[threadIdx.x >> 6];
+  const int64_t s_first = (int64_t)blockIdx.x * kBW + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kBW;
+  int64_t head = 0, tail = 0;  // ordinals of in-flight sentences: [head, tail)
+  int qn = 0;
+  bool cur = false;
+  int cur_slot = 0;
+  int64_t b0 = 0, b1 = 0, pos = 0;
+  // software prefetch: the next window's bytes are loaded as soon as its start is known (before
+  // the queue flush runs), and the next sentence's offsets one sentence ahead
+  uint32_t pbyte = 0x20u;
+  int64_t ppos = -1;
+  int64_t nb0 = -1, nb1 = -1;
+
+  auto flush = [&]() {
+    const int m = qn < 64 ? qn : 64;
+    int npc = 0;
+    bool cs_flag = false;
+    int slot = -1;
+    Pcs pc{W.pcs + lane};
+    if (lane < m) {
+      slot = W.q_slot[lane];
+      npc = unit_pieces(T, s_bloom, text, n_bytes, W.r_b0[slot] + W.q_rel[lane], W.q_len[lane],
+                        W.q_kind[lane], W.q_slow[lane] != 0, pc, W.nrm + lane * kNorm, cs_flag);
+      if (npc < 0) {
+        atomicOr(&W.r_state[slot], kFallback);
+        npc = 0;
+      }
+    }
+    const int incl = wave_incl_scan(npc);
+    const int excl = incl - npc;
+    const int prev_slot = __shfl(slot, lane > 0 ? lane - 1 : 0, 64);
+    const uint64_t F = __ballot(lane < m && (lane == 0 || slot != prev_slot));
+    const int s0 = 63 - __clzll(F & (lane == 63 ? ~0ull : ((2ull << lane) - 1)));
+    const int seg_excl = excl - __shfl(excl, s0, 64);
+    const int next_slot = __shfl(slot, lane < 63 ? lane + 1 : 63, 64);
+    const bool seg_last = lane < m && (lane == m - 1 || next_slot != slot);
+    if (lane < m) {
+      const int o = W.r_count[slot] + seg_excl;
+      const int64_t bb = W.r_b0[slot];
+      for (int q = 0; q < npc; ++q)
+        if (o + q < max_pieces) ids[bb + o + q] = pc.get(q);
+      if (cs_flag && o < max_pieces) atomicOr(&W.r_flags[slot], kLenHasClsSep);
+    }
+    wave_sync();
+    if (seg_last) {
+      W.r_count[slot] += seg_excl + npc;
+      W.r_pending[slot] -= lane - s0 + 1;
+    }
+    // drop the processed units from the queue (sources [64, qn) never overlap targets [0, qn-64))
+    const int rest = qn - m;
+    int32_t rel = 0;
+    uint8_t ql = 0, qk = 0, qs = 0, qw = 0;
+    if (lane < rest) {
+      rel = W.q_rel[m + lane];
+      ql = W.q_len[m + lane];
+      qk = W.q_kind[m + lane];
+      qs = W.q_slot[m + lane];
+      qw = W.q_slow[m + lane];
+    }
+    wave_sync();
+    if (lane < rest) {
+      W.q_rel[lane] = rel;
+      W.q_len[lane] = ql;
+      W.q_kind[lane] = qk;
+      W.q_slot[lane] = qs;
+      W.q_slow[lane] = qw;
+    }
+    wave_sync();
+    qn = rest;
+  };
+
+  auto retire = [&]() {
+    while (head < tail) {
+      const int sl = (int)(head % kRing);
+      const int st = W.r_state[sl];
+      if (!(st & kClosed) || W.r_pending[sl] > 0) break;
+      if (lane == 0) {
+        const int32_t sid = W.r_sent[sl];
+        if (st & kFallback) fb_list[atomicAdd(fb_n, 1u)] = sid;
+        else sent_len[sid] = (W.r_count[sl] < max_pieces ? W.r_count[sl] : max_pieces) | W.r_flags[sl];
+      }
+      ++head;
+    }
+    wave_sync();
+  };
+
+  while (true) {
+    if (!cur) {
+      const int64_t s = s_first + tail * stride;
+      if (s >= n_sent) break;
+      if (tail - head == kRing) {  // ring full: make room
+        flush();
+        retire();
+        continue;
+      }
+      cur_slot = (int)(tail % kRing);
+      if (nb0 >= 0) {
+        b0 = nb0;
+        b1 = nb1;
+      } else {
+        b0 = sent_off[s];
+        b1 = sent_off[s + 1];
+      }
+      nb0 = nb1 = -1;
+      if (s + stride < n_sent) {
+        nb0 = sent_off[s + stride];
+        nb1 = sent_off[s + stride + 1];
+      }
+      if (lane == 0) {
+        W.r_b0[cur_slot] = b0;
+        W.r_sent[cur_slot] = (int32_t)s;
+        W.r_count[cur_slot] = 0;
+        W.r_flags[cur_slot] = 0;
+        W.r_pending[cur_slot] = 0;
+        W.r_state[cur_slot] = 0;
+      }
+      wave_sync();
+      pos = b0;
+      cur = true;
+      ++tail;
+    }
+    if (pos < b1) {
+      const uint32_t byte = ppos == pos ? pbyte : (pos + lane < b1 ? text[pos + lane] : 0x20u);
+      const WinResult R = classify_window(T, s_ascii, text, pos, b1, byte, W);
+#ifndef LDDL_TOK_NO_PREFETCH
+      if (R.next < b1) {
+        ppos = R.next;
+        pbyte = R.next + lane < b1 ? text[R.next + lane] : 0x20u;
+      } else if (nb0 >= 0) {  // the next sentence's first window
+        ppos = nb0;
+        pbyte = nb0 + lane < nb1 ? text[nb0 + lane] : 0x20u;
+      }
+#endif
+      if (R.fallback) {
+        if (lane == 0) W.r_state[cur_slot] |= kFallback;
+        pos = b1;
+      } else {
+        const int n = R.n_units;
+        if (lane < n) {
+          const int us = W.us[lane], ue = W.ue[lane];
+          const int ulen = ue - us + 1;
+          W.q_rel[qn + lane] = (int32_t)(pos - b0 + us);
+          W.q_len[qn + lane] = (uint8_t)ulen;
+          W.q_kind[qn + lane] = W.uk[lane];
+          W.q_slot[qn + lane] = (uint8_t)cur_slot;
+          W.q_slow[qn + lane] =
+              ((R.slow >> us) & (ulen >= 64 ? ~0ull : ((1ull << ulen) - 1))) != 0;
+        }
+        if (lane == 0) W.r_pending[cur_slot] += n;
+        wave_sync();
+        qn += n;
+        pos = R.next;
+      }
+    }
+    if (pos >= b1) {
+      if (lane == 0) W.r_state[cur_slot] |= kClosed;
+      wave_sync();
+      cur = false;
+    }
+    if (qn >= 64) {
+      flush();
+      // the open sentence already has max_pieces pieces: the rest of it cannot be kept
+      if (cur && W.r_count[cur_slot] >= max_pieces) pos = b1;
+    }
+    retire();
+  }
+  while (qn > 0) {
+    flush();
+    retire();
+  }
+  retire();
 }
 
 }  // namespace
@@ -512,12 +807,22 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
   // grid-stride over sentences with exactly the resident workgroups (a second wave of
   // workgroups would start only when the first finished: a 2x tail)
   int per_cu = 0;
-  LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_wave_kernel, 64 * kTW, 0));
-  const int64_t want = (n_sent + kTW - 1) / kTW;
-  const int64_t grid = std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1));
-  hipLaunchKernelGGL(tokenize_wave_kernel, dim3((unsigned)grid), dim3(64 * kTW), 0, st, c->tab,
-                     d_text, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + 1,
-                     reinterpret_cast<uint32_t*>(fb));
+  if (path && !strcmp(path, "wave")) {  // diagnostics: one sentence per wavefront, no batching
+    LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_wave_kernel, 64 * kTW, 0));
+    const int64_t want = (n_sent + kTW - 1) / kTW;
+    const int64_t grid = std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1));
+    hipLaunchKernelGGL(tokenize_wave_kernel, dim3((unsigned)grid), dim3(64 * kTW), 0, st, c->tab,
+                       d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + 1,
+                       reinterpret_cast<uint32_t*>(fb));
+  } else {
+    LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_batch_kernel, 64 * kBW, 0));
+    // each wave streams >= ~16 sentences so its unit queue stays full across sentences
+    const int64_t want = (n_sent + 16 * kBW - 1) / (16 * kBW);
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1)));
+    hipLaunchKernelGGL(tokenize_batch_kernel, dim3((unsigned)grid), dim3(64 * kBW), 0, st, c->tab,
+                       d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + 1,
+                       reinterpret_cast<uint32_t*>(fb));
+  }
   const int64_t fgrid = std::min<int64_t>((n_sent + kBlock - 1) / kBlock, (int64_t)n_cu * 2);
   hipLaunchKernelGGL(tokenize_lane_kernel, dim3((unsigned)fgrid), dim3(kBlock), 0, st, c->tab,
                      d_text, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + 1,

@@ -104,12 +104,31 @@ def test_tokenize_adversarial_vs_oracle(case, ctxs):
         np.testing.assert_array_equal(ids, e)
 
 
-def test_tokenize_lane_path_matches_wave_path(ctxs, monkeypatch):
-    """The fallback (lane per sentence) kernel alone gives the same result as the wave kernel."""
+@pytest.mark.parametrize('path', ['lane', 'wave'])
+def test_tokenize_paths_agree(ctxs, monkeypatch, path):
+    """The lane kernel (fallback) and the unbatched wave kernel give the batched kernel's result,
+    on the synthetic corpus and on the adversarial one."""
     from lddl_amd import synth
     corp = synth.generate(seed=99, n_bytes=1 << 20, nonascii_frac=0.05)
-    a = ctxs['uncased'].tokenize_host(corp.text, corp.sent_off)
-    monkeypatch.setenv('LDDL_TOKENIZE_PATH', 'lane')
-    b = ctxs['uncased'].tokenize_host(corp.text, corp.sent_off)
-    np.testing.assert_array_equal(a[1], b[1])
-    np.testing.assert_array_equal(a[0], b[0])
+    for text, off in ((corp.text, corp.sent_off), _adversarial_corpus(seed=21, n=3000)):
+        monkeypatch.delenv('LDDL_TOKENIZE_PATH', raising=False)
+        a = ctxs['uncased'].tokenize_host(text, off)
+        monkeypatch.setenv('LDDL_TOKENIZE_PATH', path)
+        b = ctxs['uncased'].tokenize_host(text, off)
+        np.testing.assert_array_equal(a[1], b[1])
+        np.testing.assert_array_equal(a[0], b[0])
+
+
+def test_tokenize_long_and_empty_sentences(ctxs):
+    """Sentences far beyond 512 pieces (early stop), runs of empty sentences (ring retirement),
+    and one sentence per wave's stream position."""
+    from oracle import oracle as O
+    parts = [b'', b'', b'word ' * 3000, b'', b'a', b'  ', b'[SEP] x ' * 400, b''] * 50
+    text = np.frombuffer(b''.join(parts), np.uint8).copy()
+    off = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.int64)
+    tok = O.Tokenizer(VOCAB_UNCASED, lowercase=True)
+    for mp in (512, 3):
+        ids, o = ctxs['uncased'].tokenize_host(text, off, max_pieces=mp)
+        e, eo = tok.tokenize(text, off, max_pieces=mp)
+        np.testing.assert_array_equal(o, eo)
+        np.testing.assert_array_equal(ids, e)

@@ -28,6 +28,6 @@ torch.cuda.synchronize()
 ms = ev0.elapsed_time(ev1) / n
 pieces = int((sl & ((1 << 30) - 1)).sum())
 import os
-fb = os.environ.get('LDDL_TOKENIZE_PATH', 'wave')
+fb = os.environ.get('LDDL_TOKENIZE_PATH', 'batch')
 print('[{}] tokenize: {:.3f} ms/iter, {:.2f} GB/s text, {:.3f} G pieces/s, pieces={}'.format(
     fb, ms, len(corp.text) / ms / 1e6, pieces / ms / 1e6, pieces), flush=True)
