@@ -133,11 +133,14 @@ def main():
         if args.workload == 'c4':
             bb = balance(ctx, pb, 8, args.seq // 8)
             n_tok = int(bb.tokens.numel()) + 3 * bb.n_rows
+            del bb
         else:
             n_tok = int(pb.tokens.numel()) + 3 * pb.n_pairs
         if ev is not None:
             ev[2].record()
-        return n_tok, pb, sent_len
+        n_pairs = pb.n_pairs
+        del pb  # nothing of a step outlives it (HBM is reused by the next step)
+        return n_tok, n_pairs, sent_len
 
     for _ in range(args.warmup):
         step()
@@ -150,16 +153,16 @@ def main():
     out_tokens = 0
     last = None
     for k in range(args.steps):
-        n, pb, sent_len = step(evs[k])
+        n, n_pairs, sent_len = step(evs[k])
         out_tokens += n
-        last = (pb, sent_len)
+        last = (n_pairs, sent_len)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     tok_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     pair_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
-    pb, sent_len = last
+    n_pairs, sent_len = last
     pieces = int((sent_len & ((1 << 30) - 1)).sum())
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -211,7 +214,7 @@ def main():
             'seq_len': args.seq, 'masking': 'static', 'duplicate_factor': 5,
             'rng': 'replay (CPython MT19937, random.seed per partition)',
             'batch_bytes': int(n_bytes), 'sentences': int(n_sent), 'documents': int(corp.n_doc),
-            'partitions': int(len(part) - 1), 'wordpieces': pieces, 'pairs': int(pb.n_pairs),
+            'partitions': int(len(part) - 1), 'wordpieces': pieces, 'pairs': int(n_pairs),
             'vocab': os.path.basename(VOCAB), 'parallelism': 'dp{} (document shards)'.format(world),
         },
         'stages_ms': {'tokenize': tok_ms,

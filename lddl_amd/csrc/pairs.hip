@@ -459,6 +459,11 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
   uint16_t* cand = jarr + A.seq_r64;                                       // [seq] (slow path)
   uint16_t* tpos = cand + A.seq_r64;                                       // [max_pred]
   int32_t* ttok = reinterpret_cast<int32_t*>(tpos + ((A.max_pred + 7) & ~7));
+  // traceback structures: nxt[v] = first later step that picks position v; pm[v] = lanes of the
+  // current slot chunk whose first pick is v (64-bit, two words); first[l] = lane l's first step
+  uint32_t* s_nxt = reinterpret_cast<uint32_t*>(ttok + ((A.max_pred + 3) & ~3));
+  uint32_t* s_pm = s_nxt + A.seq_r64;
+  uint32_t* s_first = s_pm + 2 * A.seq_r64;
   const int p = blockIdx.x;
   const int lane = threadIdx.x;
   const bool leader = lane == 0;
@@ -566,27 +571,52 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
           int32_t num = (int32_t)rint((double)(na + nb + 3) * A.ratio);  // round(): half-even
           if (num < 1) num = 1;
           if (num > nc) num = nc;
-          // the j draws in registers: jr[k] holds j_{64k + lane}
-          uint32_t jr[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) jr[k] = (64 * k + lane < nc) ? jarr[64 * k + lane] : 0u;
+          // Final slot pp of the shuffled candidates holds original index y: start at v0 = j_pp
+          // (j_0 = 0); the first later step i > pp with j_i = v0 moves it to i, after which
+          // only nxt[] applies (a step i' > i picking position i). nxt[] and the first steps are
+          // built with LDS atomics, so each slot is a short pointer chase instead of a pass over
+          // all nc steps.
+          constexpr uint32_t kNone = 0xFFFFFFFFu;
+          for (int i = lane; i < nc; i += 64) {
+            s_nxt[i] = kNone;
+            s_pm[2 * i] = 0u;
+            s_pm[2 * i + 1] = 0u;
+          }
+          __syncthreads();
+          for (int i = lane + 1; i < nc; i += 64) {
+            const uint32_t v = jarr[i];
+            if (v < (uint32_t)i) atomicMin(&s_nxt[v], (uint32_t)i);
+          }
           for (int32_t c0 = 0; c0 < num; c0 += 64) {
-            // final slot pp (< num) of the shuffled candidates: undo the transpositions
-            // i = pp+1 .. nc-1 to find its original index y
             const int pp = c0 + lane;
-            int y = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              if ((pp >> 6) == k) y = pp == 0 ? 0 : (int)jr[k];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const int i_lo = max(64 * k, c0 + 1), i_hi = min(64 * k + 64, nc);
-              for (int i2 = i_lo; i2 < i_hi; ++i2) {
-                // going backwards y < i2 always holds, so only j_i == y moves it (to i)
-                const int ji = (int)rdlane(jr[k], i2 - 64 * k);
-                y = (ji == y && i2 > pp) ? i2 : y;
+            const bool act = pp < num;
+            const int v0 = act && pp > 0 ? (int)jarr[pp] : 0;
+            s_first[lane] = kNone;
+            if (act) atomicOr(&s_pm[2 * v0 + (lane >> 5)], 1u << (lane & 31));
+            __syncthreads();
+            for (int i = lane + 1; i < nc; i += 64) {
+              const int v = jarr[i];
+              const int lim = i - c0;  // lanes with pp < i
+              if (lim <= 0) continue;
+              uint64_t m = ((uint64_t)s_pm[2 * v + 1] << 32) | s_pm[2 * v];
+              if (lim < 64) m &= (1ull << lim) - 1;
+              while (m) {
+                const int b = __ffsll((unsigned long long)m) - 1;
+                atomicMin(&s_first[b], (uint32_t)i);
+                m &= m - 1;
               }
             }
+            __syncthreads();
+            int y = v0;
+            if (act) {
+              const uint32_t f = s_first[lane];
+              if (f != kNone) {
+                y = (int)f;
+                for (uint32_t nx = s_nxt[y]; nx != kNone; nx = s_nxt[y]) y = (int)nx;
+              }
+              s_pm[2 * v0 + (lane >> 5)] = 0u;  // reset for the next chunk
+            }
+            __syncthreads();
             const int cval = slow ? (int)cand[y < nc ? y : 0] : (y < na ? y + 1 : y + 2);
             STAMP_ADD(3, st_t);
             const int cmax = min(64, num - c0);
@@ -971,7 +1001,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
 #endif
   if (prm->seq > 512) TRY((set_error("replay planner supports target_seq_length <= 512"), -1));
   const size_t lds = 4 * kN + 4 * (kDocLds + 4) + 4 * (size_t)A.seq_r64 +
-                     2 * ((max_pred + 7) & ~7) + 4 * max_pred + 16;
+                     2 * ((max_pred + 7) & ~7) + 4 * ((max_pred + 3) & ~3) +
+                     12 * (size_t)A.seq_r64 + 4 * 64 + 16;
   // mask pool: sized from the kept tokens (expected use ~0.15 * 1.5 * dup * tokens + pairs); a
   // plan that outgrows it reports the exact size and is planned again (deterministic replay)
   unsigned long long* pool_ctl;  // [0] used, [1] overflow flag

@@ -37,3 +37,4 @@ for it in range(2):
     print('pairs {:.1f} ms; balance: {}'.format((t1 - t0) * 1e3, ', '.join(
         '{} {:.1f} ms'.format(k, (tm[k] - tm[p]) * 1e3) for p, k in zip(keys, keys[1:]))),
         flush=True)
+    del pb, bb
