@@ -108,7 +108,10 @@ __global__ void part_offsets_kernel(const int64_t* part_doc_off, int64_t n_part,
 // flow); only parallel phases (twist, temper, speculative shuffle draws) use the lanes.
 // ---------------------------------------------------------------------------------------------
 constexpr int kN = 624, kM = 397;
-constexpr int kFyTail = 16;           // fy_draws: steps i < kFyTail are drawn sequentially
+#ifndef LDDL_FY_TAIL
+#define LDDL_FY_TAIL 32
+#endif
+constexpr int kFyTail = LDDL_FY_TAIL;  // fy_draws: steps i < kFyTail are drawn sequentially
 constexpr int64_t kPoolChunk = 4096;  // mask pool entries reserved per atomic
 
 __device__ inline int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
