@@ -122,6 +122,8 @@ def main():
     part_off = torch.from_numpy(part).to(dev)
     part_seed = torch.from_numpy(seeds).to(dev)
 
+    diag = {}  # {'balance': {}}: balance() records synchronised phase times (untimed step only)
+
     def step(ev=None):
         if ev is not None:
             ev[0].record()
@@ -131,16 +133,17 @@ def main():
         pb = make_pairs(ctx, sent_off, ids, sent_len, doc_off, part_off, part_seed, seq=args.seq,
                         dup=5, masking=True, short_seq_prob=0.1, masked_lm_ratio=0.15)
         if args.workload == 'c4':
-            bb = balance(ctx, pb, 8, args.seq // 8)
+            bb = balance(ctx, pb, 8, args.seq // 8, timings=diag.get('balance'))
             n_tok = int(bb.tokens.numel()) + 3 * bb.n_rows
             del bb
         else:
             n_tok = int(pb.tokens.numel()) + 3 * pb.n_pairs
         if ev is not None:
             ev[2].record()
-        n_pairs = pb.n_pairs
+        st = {'pairs': pb.n_pairs, 'masked': pb.n_masked, 'plan_ms': pb.plan_ms,
+              'kept_sent': pb.n_kept_sentences, 'kept_doc': pb.n_kept_documents}
         del pb  # nothing of a step outlives it (HBM is reused by the next step)
-        return n_tok, n_pairs, sent_len
+        return n_tok, st, sent_len
 
     for _ in range(args.warmup):
         step()
@@ -151,19 +154,28 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     out_tokens = 0
-    last = None
+    stats = []
     for k in range(args.steps):
-        n, n_pairs, sent_len = step(evs[k])
+        n, st, sent_len = step(evs[k])
         out_tokens += n
-        last = (n_pairs, sent_len)
+        stats.append(st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     tok_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     pair_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
-    n_pairs, sent_len = last
+    plan_ms = float(np.mean([s['plan_ms'] for s in stats]))
+    st = stats[-1]
+    n_pairs = st['pairs']
     pieces = int((sent_len & ((1 << 30) - 1)).sum())
+    bal_ms = None
+    if args.workload == 'c4':  # one more, untimed step with the balance phases timed
+        diag['balance'] = {}
+        step()
+        bt = diag.pop('balance')
+        keys = list(bt)
+        bal_ms = {k: (bt[k] - bt[p]) * 1e3 for p, k in zip(keys, keys[1:])}
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -174,9 +186,17 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
-    # roofline of the dominant kernel (tokenizer): algorithmic bytes per launch =
-    # text bytes read + sentence offsets read (8 B each) + ids written (4 B / piece) + sent_len (4 B)
+    # Rooflines. Dominant kernel = plan_replay_kernel (CPython-exact pair/mask
+    # planner); its algorithmic bytes per launch: sentence lengths read per duplicate pass
+    # (4 B x dup x kept sentences) + document offsets (8 B x dup x kept documents) + per pair a
+    # 32-B descriptor, 4-B shuffle draw, 4-B mask count and 8-B mask offset + 6 B per masked
+    # position (2-B position + 4-B token) — all writes to HBM, the MT19937 state stays in LDS.
     n_bytes, n_sent = corp.text.size, corp.n_sent
+    plan_bytes = (4 * 5 * st['kept_sent'] + 8 * 5 * st['kept_doc'] + 48 * n_pairs +
+                  6 * st['masked'])
+    plan_gbs = plan_bytes / (plan_ms * 1e-3) / 1e9 if plan_ms > 0 else 0.0
+    # tokenizer: text bytes read + sentence offsets read (8 B each) + ids written (4 B / piece)
+    # + sent_len (4 B / sentence)
     tok_bytes = n_bytes + 8 * (n_sent + 1) + 4 * pieces + 4 * n_sent
     achieved = tok_bytes / (tok_ms * 1e-3) / 1e9
     prof_traffic = None
@@ -220,10 +240,18 @@ def main():
         'stages_ms': {'tokenize': tok_ms,
                       ('pairs_plan_and_gather' if args.workload == 'c2' else
                        'pairs_bin_and_balance'): pair_ms},
-        'roofline': {'kernel': 'tokenize_wave_kernel', 'bound': 'hbm', 'achieved': achieved,
-                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
-                     'traffic': prof_traffic, 'algorithmic_bytes_per_launch': tok_bytes},
+        'roofline': {'kernel': 'plan_replay_kernel', 'bound': 'hbm', 'achieved': plan_gbs,
+                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': plan_gbs / HBM_PEAK_GBS,
+                     'traffic': None, 'algorithmic_bytes_per_launch': plan_bytes,
+                     'launch_ms': plan_ms,
+                     'note': 'issue-bound on the CU scalar unit, not HBM (DESIGN.md 4)'},
+        'roofline_tokenizer': {'kernel': 'tokenize_batch_kernel', 'bound': 'hbm',
+                               'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                               'frac': achieved / HBM_PEAK_GBS, 'traffic': prof_traffic,
+                               'algorithmic_bytes_per_launch': tok_bytes, 'launch_ms': tok_ms},
     }
+    if bal_ms is not None:
+        res['balance_phases_ms_untimed_step'] = bal_ms
     if world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(corp, part, seeds, args)
     print(json.dumps(res), flush=True)

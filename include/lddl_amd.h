@@ -116,6 +116,8 @@ int lddl_pairs_destroy(lddl_pairs* plan, void* stream);
 /* d_part_pair_off[n_part + 1]: first output pair of each partition (pairs are emitted in
  * partition order), i.e. the row ranges of the reference's per-partition outputs. */
 int lddl_pairs_part_offsets(lddl_pairs* plan, void* stream, int64_t* d_part_pair_off);
+/* Device time (ms, HIP events on the plan's stream) of the planner kernel of lddl_pairs_plan. */
+int lddl_pairs_plan_ms(const lddl_pairs* plan, float* ms);
 
 /* ---------------------------------------------------------------------------------------------
  * Per-partition sequence-length binning.

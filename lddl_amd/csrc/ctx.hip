@@ -37,6 +37,15 @@ extern "C" int lddl_ctx_create(int device, const uint8_t* norm_table, int64_t ta
   if (table_len < need) LDDL_FAIL(-1, "truncated normaliser table (%lld < %lld)",
                                   (long long)table_len, (long long)need);
   LDDL_HIP(hipSetDevice(device));
+  // keep stream-ordered allocations (planner / tokenizer temporaries) cached across calls
+  // instead of returning them to the driver at every synchronisation
+  {
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+      uint64_t thr = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+  }
   auto* c = new lddl_ctx();
   c->device = device;
 

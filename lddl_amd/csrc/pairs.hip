@@ -773,7 +773,8 @@ struct GatherArgs {
   const uint16_t* mpos;
   const int32_t* mtok;
   const int64_t* moff;
-  int32_t max_pred, masking;
+  int32_t max_pred, masking, seq;
+  int64_t n_kept_sent;
   int64_t n_pairs;
   const int64_t* tok_off;
   const int64_t* pos_off;
@@ -787,41 +788,70 @@ struct GatherArgs {
 constexpr int kGatherWaves = 4;
 constexpr int kMaxPredLds = 1024;
 
-// Copy `count` tokens of the span starting at kept sentence k0 after skipping `front` tokens to
-// out[0..count); output index t has sequence position pos0 + t.
-__device__ void copy_span(const GatherArgs& G, int64_t k0, int32_t front, int32_t count, int32_t* out,
-                          int32_t pos0, const uint16_t* mp, const int32_t* mt, int32_t nm,
+constexpr int kMaxSeqLds = 1024;  // gather: position -> mask map entries per wave
+
+// Copy `count` tokens of the span that starts at kept sentence k0 after skipping `front` tokens
+// to out[0..count); output index t has sequence position pos0 + t. The span's sentence lengths
+// and starts are loaded 64 at a time (one per lane) and prefix-summed, so the copy of each
+// 64-token chunk only walks the few sentences that overlap it. Masked positions are found in the
+// wave's LDS map (position -> 1 + index into the pair's sorted masks, 0 = unmasked).
+__device__ void copy_span(const GatherArgs& G, int64_t k0, int32_t front, int32_t count,
+                          int32_t* out, int32_t pos0, const uint16_t* map, const int32_t* mt,
                           int32_t* lab) {
-  int32_t t = 0;
   const int lane = lane_id();
-  for (int64_t k = k0; t < count; ++k) {
-    const int32_t l = G.ks_len[k] & kLenMask;
-    if (front >= l) { front -= l; continue; }
-    const int32_t take = min(l - front, count - t);
-    const int32_t* srcp = G.ids + G.ks_start[k] + front;
-    for (int32_t x = lane; x < take; x += 64) {
-      int32_t tok = srcp[x];
-      if (nm) {
-        const int32_t pos = pos0 + t + x;
-        int lo = 0, hi = nm;  // binary search in the sorted masked positions
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (mp[mid] < pos) lo = mid + 1; else hi = mid;
-        }
-        if (lo < nm && mp[lo] == pos) {
-          lab[lo] = tok;
-          if (mt[lo] != kKeep) tok = mt[lo];
-        }
+  int32_t t = 0;       // tokens written
+  int64_t kb = k0;     // first sentence of the current 64-sentence batch
+  int32_t skip = front;
+  while (t < count) {
+    // batch of up to 64 sentences: inclusive prefix of lengths
+    const bool ok = kb + lane < G.n_kept_sent;  // sentences past the span are harmless
+    const int32_t myl = ok ? G.ks_len[kb + lane] & kLenMask : 0;
+    const int64_t mys = ok ? G.ks_start[kb + lane] : 0;
+    const int32_t incl = wave_incl_scan(myl);
+    const int32_t tot = __shfl(incl, 63, 64);
+    // tokens of this batch usable by the span: [skip, tot)
+    const int32_t avail = tot - skip;
+    if (avail <= 0) {
+      skip -= tot;
+      kb += 64;
+      continue;
+    }
+    const int32_t take = min(avail, count - t);
+    for (int32_t c0 = 0; c0 < take; c0 += 64) {
+      const int32_t x = skip + c0 + lane;  // position inside the batch's concatenation
+      const bool act = c0 + lane < take;
+      // sentence of x: number of inclusive prefixes <= x (sentences overlapping the chunk)
+      const int32_t lo_x = skip + c0, hi_x = skip + min(c0 + 64, take) - 1;
+      int j = 0;
+      // first sentence overlapping the chunk: count of prefixes <= lo_x
+      j = __popcll(__ballot(incl <= lo_x));
+      int32_t tok = 0;
+      while (true) {
+        const int32_t e = __shfl(incl, j, 64);      // end of sentence j (exclusive)
+        const int32_t bgn = e - __shfl(myl, j, 64);
+        const int64_t st = __shfl(mys, j, 64);
+        if (act && x >= bgn && x < e) tok = G.ids[st + (x - bgn)];
+        if (e > hi_x) break;
+        ++j;
       }
-      out[t + x] = tok;
+      if (act) {
+        const int32_t pos = pos0 + t + c0 + lane;
+        const int m = map ? (int)map[pos] : 0;
+        if (m) {
+          lab[m - 1] = tok;
+          if (mt[m - 1] != kKeep) tok = mt[m - 1];
+        }
+        out[t + c0 + lane] = tok;
+      }
     }
     t += take;
-    front = 0;
+    skip = 0;
+    kb += 64;
   }
 }
 
 __global__ void __launch_bounds__(64 * kGatherWaves) gather_kernel(GatherArgs G) {
-  __shared__ uint16_t s_pos[kGatherWaves][kMaxPredLds];
+  __shared__ uint16_t s_map[kGatherWaves][kMaxSeqLds];
   __shared__ int32_t s_tok[kGatherWaves][kMaxPredLds];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * kGatherWaves + w;
@@ -829,24 +859,30 @@ __global__ void __launch_bounds__(64 * kGatherWaves) gather_kernel(GatherArgs G)
   const int64_t slot = active ? G.src[q] : 0;
   int32_t nm = 0;
   int32_t* lab = nullptr;
+  uint16_t* map = s_map[w];
   if (G.masking && active) {
+    for (int j = lane; j < G.seq; j += 64) map[j] = 0;
     nm = G.nmask[slot];
+  }
+  __syncthreads();
+  if (G.masking && active) {
     const int64_t mb = G.moff[slot];
     for (int j = lane; j < nm; j += 64) {
       const uint16_t pv = G.mpos[mb + j];
-      s_pos[w][j] = pv;
+      map[pv] = (uint16_t)(j + 1);
       s_tok[w][j] = G.mtok[mb + j];
       G.out_pos[G.pos_off[q] + j] = pv;
     }
     lab = G.out_lab + G.pos_off[q];
   }
-  __syncthreads();  // masked positions visible to every lane of the wave
+  __syncthreads();  // the map is visible to every lane of the wave
   if (!active) return;
   const PairDesc d = G.desc[slot];
   const int32_t nb = d.nb_rn & 0x7FFFFFFF;
   int32_t* out = G.out_tok + G.tok_off[q];
-  copy_span(G, d.a_ks, d.a_front, d.na, out, 1, s_pos[w], s_tok[w], nm, lab);
-  copy_span(G, d.b_ks, d.b_front, nb, out + d.na, d.na + 2, s_pos[w], s_tok[w], nm, lab);
+  const uint16_t* mp = G.masking ? map : nullptr;
+  copy_span(G, d.a_ks, d.a_front, d.na, out, 1, mp, s_tok[w], lab);
+  copy_span(G, d.b_ks, d.b_front, nb, out + d.na, d.na + 2, mp, s_tok[w], lab);
   if (lane == 0) {
     G.len_a[q] = d.na;
     G.is_rn[q] = (uint8_t)((uint32_t)d.nb_rn >> 31);
@@ -861,7 +897,7 @@ using namespace lddl;
 // Device-resident plan of one batch of partitions (library-owned temporaries).
 struct lddl_pairs {
   int device = 0;
-  int32_t masking = 0, max_pred = 0;
+  int32_t masking = 0, max_pred = 0, seq = 0;
   int64_t n_part = 0, n_pairs = 0, n_tokens = 0, n_masked = 0, n_kept_sent = 0, n_kept_doc = 0;
   std::vector<void*> allocs;
   // views
@@ -874,6 +910,7 @@ struct lddl_pairs {
   int64_t* moff = nullptr;
   int64_t *src = nullptr, *tok_off = nullptr, *pos_off = nullptr;
   int64_t* part_base = nullptr;  // [n_part + 1] first output pair of each partition
+  hipEvent_t ev[2] = {nullptr, nullptr};  // around the last plan_replay_kernel launch
 
   template <typename T>
   int alloc(T** p, int64_t n, hipStream_t st) {
@@ -884,6 +921,11 @@ struct lddl_pairs {
   void release(hipStream_t st) {
     for (void* p : allocs) (void)hipFreeAsync(p, st);
     allocs.clear();
+    for (hipEvent_t& e : ev)
+      if (e) {
+        (void)hipEventDestroy(e);
+        e = nullptr;
+      }
   }
 };
 
@@ -924,7 +966,10 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   P->device = c->device;
   P->n_part = n_part;
   P->masking = prm->masking;
+  P->seq = prm->seq;
   P->ids = d_ids;
+  TRY(hipEventCreate(&P->ev[0]) == hipSuccess && hipEventCreate(&P->ev[1]) == hipSuccess
+          ? 0 : (set_error("hipEventCreate failed"), -100));
   int64_t *ks_pos, *kd_pos, *scratch, *part_npairs, *part_base;
   const int64_t nscr = scan_scratch_elems(std::max(n_sent, n_doc) + n_part + 1);
   TRY(P->alloc(&scratch, nscr, st));
@@ -1035,8 +1080,10 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     A.pool_cap = cap;
     A.pool_used = pool_ctl;
     A.overflow = reinterpret_cast<int32_t*>(pool_ctl + 1);
+    LDDL_HIP(hipEventRecord(P->ev[0], st));
     hipLaunchKernelGGL(plan_replay_kernel, dim3((unsigned)n_part), dim3(64), lds, st, A);
     LDDL_HIP(hipGetLastError());
+    LDDL_HIP(hipEventRecord(P->ev[1], st));
     if (!prm->masking) break;
     unsigned long long ctl[2];
     LDDL_HIP(hipMemcpyAsync(ctl, pool_ctl, 16, hipMemcpyDeviceToHost, st));
@@ -1117,9 +1164,28 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
   if (!P) LDDL_FAIL(-1, "null plan");
   hipStream_t st = as_stream(stream);
   if (P->n_pairs == 0) return 0;
-  GatherArgs G{P->ks_start, P->ks_len, P->ids, P->src, P->desc, P->nmask, P->mpos, P->mtok, P->moff,
-               P->max_pred, P->masking, P->n_pairs, P->tok_off, P->pos_off, d_tokens, d_len_a,
-               d_is_rn, d_pos, d_lab};
+  GatherArgs G{};
+  G.ks_start = P->ks_start;
+  G.ks_len = P->ks_len;
+  G.ids = P->ids;
+  G.src = P->src;
+  G.desc = P->desc;
+  G.nmask = P->nmask;
+  G.mpos = P->mpos;
+  G.mtok = P->mtok;
+  G.moff = P->moff;
+  G.max_pred = P->max_pred;
+  G.masking = P->masking;
+  G.seq = P->seq;
+  G.n_kept_sent = P->n_kept_sent;
+  G.n_pairs = P->n_pairs;
+  G.tok_off = P->tok_off;
+  G.pos_off = P->pos_off;
+  G.out_tok = d_tokens;
+  G.len_a = d_len_a;
+  G.is_rn = d_is_rn;
+  G.out_pos = d_pos;
+  G.out_lab = d_lab;
   const int64_t grid = (P->n_pairs + kGatherWaves - 1) / kGatherWaves;
   hipLaunchKernelGGL(gather_kernel, dim3((unsigned)grid), dim3(64 * kGatherWaves), 0, st, G);
   LDDL_HIP(hipGetLastError());
@@ -1134,6 +1200,13 @@ extern "C" int lddl_pairs_destroy(lddl_pairs* P, void* stream) {
   if (!P) return 0;
   P->release(as_stream(stream));
   delete P;
+  return 0;
+}
+
+extern "C" int lddl_pairs_plan_ms(const lddl_pairs* P, float* ms) {
+  if (!P || !ms) LDDL_FAIL(-1, "null argument");
+  *ms = 0.f;
+  if (P->n_part && P->ev[0]) LDDL_HIP(hipEventElapsedTime(ms, P->ev[0], P->ev[1]));
   return 0;
 }
 

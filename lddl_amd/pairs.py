@@ -28,6 +28,8 @@ class PairBatch:
     n_kept_sentences: int = 0
     n_kept_documents: int = 0
     part_off: torch.Tensor = None  # int64 [n_part + 1]: pair range of each partition
+    plan_ms: float = 0.0           # device time of the planner kernel (HIP events)
+    n_masked: int = 0
 
     @property
     def n_pairs(self):
@@ -86,7 +88,9 @@ def make_pairs(ctx, sent_off, ids, sent_len, doc_sent_off, part_doc_off, part_se
                                   _ptr(pos), _ptr(labels), _ptr(pos_off)))
         part_off = torch.empty(n_part + 1, dtype=torch.int64, device=dev)
         check(lib.lddl_pairs_part_offsets(h, st, _ptr(part_off)))
+        ms = ctypes.c_float()
+        check(lib.lddl_pairs_plan_ms(h, ctypes.byref(ms)))
     finally:
         lib.lddl_pairs_destroy(h, st)
     return PairBatch(tokens, tok_off, len_a, is_rn, pos, labels, pos_off, int(counts[3]),
-                     int(counts[4]), part_off)
+                     int(counts[4]), part_off, float(ms.value), n_mask)
