@@ -108,10 +108,6 @@ __global__ void part_offsets_kernel(const int64_t* part_doc_off, int64_t n_part,
 // flow); only parallel phases (twist, temper, speculative shuffle draws) use the lanes.
 // ---------------------------------------------------------------------------------------------
 constexpr int kN = 624, kM = 397;
-#ifndef LDDL_FY_TAIL
-#define LDDL_FY_TAIL 32
-#endif
-constexpr int kFyTail = LDDL_FY_TAIL;  // fy_draws: steps i < kFyTail are drawn sequentially
 constexpr int64_t kPoolChunk = 4096;  // mask pool entries reserved per atomic
 
 __device__ inline int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -215,62 +211,38 @@ struct WaveRng {
     return v;
   }
   // Fisher-Yates draws of random.shuffle over n items: j_i = _randbelow(i+1), i = n-1 .. 1,
-  // delivered as sink(i, j_i). Wave-parallel over 64 words at a time: while k = bit_length(s+1)
-  // is fixed, word t is rejected iff R_t < c_t with c_t = (w_t >> (32-k)) - s0 + t and R_t the
-  // rejections before t. The sets {t : c_t > m} are nested, so the m-th rejection is the first
-  // lane after the (m-1)-th with c_t > m: one compare (= ballot) and a few scalar ops each.
+  // delivered as sink(i, j_i). Wave-parallel over 64 words at a time. Word t of the window is
+  // drawn for step i_t = s0 - t + R_t (R_t = rejections before t) and rejected iff
+  // (w_t >> (32 - bit_length(i_t + 1))) > i_t. R is the fixed point of R_t = #{u < t : rejected
+  // under R_u}, found by Jacobi iteration on ballots: the recurrence is causal, so every pass
+  // fixes at least the first wrong lane, and in practice 4-8 passes settle a whole window across
+  // any number of bit-length buckets. Each pass is a handful of VALU ops and one ballot.
   template <typename Sink>
   __device__ void fy_draws(int64_t n, Sink sink) {
     const int lane = threadIdx.x;
     const uint64_t lt_mask = (1ull << lane) - 1;
     int32_t s0 = (int32_t)(n - 1);  // next step (uniform); n < 2^30 (host-checked)
     while (s0 >= 1) {
-      if (s0 < kFyTail) {
-        // the last buckets (bit_length <= 4) are a handful of draws each: plain sequential
-        // draws cost less than one window pass per bucket
-        wbase = -1024;
-        while (s0 >= 1) {
-          const uint32_t j = randbelow((uint32_t)(s0 + 1));
-          if (lane == 0) sink((int64_t)s0, j);
-          --s0;
-        }
-        break;
-      }
       if (mti >= kN) twist();
-      const int k = 32 - __clz((uint32_t)(s0 + 1));
-      const int32_t s_lo = (1 << (k - 1)) - 1 > 1 ? (1 << (k - 1)) - 1 : 1;
-      const int32_t need = s0 - s_lo + 1;  // steps served by this k
       const int L = min(64, kN - mti);
       const uint32_t w = lane < L ? temper(mt[mti + lane]) : 0u;
-      const int32_t x = (int32_t)(w >> (32 - k));
-      // word t is rejected iff c_t > R_t (R_t = rejections before t); clamp keeps it in int range
-      const int32_t c = lane < L ? min(max(x - s0 + lane, -1), 127) : -1;
-      // the m-th rejection is the first lane after the (m-1)-th with c > m. The nested sets
-      // {c > m} are ballotted 8 at a time by independent compares, then resolved by a pure
-      // scalar chain (no VALU->SALU round trip per rejection).
-      uint64_t rej = 0;
-      int pos = 0;
-      for (int m0 = 0; m0 < 64; m0 += 8) {
-        uint64_t B[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) B[q] = __ballot(c > m0 + q);
-        bool done = false;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const uint64_t bm = B[q] & (pos < 64 ? (~0ull << pos) : 0ull);
-          if (!bm) { done = true; break; }
-          const int r = __ffsll((unsigned long long)bm) - 1;
-          rej |= 1ull << r;
-          pos = r + 1;
-        }
-        if (done || pos >= L) break;
+      int32_t R = 0;
+      uint64_t rej = ~0ull;
+      int32_t i = 0;
+      uint32_t x = 0;
+      for (int it = 0; it < 66; ++it) {
+        i = s0 - lane + R;
+        const int k = 32 - __clz((uint32_t)(i + 1));
+        x = i >= 1 ? w >> (32 - k) : 0u;
+        const uint64_t bm = __ballot(lane < L && i >= 1 && x > (uint32_t)i);
+        if (bm == rej) break;
+        rej = bm;
+        R = __popcll(rej & lt_mask);
       }
-      const int32_t R = __popcll(rej & lt_mask);
-      const int32_t rank = lane - R;  // accepted words before this lane
-      const uint64_t consumed = __ballot(lane < L && rank < need);
-      const int E = __popcll(consumed);
-      const bool accepted = lane < E && !((rej >> lane) & 1ull);
-      if (accepted) sink((int64_t)(s0 - rank), (uint32_t)x);
+      // words consumed: up to the first lane past the last step (i < 1) or the window end
+      const uint64_t fin = __ballot(lane < L && i < 1);
+      const int E = fin ? __ffsll((unsigned long long)fin) - 1 : L;
+      if (lane < E && !((rej >> lane) & 1ull)) sink((int64_t)i, x);
       mti += E;
       s0 -= E - __popcll(rej & (E >= 64 ? ~0ull : ((1ull << E) - 1)));
       s0 = uni(s0);
