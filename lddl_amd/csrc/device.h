@@ -95,6 +95,13 @@ __device__ inline T wave_incl_scan(T v) {
   return v;
 }
 
+// LDS written by some lanes of a wave becomes visible to all lanes of that wave
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <typename T>
 __device__ inline T wave_sum(T v) {
 #pragma unroll

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "ctx.h"
@@ -861,6 +862,179 @@ __global__ void __launch_bounds__(64 * kGatherWaves) gather_kernel(GatherArgs G)
   }
 }
 
+// Gather, batched: each wave copies K consecutive output pairs. The 2K spans (A and B of each
+// pair) get Gs-lane segments of a small sentence table (lane j of a segment holds sentence k0+j:
+// length, start, inclusive length prefix), so a span costs Gs*12 bytes of table reads instead of
+// 64*12. Output token x of a pair is position x of A's window (x < na) or of B's; its sentence is
+// found by walking the few table entries that overlap its 64-token chunk. All K*C token loads are
+// issued before any is consumed, which is what hides HBM latency here (one pair per wave left
+// ~80% of wave cycles waiting on dependent loads). A span whose window needs more than Gs
+// sentences takes the sequential copy_span path (uniform branch, rare).
+constexpr int kG3Waves = 4;
+
+template <int Gs, int K, int C>
+__global__ void __launch_bounds__(64 * kG3Waves) gather3_kernel(GatherArgs G, int32_t map_len) {
+  constexpr int T = (2 * K * Gs + 63) / 64;  // table registers
+  constexpr int SPR = 64 / Gs;               // spans per table register
+  extern __shared__ __attribute__((aligned(16))) uint8_t g3_smem[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int sj = lane & (Gs - 1), sseg = lane / Gs;
+  uint16_t* maps = reinterpret_cast<uint16_t*>(g3_smem) + (size_t)w * K * map_len;
+  int32_t* toks = reinterpret_cast<int32_t*>(g3_smem + (size_t)kG3Waves * K * map_len * 2) +
+                  (size_t)w * K * G.max_pred;
+  const int64_t qb = ((int64_t)blockIdx.x * kG3Waves + w) * K;
+
+  int64_t slot[K], tof[K];
+  int64_t aks[K], bks[K];
+  int32_t afr[K], na[K], bfr[K], nb[K], rn[K], nm[K];
+  bool act[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    act[k] = qb + k < G.n_pairs;
+    slot[k] = act[k] ? G.src[qb + k] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    PairDesc d{0, 0, 0, 0, 0, 0};
+    if (act[k]) d = G.desc[slot[k]];
+    aks[k] = d.a_ks;
+    bks[k] = d.b_ks;
+    afr[k] = d.a_front;
+    na[k] = d.na;
+    bfr[k] = d.b_front;
+    nb[k] = d.nb_rn & 0x7FFFFFFF;
+    rn[k] = (int32_t)((uint32_t)d.nb_rn >> 31);
+    tof[k] = act[k] ? G.tok_off[qb + k] : 0;
+    nm[k] = (G.masking && act[k]) ? G.nmask[slot[k]] : 0;
+  }
+  // sentence tables
+  int32_t tlen[T], tinc[T];
+  int64_t tst[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int s = t * SPR + sseg;  // this lane's span
+    int64_t k0 = -1;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (s == 2 * k && act[k]) k0 = aks[k];
+      if (s == 2 * k + 1 && act[k]) k0 = bks[k];
+    }
+    const bool ok = k0 >= 0 && k0 + sj < G.n_kept_sent;
+    tlen[t] = ok ? G.ks_len[k0 + sj] & kLenMask : 0;
+    tst[t] = ok ? G.ks_start[k0 + sj] : 0;
+  }
+  // masks: position -> 1 + index map and replacement table per pair
+  if (G.masking) {
+    uint32_t* m32 = reinterpret_cast<uint32_t*>(maps);
+    for (int i = lane; i < K * map_len / 2; i += 64) m32[i] = 0u;
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (!nm[k]) continue;
+      const int64_t mb = G.moff[slot[k]], po = G.pos_off[qb + k];
+      for (int j = lane; j < nm[k]; j += 64) {
+        const uint16_t pv = G.mpos[mb + j];
+        maps[k * map_len + pv] = (uint16_t)(j + 1);
+        toks[k * G.max_pred + j] = G.mtok[mb + j];
+        G.out_pos[po + j] = pv;
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    int32_t v = tlen[t];
+#pragma unroll
+    for (int dd = 1; dd < Gs; dd <<= 1) {
+      const int32_t o = __shfl_up(v, dd, Gs);
+      if (sj >= dd) v += o;
+    }
+    tinc[t] = v;
+  }
+  // fast path check per pair: both windows end inside their table segments
+  bool fast[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int sa = 2 * k, sb = 2 * k + 1;
+    const int32_t ea = (int32_t)__builtin_amdgcn_readlane(tinc[sa / SPR], (sa % SPR) * Gs + Gs - 1);
+    const int32_t eb = (int32_t)__builtin_amdgcn_readlane(tinc[sb / SPR], (sb % SPR) * Gs + Gs - 1);
+    fast[k] = act[k] && ea >= afr[k] + na[k] && eb >= bfr[k] + nb[k];
+  }
+  // source addresses
+  int64_t addr[K][C];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) addr[k][c] = -1;
+    if (!fast[k]) continue;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // h = 0: A, 1: B
+      const int s = 2 * k + h;
+      const int tr = s / SPR, sb0 = (s % SPR) * Gs;
+      const int32_t wlo = h ? na[k] : 0, whi = h ? na[k] + nb[k] : na[k];  // x range of the span
+      const int32_t fr = h ? bfr[k] : afr[k];
+      const uint64_t segm = (Gs == 64 ? ~0ull : ((1ull << Gs) - 1)) << sb0;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const int32_t x0 = c * 64 > wlo ? c * 64 : wlo, x1 = (c * 64 + 64 < whi ? c * 64 + 64 : whi);
+        if (x0 >= x1) continue;  // uniform
+        const int32_t x = c * 64 + lane;
+        const bool mine = x >= x0 && x < x1;
+        const int32_t y = fr + (x - wlo);  // offset in the span's concatenation
+        const int32_t lo = fr + (x0 - wlo), hi = fr + (x1 - 1 - wlo);
+        int j = __popcll(__ballot(tinc[tr] <= lo) & segm);
+        while (true) {
+          const int32_t e = __builtin_amdgcn_readlane(tinc[tr], sb0 + j);
+          const int32_t bgn = e - __builtin_amdgcn_readlane(tlen[tr], sb0 + j);
+          const int64_t st = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(tst[tr] >> 32), sb0 + j)
+                              << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)tst[tr], sb0 + j);
+          if (mine && y >= bgn && y < e) addr[k][c] = st + (y - bgn);
+          if (e > hi || j == Gs - 1) break;
+          ++j;
+        }
+      }
+    }
+  }
+  int32_t tok[K][C];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int c = 0; c < C; ++c) tok[k][c] = addr[k][c] >= 0 ? G.ids[addr[k][c]] : 0;
+  if (G.masking) wave_sync();  // maps complete
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (!act[k]) continue;
+    const uint16_t* map = G.masking ? maps + k * map_len : nullptr;
+    const int32_t* mt = toks + k * G.max_pred;
+    int32_t* lab = G.masking ? G.out_lab + G.pos_off[qb + k] : nullptr;
+    int32_t* out = G.out_tok + tof[k];
+    if (fast[k]) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const int32_t x = c * 64 + lane;
+        if (x < na[k] + nb[k]) {
+          int32_t v = tok[k][c];
+          if (map) {
+            const int m = map[x < na[k] ? x + 1 : x + 2];
+            if (m) {
+              lab[m - 1] = v;
+              if (mt[m - 1] != kKeep) v = mt[m - 1];
+            }
+          }
+          out[x] = v;
+        }
+      }
+    } else {
+      copy_span(G, aks[k], afr[k], na[k], out, 1, map, mt, lab);
+      copy_span(G, bks[k], bfr[k], nb[k], out + na[k], na[k] + 2, map, mt, lab);
+    }
+    if (lane == 0) {
+      G.len_a[qb + k] = na[k];
+      G.is_rn[qb + k] = (uint8_t)rn[k];
+    }
+  }
+}
+
 }  // namespace
 }  // namespace lddl
 
@@ -1158,8 +1332,27 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
   G.is_rn = d_is_rn;
   G.out_pos = d_pos;
   G.out_lab = d_lab;
-  const int64_t grid = (P->n_pairs + kGatherWaves - 1) / kGatherWaves;
-  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)grid), dim3(64 * kGatherWaves), 0, st, G);
+  static const char* gpath = getenv("LDDL_GATHER");  // "v2": one pair per wave (A/B runs)
+  const int32_t map_len = (P->seq + 1) & ~1;
+  auto launch3 = [&](auto kern, int K) {
+    const int64_t per_wg = (int64_t)K * kG3Waves;
+    const size_t lds = P->masking ? (size_t)kG3Waves * K * (2 * map_len + 4 * P->max_pred) : 0;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((P->n_pairs + per_wg - 1) / per_wg)),
+                       dim3(64 * kG3Waves), lds, st, G, map_len);
+  };
+  if (gpath && !strcmp(gpath, "v2")) {
+    const int64_t grid = (P->n_pairs + kGatherWaves - 1) / kGatherWaves;
+    hipLaunchKernelGGL(gather_kernel, dim3((unsigned)grid), dim3(64 * kGatherWaves), 0, st, G);
+  } else if (P->seq <= 128) {
+    launch3(gather3_kernel<8, 4, 2>, 4);
+  } else if (P->seq <= 256) {
+    launch3(gather3_kernel<16, 4, 4>, 4);
+  } else if (P->seq <= 512) {
+    launch3(gather3_kernel<32, 2, 8>, 2);
+  } else {
+    const int64_t grid = (P->n_pairs + kGatherWaves - 1) / kGatherWaves;
+    hipLaunchKernelGGL(gather_kernel, dim3((unsigned)grid), dim3(64 * kGatherWaves), 0, st, G);
+  }
   LDDL_HIP(hipGetLastError());
   if (d_tok_off)
     LDDL_HIP(hipMemcpyAsync(d_tok_off, P->tok_off, 8 * (P->n_pairs + 1), hipMemcpyDeviceToDevice, st));

@@ -221,12 +221,6 @@ struct alignas(16) WaveLds {
 
 // Order this wave's LDS writes before its later LDS reads of other lanes' data (the waves of a
 // workgroup work on different sentences, so a workgroup barrier would not be uniform).
-__device__ inline void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 __device__ inline uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
 
 __device__ inline int match_special_at(const Tables& T, const uint8_t* b, int64_t i, int64_t end) {
