@@ -373,11 +373,11 @@ struct WaveRng {
 
 struct PlanArgs {
   // kept corpus
-  const int64_t* ks_start;
+  const int64_t* kscan;  // dense token offset of each kept sentence
   const int32_t* ks_len;
   const int64_t* kd_off;
   const int64_t* kp_off;
-  const int32_t* ids;
+  const int32_t* dense;  // kept tokens, packed (densify_kernel)
   const int64_t* part_seed;
   // params
   int32_t seq, dup, masking, vocab_size, cls_id, sep_id, mask_id, max_pred;
@@ -417,13 +417,9 @@ struct LenWin {
   }
 };
 
-// token j (0-based) of the span that starts at kept sentence k0 (sequential walk; slow path only)
+// token j (0-based) of the span that starts at kept sentence k0 (slow path only)
 __device__ int32_t span_token(const PlanArgs& A, int64_t k0, int64_t j) {
-  for (int64_t k = k0;; ++k) {
-    const int32_t l = A.ks_len[k] & kLenMask;
-    if (j < l) return A.ids[A.ks_start[k] + j];
-    j -= l;
-  }
+  return A.dense[A.kscan[k0] + j];
 }
 
 __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
@@ -736,10 +732,50 @@ struct PairMasks {
   __device__ int64_t operator()(int64_t q) const { return nmask[src[q]]; }
 };
 
+// Kept tokens packed densely in kept-sentence order: kept sentence k's pieces are
+// dense[kscan[k] .. kscan[k+1]). A pair's A (and B) window is then one contiguous run
+// dense[kscan[a_ks] + a_front ..+ na), because a span only ever covers consecutive kept
+// sentences of one document. One wave per 64 kept sentences; 64-token output chunks are stored
+// coalesced, each lane finding its sentence among the few that overlap the chunk.
+__global__ void __launch_bounds__(256) densify_kernel(const int64_t* __restrict__ ks_start,
+                                                      const int32_t* __restrict__ ks_len,
+                                                      const int64_t* __restrict__ kscan, int64_t n,
+                                                      const int32_t* __restrict__ ids,
+                                                      int32_t* __restrict__ dense) {
+  const int lane = threadIdx.x & 63;
+  const int64_t k0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (k0 >= n) return;
+  const int64_t k = k0 + lane;
+  const bool ok = k < n;
+  const int32_t len = ok ? ks_len[k] & kLenMask : 0;
+  const int64_t st = ok ? ks_start[k] : 0;
+  const int32_t incl = wave_incl_scan(len);
+  const int32_t total = __shfl(incl, 63, 64);
+  const int64_t base = kscan[k0];
+  int j = 0;
+  for (int32_t c0 = 0; c0 < total; c0 += 64) {
+    const int32_t x = c0 + lane, hi = min(c0 + 63, total - 1);
+    while (__shfl(incl, j, 64) <= c0) ++j;  // first sentence overlapping the chunk
+    int64_t src = 0;
+    for (int jj = j;; ++jj) {
+      const int32_t e = __shfl(incl, jj, 64);
+      const int32_t b = e - __shfl(len, jj, 64);
+      const int64_t s = __shfl(st, jj, 64);
+      if (x >= b && x < e) src = s + (x - b);
+      if (e > hi) break;
+    }
+    if (x < total) dense[base + x] = ids[src];
+  }
+}
+
+struct KeptLen {
+  const int32_t* len;
+  __device__ int64_t operator()(int64_t k) const { return len[k] & kLenMask; }
+};
+
 struct GatherArgs {
-  const int64_t* ks_start;
-  const int32_t* ks_len;
-  const int32_t* ids;
+  const int64_t* kscan;  // dense offset of each kept sentence
+  const int32_t* dense;  // kept tokens, packed
   const int64_t* src;
   const PairDesc* desc;
   const int32_t* nmask;
@@ -747,7 +783,6 @@ struct GatherArgs {
   const int32_t* mtok;
   const int64_t* moff;
   int32_t max_pred, masking, seq;
-  int64_t n_kept_sent;
   int64_t n_pairs;
   const int64_t* tok_off;
   const int64_t* pos_off;
@@ -758,135 +793,26 @@ struct GatherArgs {
   int32_t* out_lab;
 };
 
-constexpr int kGatherWaves = 4;
 constexpr int kMaxPredLds = 1024;
+constexpr int kMaxSeqGather = 4096;  // LDS position -> mask map per pair
+constexpr int kGWaves = 4;
 
-constexpr int kMaxSeqLds = 1024;  // gather: position -> mask map entries per wave
-
-// Copy `count` tokens of the span that starts at kept sentence k0 after skipping `front` tokens
-// to out[0..count); output index t has sequence position pos0 + t. The span's sentence lengths
-// and starts are loaded 64 at a time (one per lane) and prefix-summed, so the copy of each
-// 64-token chunk only walks the few sentences that overlap it. Masked positions are found in the
-// wave's LDS map (position -> 1 + index into the pair's sorted masks, 0 = unmasked).
-__device__ void copy_span(const GatherArgs& G, int64_t k0, int32_t front, int32_t count,
-                          int32_t* out, int32_t pos0, const uint16_t* map, const int32_t* mt,
-                          int32_t* lab) {
-  const int lane = lane_id();
-  int32_t t = 0;       // tokens written
-  int64_t kb = k0;     // first sentence of the current 64-sentence batch
-  int32_t skip = front;
-  while (t < count) {
-    // batch of up to 64 sentences: inclusive prefix of lengths
-    const bool ok = kb + lane < G.n_kept_sent;  // sentences past the span are harmless
-    const int32_t myl = ok ? G.ks_len[kb + lane] & kLenMask : 0;
-    const int64_t mys = ok ? G.ks_start[kb + lane] : 0;
-    const int32_t incl = wave_incl_scan(myl);
-    const int32_t tot = __shfl(incl, 63, 64);
-    // tokens of this batch usable by the span: [skip, tot)
-    const int32_t avail = tot - skip;
-    if (avail <= 0) {
-      skip -= tot;
-      kb += 64;
-      continue;
-    }
-    const int32_t take = min(avail, count - t);
-    for (int32_t c0 = 0; c0 < take; c0 += 64) {
-      const int32_t x = skip + c0 + lane;  // position inside the batch's concatenation
-      const bool act = c0 + lane < take;
-      // sentence of x: number of inclusive prefixes <= x (sentences overlapping the chunk)
-      const int32_t lo_x = skip + c0, hi_x = skip + min(c0 + 64, take) - 1;
-      int j = 0;
-      // first sentence overlapping the chunk: count of prefixes <= lo_x
-      j = __popcll(__ballot(incl <= lo_x));
-      int32_t tok = 0;
-      while (true) {
-        const int32_t e = __shfl(incl, j, 64);      // end of sentence j (exclusive)
-        const int32_t bgn = e - __shfl(myl, j, 64);
-        const int64_t st = __shfl(mys, j, 64);
-        if (act && x >= bgn && x < e) tok = G.ids[st + (x - bgn)];
-        if (e > hi_x) break;
-        ++j;
-      }
-      if (act) {
-        const int32_t pos = pos0 + t + c0 + lane;
-        const int m = map ? (int)map[pos] : 0;
-        if (m) {
-          lab[m - 1] = tok;
-          if (mt[m - 1] != kKeep) tok = mt[m - 1];
-        }
-        out[t + c0 + lane] = tok;
-      }
-    }
-    t += take;
-    skip = 0;
-    kb += 64;
-  }
-}
-
-__global__ void __launch_bounds__(64 * kGatherWaves) gather_kernel(GatherArgs G) {
-  __shared__ uint16_t s_map[kGatherWaves][kMaxSeqLds];
-  __shared__ int32_t s_tok[kGatherWaves][kMaxPredLds];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t q = (int64_t)blockIdx.x * kGatherWaves + w;
-  const bool active = q < G.n_pairs;
-  const int64_t slot = active ? G.src[q] : 0;
-  int32_t nm = 0;
-  int32_t* lab = nullptr;
-  uint16_t* map = s_map[w];
-  if (G.masking && active) {
-    for (int j = lane; j < G.seq; j += 64) map[j] = 0;
-    nm = G.nmask[slot];
-  }
-  __syncthreads();
-  if (G.masking && active) {
-    const int64_t mb = G.moff[slot];
-    for (int j = lane; j < nm; j += 64) {
-      const uint16_t pv = G.mpos[mb + j];
-      map[pv] = (uint16_t)(j + 1);
-      s_tok[w][j] = G.mtok[mb + j];
-      G.out_pos[G.pos_off[q] + j] = pv;
-    }
-    lab = G.out_lab + G.pos_off[q];
-  }
-  __syncthreads();  // the map is visible to every lane of the wave
-  if (!active) return;
-  const PairDesc d = G.desc[slot];
-  const int32_t nb = d.nb_rn & 0x7FFFFFFF;
-  int32_t* out = G.out_tok + G.tok_off[q];
-  const uint16_t* mp = G.masking ? map : nullptr;
-  copy_span(G, d.a_ks, d.a_front, d.na, out, 1, mp, s_tok[w], lab);
-  copy_span(G, d.b_ks, d.b_front, nb, out + d.na, d.na + 2, mp, s_tok[w], lab);
-  if (lane == 0) {
-    G.len_a[q] = d.na;
-    G.is_rn[q] = (uint8_t)((uint32_t)d.nb_rn >> 31);
-  }
-}
-
-// Gather, batched: each wave copies K consecutive output pairs. The 2K spans (A and B of each
-// pair) get Gs-lane segments of a small sentence table (lane j of a segment holds sentence k0+j:
-// length, start, inclusive length prefix), so a span costs Gs*12 bytes of table reads instead of
-// 64*12. Output token x of a pair is position x of A's window (x < na) or of B's; its sentence is
-// found by walking the few table entries that overlap its 64-token chunk. All K*C token loads are
-// issued before any is consumed, which is what hides HBM latency here (one pair per wave left
-// ~80% of wave cycles waiting on dependent loads). A span whose window needs more than Gs
-// sentences takes the sequential copy_span path (uniform branch, rare).
-constexpr int kG3Waves = 4;
-
-template <int Gs, int K, int C>
-__global__ void __launch_bounds__(64 * kG3Waves) gather3_kernel(GatherArgs G, int32_t map_len) {
-  constexpr int T = (2 * K * Gs + 63) / 64;  // table registers
-  constexpr int SPR = 64 / Gs;               // spans per table register
-  extern __shared__ __attribute__((aligned(16))) uint8_t g3_smem[];
+// Gather: each wave emits K consecutive output pairs (their tokens are contiguous in the output).
+// Per pair: A = dense[kscan[a_ks] + a_front ..+ na), B likewise; output token x < na + nb comes from
+// A (x < na) or B. The masks of each pair go to an LDS map (position -> 1 + mask index) so each
+// output lane finds its own decision; labels take the original token. All K*C token loads of the
+// wave are issued before any is consumed (the kernel is bound by load latency and cache lines).
+template <int K, int C>
+__global__ void __launch_bounds__(64 * kGWaves) gather_kernel(GatherArgs G, int32_t map_len) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int sj = lane & (Gs - 1), sseg = lane / Gs;
-  uint16_t* maps = reinterpret_cast<uint16_t*>(g3_smem) + (size_t)w * K * map_len;
-  int32_t* toks = reinterpret_cast<int32_t*>(g3_smem + (size_t)kG3Waves * K * map_len * 2) +
+  uint16_t* maps = reinterpret_cast<uint16_t*>(g_smem) + (size_t)w * K * map_len;
+  int32_t* toks = reinterpret_cast<int32_t*>(g_smem + (size_t)kGWaves * K * map_len * 2) +
                   (size_t)w * K * G.max_pred;
-  const int64_t qb = ((int64_t)blockIdx.x * kG3Waves + w) * K;
+  const int64_t qb = ((int64_t)blockIdx.x * kGWaves + w) * K;
 
-  int64_t slot[K], tof[K];
-  int64_t aks[K], bks[K];
-  int32_t afr[K], na[K], bfr[K], nb[K], rn[K], nm[K];
+  int64_t slot[K], tof[K], aoff[K], boff[K];
+  int32_t na[K], nb[K], rn[K], nm[K];
   bool act[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -897,141 +823,71 @@ __global__ void __launch_bounds__(64 * kG3Waves) gather3_kernel(GatherArgs G, in
   for (int k = 0; k < K; ++k) {
     PairDesc d{0, 0, 0, 0, 0, 0};
     if (act[k]) d = G.desc[slot[k]];
-    aks[k] = d.a_ks;
-    bks[k] = d.b_ks;
-    afr[k] = d.a_front;
     na[k] = d.na;
-    bfr[k] = d.b_front;
     nb[k] = d.nb_rn & 0x7FFFFFFF;
     rn[k] = (int32_t)((uint32_t)d.nb_rn >> 31);
+    aoff[k] = act[k] ? G.kscan[d.a_ks] + d.a_front : 0;
+    boff[k] = act[k] ? G.kscan[d.b_ks] + d.b_front : 0;
     tof[k] = act[k] ? G.tok_off[qb + k] : 0;
     nm[k] = (G.masking && act[k]) ? G.nmask[slot[k]] : 0;
   }
-  // sentence tables
-  int32_t tlen[T], tinc[T];
-  int64_t tst[T];
+  for (int32_t cb = 0;; cb += 64 * C) {  // one pass for seq <= 64 * C + 3
+    int32_t tok[K][C];
 #pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const int s = t * SPR + sseg;  // this lane's span
-    int64_t k0 = -1;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (s == 2 * k && act[k]) k0 = aks[k];
-      if (s == 2 * k + 1 && act[k]) k0 = bks[k];
-    }
-    const bool ok = k0 >= 0 && k0 + sj < G.n_kept_sent;
-    tlen[t] = ok ? G.ks_len[k0 + sj] & kLenMask : 0;
-    tst[t] = ok ? G.ks_start[k0 + sj] : 0;
-  }
-  // masks: position -> 1 + index map and replacement table per pair
-  if (G.masking) {
-    uint32_t* m32 = reinterpret_cast<uint32_t*>(maps);
-    for (int i = lane; i < K * map_len / 2; i += 64) m32[i] = 0u;
-    wave_sync();
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (!nm[k]) continue;
-      const int64_t mb = G.moff[slot[k]], po = G.pos_off[qb + k];
-      for (int j = lane; j < nm[k]; j += 64) {
-        const uint16_t pv = G.mpos[mb + j];
-        maps[k * map_len + pv] = (uint16_t)(j + 1);
-        toks[k * G.max_pred + j] = G.mtok[mb + j];
-        G.out_pos[po + j] = pv;
-      }
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    int32_t v = tlen[t];
-#pragma unroll
-    for (int dd = 1; dd < Gs; dd <<= 1) {
-      const int32_t o = __shfl_up(v, dd, Gs);
-      if (sj >= dd) v += o;
-    }
-    tinc[t] = v;
-  }
-  // fast path check per pair: both windows end inside their table segments
-  bool fast[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int sa = 2 * k, sb = 2 * k + 1;
-    const int32_t ea = (int32_t)__builtin_amdgcn_readlane(tinc[sa / SPR], (sa % SPR) * Gs + Gs - 1);
-    const int32_t eb = (int32_t)__builtin_amdgcn_readlane(tinc[sb / SPR], (sb % SPR) * Gs + Gs - 1);
-    fast[k] = act[k] && ea >= afr[k] + na[k] && eb >= bfr[k] + nb[k];
-  }
-  // source addresses
-  int64_t addr[K][C];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-#pragma unroll
-    for (int c = 0; c < C; ++c) addr[k][c] = -1;
-    if (!fast[k]) continue;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {  // h = 0: A, 1: B
-      const int s = 2 * k + h;
-      const int tr = s / SPR, sb0 = (s % SPR) * Gs;
-      const int32_t wlo = h ? na[k] : 0, whi = h ? na[k] + nb[k] : na[k];  // x range of the span
-      const int32_t fr = h ? bfr[k] : afr[k];
-      const uint64_t segm = (Gs == 64 ? ~0ull : ((1ull << Gs) - 1)) << sb0;
+    for (int k = 0; k < K; ++k)
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const int32_t x0 = c * 64 > wlo ? c * 64 : wlo, x1 = (c * 64 + 64 < whi ? c * 64 + 64 : whi);
-        if (x0 >= x1) continue;  // uniform
-        const int32_t x = c * 64 + lane;
-        const bool mine = x >= x0 && x < x1;
-        const int32_t y = fr + (x - wlo);  // offset in the span's concatenation
-        const int32_t lo = fr + (x0 - wlo), hi = fr + (x1 - 1 - wlo);
-        int j = __popcll(__ballot(tinc[tr] <= lo) & segm);
-        while (true) {
-          const int32_t e = __builtin_amdgcn_readlane(tinc[tr], sb0 + j);
-          const int32_t bgn = e - __builtin_amdgcn_readlane(tlen[tr], sb0 + j);
-          const int64_t st = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(tst[tr] >> 32), sb0 + j)
-                              << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane((int)tst[tr], sb0 + j);
-          if (mine && y >= bgn && y < e) addr[k][c] = st + (y - bgn);
-          if (e > hi || j == Gs - 1) break;
-          ++j;
+        const int32_t x = cb + c * 64 + lane;
+        tok[k][c] = x < na[k] ? G.dense[aoff[k] + x]
+                              : (x < na[k] + nb[k] ? G.dense[boff[k] + (x - na[k])] : 0);
+      }
+    if (G.masking && cb == 0) {  // token loads are in flight while the mask maps are built
+      uint32_t* m32 = reinterpret_cast<uint32_t*>(maps);
+      for (int i = lane; i < K * map_len / 2; i += 64) m32[i] = 0u;
+      wave_sync();
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (!nm[k]) continue;
+        const int64_t mb = G.moff[slot[k]], po = G.pos_off[qb + k];
+        for (int j = lane; j < nm[k]; j += 64) {
+          const uint16_t pv = G.mpos[mb + j];
+          maps[k * map_len + pv] = (uint16_t)(j + 1);
+          toks[k * G.max_pred + j] = G.mtok[mb + j];
+          G.out_pos[po + j] = pv;
         }
       }
+      wave_sync();
     }
-  }
-  int32_t tok[K][C];
+    bool more = false;
 #pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int c = 0; c < C; ++c) tok[k][c] = addr[k][c] >= 0 ? G.ids[addr[k][c]] : 0;
-  if (G.masking) wave_sync();  // maps complete
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    if (!act[k]) continue;
-    const uint16_t* map = G.masking ? maps + k * map_len : nullptr;
-    const int32_t* mt = toks + k * G.max_pred;
-    int32_t* lab = G.masking ? G.out_lab + G.pos_off[qb + k] : nullptr;
-    int32_t* out = G.out_tok + tof[k];
-    if (fast[k]) {
+    for (int k = 0; k < K; ++k) {
+      if (!act[k]) continue;
+      const int32_t n = na[k] + nb[k];
+      const uint16_t* map = maps + k * map_len;
+      const int32_t* mt = toks + k * G.max_pred;
+      int32_t* out = G.out_tok + tof[k];
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const int32_t x = c * 64 + lane;
-        if (x < na[k] + nb[k]) {
+        const int32_t x = cb + c * 64 + lane;
+        if (x < n) {
           int32_t v = tok[k][c];
-          if (map) {
+          if (G.masking) {
             const int m = map[x < na[k] ? x + 1 : x + 2];
             if (m) {
-              lab[m - 1] = v;
+              G.out_lab[G.pos_off[qb + k] + m - 1] = v;
               if (mt[m - 1] != kKeep) v = mt[m - 1];
             }
           }
           out[x] = v;
         }
       }
-    } else {
-      copy_span(G, aks[k], afr[k], na[k], out, 1, map, mt, lab);
-      copy_span(G, bks[k], bfr[k], nb[k], out + na[k], na[k] + 2, map, mt, lab);
+      more |= n > cb + 64 * C;
+      if (cb == 0 && lane == 0) {
+        G.len_a[qb + k] = na[k];
+        G.is_rn[qb + k] = (uint8_t)rn[k];
+      }
     }
-    if (lane == 0) {
-      G.len_a[qb + k] = na[k];
-      G.is_rn[qb + k] = (uint8_t)rn[k];
-    }
+    if (!more) break;
   }
 }
 
@@ -1047,9 +903,9 @@ struct lddl_pairs {
   int64_t n_part = 0, n_pairs = 0, n_tokens = 0, n_masked = 0, n_kept_sent = 0, n_kept_doc = 0;
   std::vector<void*> allocs;
   // views
-  int64_t *ks_start = nullptr, *kd_off = nullptr, *kp_off = nullptr;
+  int64_t *ks_start = nullptr, *kd_off = nullptr, *kp_off = nullptr, *kscan = nullptr;
   int32_t* ks_len = nullptr;
-  const int32_t* ids = nullptr;
+  int32_t* dense = nullptr;  // kept tokens, packed in kept-sentence order
   PairDesc* desc = nullptr;
   int32_t *order = nullptr, *nmask = nullptr, *mtok = nullptr;
   uint16_t* mpos = nullptr;
@@ -1105,6 +961,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   if (prm->rng != LDDL_RNG_REPLAY) LDDL_FAIL(-1, "rng mode %d not available", prm->rng);
   const int32_t cls = c->tab.special_id[kCls], sep = c->tab.special_id[kSep],
                 msk = c->tab.special_id[kMask];
+  if (prm->masking && prm->seq > kMaxSeqGather)
+    LDDL_FAIL(-1, "static masking supports target_seq_length <= %d", kMaxSeqGather);
   if (prm->masking && (cls < 0 || sep < 0 || msk < 0))
     LDDL_FAIL(-1, "static masking needs [CLS] [SEP] [MASK] in the vocab");
   hipStream_t st = as_stream(stream);
@@ -1113,7 +971,6 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   P->n_part = n_part;
   P->masking = prm->masking;
   P->seq = prm->seq;
-  P->ids = d_ids;
   TRY(hipEventCreate(&P->ev[0]) == hipSuccess && hipEventCreate(&P->ev[1]) == hipSuccess
           ? 0 : (set_error("hipEventCreate failed"), -100));
   int64_t *ks_pos, *kd_pos, *scratch, *part_npairs, *part_base;
@@ -1144,6 +1001,18 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   hipLaunchKernelGGL(part_offsets_kernel, dim3((unsigned)((n_part + 256) / 256)), dim3(256), 0, st,
                      d_part_doc_off, n_part, kd_pos, P->kp_off);
   LDDL_HIP(hipGetLastError());
+  // dense kept tokens
+  TRY(P->alloc(&P->kscan, P->n_kept_sent + 1, st));
+  if (scan_exclusive(KeptLen{P->ks_len}, P->n_kept_sent, P->kscan, scratch, st) != hipSuccess)
+    TRY(-100);
+  int64_t n_kept_tok = 0;
+  LDDL_HIP(hipMemcpyAsync(&n_kept_tok, P->kscan + P->n_kept_sent, 8, hipMemcpyDeviceToHost, st));
+  LDDL_HIP(hipStreamSynchronize(st));
+  TRY(P->alloc(&P->dense, n_kept_tok, st));
+  if (P->n_kept_sent)
+    hipLaunchKernelGGL(densify_kernel, dim3((unsigned)((P->n_kept_sent + 255) / 256)), dim3(256), 0,
+                       st, P->ks_start, P->ks_len, P->kscan, P->n_kept_sent, d_ids, P->dense);
+  LDDL_HIP(hipGetLastError());
   // plan
   const int64_t slots = (int64_t)prm->dup * P->n_kept_sent;
   int32_t max_pred = 0;
@@ -1164,11 +1033,11 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     TRY(P->alloc(&P->moff, slots, st));
   }
   PlanArgs A{};
-  A.ks_start = P->ks_start;
+  A.kscan = P->kscan;
   A.ks_len = P->ks_len;
   A.kd_off = P->kd_off;
   A.kp_off = P->kp_off;
-  A.ids = d_ids;
+  A.dense = P->dense;
   A.part_seed = d_part_seed;
   A.seq = prm->seq;
   A.dup = prm->dup;
@@ -1311,9 +1180,8 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
   hipStream_t st = as_stream(stream);
   if (P->n_pairs == 0) return 0;
   GatherArgs G{};
-  G.ks_start = P->ks_start;
-  G.ks_len = P->ks_len;
-  G.ids = P->ids;
+  G.kscan = P->kscan;
+  G.dense = P->dense;
   G.src = P->src;
   G.desc = P->desc;
   G.nmask = P->nmask;
@@ -1323,7 +1191,6 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
   G.max_pred = P->max_pred;
   G.masking = P->masking;
   G.seq = P->seq;
-  G.n_kept_sent = P->n_kept_sent;
   G.n_pairs = P->n_pairs;
   G.tok_off = P->tok_off;
   G.pos_off = P->pos_off;
@@ -1332,27 +1199,19 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
   G.is_rn = d_is_rn;
   G.out_pos = d_pos;
   G.out_lab = d_lab;
-  static const char* gpath = getenv("LDDL_GATHER");  // "v2": one pair per wave (A/B runs)
   const int32_t map_len = (P->seq + 1) & ~1;
-  auto launch3 = [&](auto kern, int K) {
-    const int64_t per_wg = (int64_t)K * kG3Waves;
-    const size_t lds = P->masking ? (size_t)kG3Waves * K * (2 * map_len + 4 * P->max_pred) : 0;
+  auto launch = [&](auto kern, int K) {
+    const int64_t per_wg = (int64_t)K * kGWaves;
+    const size_t lds = P->masking ? (size_t)kGWaves * K * (2 * map_len + 4 * P->max_pred) : 0;
     hipLaunchKernelGGL(kern, dim3((unsigned)((P->n_pairs + per_wg - 1) / per_wg)),
-                       dim3(64 * kG3Waves), lds, st, G, map_len);
+                       dim3(64 * kGWaves), lds, st, G, map_len);
   };
-  if (gpath && !strcmp(gpath, "v2")) {
-    const int64_t grid = (P->n_pairs + kGatherWaves - 1) / kGatherWaves;
-    hipLaunchKernelGGL(gather_kernel, dim3((unsigned)grid), dim3(64 * kGatherWaves), 0, st, G);
-  } else if (P->seq <= 128) {
-    launch3(gather3_kernel<8, 4, 2>, 4);
-  } else if (P->seq <= 256) {
-    launch3(gather3_kernel<16, 4, 4>, 4);
-  } else if (P->seq <= 512) {
-    launch3(gather3_kernel<32, 2, 8>, 2);
-  } else {
-    const int64_t grid = (P->n_pairs + kGatherWaves - 1) / kGatherWaves;
-    hipLaunchKernelGGL(gather_kernel, dim3((unsigned)grid), dim3(64 * kGatherWaves), 0, st, G);
-  }
+#ifndef LDDL_GK128
+#define LDDL_GK128 4
+#endif
+  if (P->seq <= 131) launch(gather_kernel<LDDL_GK128, 2>, LDDL_GK128);
+  else if (P->seq <= 259) launch(gather_kernel<4, 4>, 4);
+  else launch(gather_kernel<2, 8>, 2);
   LDDL_HIP(hipGetLastError());
   if (d_tok_off)
     LDDL_HIP(hipMemcpyAsync(d_tok_off, P->tok_off, 8 * (P->n_pairs + 1), hipMemcpyDeviceToDevice, st));
