@@ -99,6 +99,9 @@ def main():
     ap.add_argument('--gen-threads', type=int, default=16)
     ap.add_argument('--cpu-sample-bytes', type=int, default=48 << 20)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--rng', choices=['replay', 'native'], default='replay',
+                    help='replay: CPython MT19937 per partition, bit-exact with the reference; '
+                         'native: Philox counter RNG, documents and pairs in parallel')
     args = ap.parse_args()
     if args.seq is None:
         args.seq = 128 if args.workload == 'c2' else 512
@@ -131,7 +134,8 @@ def main():
         if ev is not None:
             ev[1].record()
         pb = make_pairs(ctx, sent_off, ids, sent_len, doc_off, part_off, part_seed, seq=args.seq,
-                        dup=5, masking=True, short_seq_prob=0.1, masked_lm_ratio=0.15)
+                        dup=5, masking=True, short_seq_prob=0.1, masked_lm_ratio=0.15,
+                        rng=args.rng)
         if args.workload == 'c4':
             bb = balance(ctx, pb, 8, args.seq // 8, timings=diag.get('balance'))
             n_tok = int(bb.tokens.numel()) + 3 * bb.n_rows
@@ -232,14 +236,17 @@ def main():
                          '; {} MiB of sentence text per GPU per step, {} KiB partitions').format(
                              args.seed, args.seq, args.batch_bytes >> 20, args.partition_bytes >> 10),
             'seq_len': args.seq, 'masking': 'static', 'duplicate_factor': 5,
-            'rng': 'replay (CPython MT19937, random.seed per partition)',
+            'rng': ('replay (CPython MT19937, random.seed per partition)' if args.rng == 'replay'
+                    else 'native (Philox4x32-10 counter RNG per partition/unit/pair)'),
             'batch_bytes': int(n_bytes), 'sentences': int(n_sent), 'documents': int(corp.n_doc),
             'partitions': int(len(part) - 1), 'wordpieces': pieces, 'pairs': int(n_pairs),
             'vocab': os.path.basename(VOCAB), 'parallelism': 'dp{} (document shards)'.format(world),
         },
         'stages_ms': {'tokenize': tok_ms,
                       ('pairs_plan_and_gather' if args.workload == 'c2' else
-                       'pairs_bin_and_balance'): pair_ms},
+                       'pairs_bin_and_balance'): pair_ms,
+                      'per_step_pairs': [round(e[1].elapsed_time(e[2]), 2) for e in evs],
+                      'per_step_plan': [round(x['plan_ms'], 2) for x in stats]},
         'roofline': {'kernel': 'plan_replay_kernel', 'bound': 'hbm', 'achieved': plan_gbs,
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': plan_gbs / HBM_PEAK_GBS,
                      'traffic': None, 'algorithmic_bytes_per_launch': plan_bytes,

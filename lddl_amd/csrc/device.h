@@ -95,6 +95,24 @@ __device__ inline T wave_incl_scan(T v) {
   return v;
 }
 
+// Philox4x32-10 (Salmon et al., SC'11)
+struct Philox {
+  __device__ static uint4 round(uint4 c, uint2 k) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    return make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k.x, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k.y,
+                      (uint32_t)p0);
+  }
+  __device__ static uint4 gen(uint4 c, uint2 k) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      c = round(c, k);
+      k.x += 0x9E3779B9u;
+      k.y += 0xBB67AE85u;
+    }
+    return c;
+  }
+};
+
 // LDS written by some lanes of a wave becomes visible to all lanes of that wave
 __device__ inline void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

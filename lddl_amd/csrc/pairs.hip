@@ -656,6 +656,303 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
   if (leader) A.part_npairs[p] = np;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Native RNG mode (LDDL_RNG_NATIVE): the same algorithms (create_pairs_from_document,
+// _truncate_seq_pair, create_masked_lm_predictions, the partition shuffle) drawing from
+// Philox4x32-10 instead of one sequential MT19937 per partition, so every (duplicate, document)
+// walk and every pair's masking runs in its own lane. A stream is keyed by
+// (native_seed, part_seed[p]) and counted by the unit's or pair's index inside its partition, so
+// a partition's output does not depend on how partitions are batched or sharded.
+// Distributions are those of the reference: randint / _randbelow by the same bit-length
+// rejection, random() < p on the same 53-bit integer, each truncation side a fair coin, the
+// masked set a uniform num_to_predict-subset of the candidates (Floyd's algorithm: the shuffled
+// prefix of pretrain.py:197-207 is a uniform subset), 80/10/10 decisions per masked token.
+// ---------------------------------------------------------------------------------------------
+__device__ inline uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ inline uint64_t part_key(uint64_t native_seed, int64_t part_seed) {
+  return mix64(native_seed ^ mix64((uint64_t)part_seed + 0x9E3779B97F4A7C15ull));
+}
+
+enum : uint32_t { kStreamWalk = 1, kStreamMask = 2, kStreamOrder = 3 };
+
+struct CtrRng {
+  uint2 key;
+  uint32_t id0, id1, blk;
+  uint4 buf;
+  int have;
+  __device__ CtrRng(uint64_t k, int64_t index, uint32_t stream)
+      : key{(uint32_t)k, (uint32_t)(k >> 32)},
+        id0((uint32_t)index),
+        id1((uint32_t)((uint64_t)index >> 32) << 4 | stream),
+        blk(0),
+        have(0) {}
+  __device__ uint32_t u32() {
+    if (have == 0) {
+      buf = Philox::gen(make_uint4(blk++, id0, id1, 0x6C64646Cu), key);
+      have = 4;
+    }
+    --have;
+    return have == 3 ? buf.x : have == 2 ? buf.y : have == 1 ? buf.z : buf.w;
+  }
+  __device__ uint64_t rand53() {  // the 53-bit integer behind random()
+    const uint32_t a = u32() >> 5, b = u32() >> 6;
+    return ((uint64_t)a << 26) | b;
+  }
+  __device__ bool coin() { return u32() < 0x80000000u; }
+  __device__ uint32_t randbelow(uint32_t n) {  // _randbelow: k-bit draws until < n
+    const int k = 32 - __clz(n);
+    uint32_t r = u32() >> (32 - k);
+    while (r >= n) r = u32() >> (32 - k);
+    return r;
+  }
+  __device__ int64_t randint(int64_t a, int64_t b) { return a + randbelow((uint32_t)(b - a + 1)); }
+  __device__ int32_t heads(int32_t n) {  // number of heads in n fair coins
+    int32_t h = 0;
+    for (; n >= 32; n -= 32) h += __popc(u32());
+    if (n > 0) h += __popc(u32() & ((1u << n) - 1u));
+    return h;
+  }
+};
+
+struct NativeArgs {
+  const int32_t* ks_len;
+  const int64_t* kd_off;
+  const int64_t* kp_off;
+  const int64_t* kscan;
+  const int32_t* dense;
+  const int64_t* part_seed;
+  int64_t n_part, n_units, unit0;  // units dup * (kp_off[0] .. kp_off[n_part])
+  uint64_t native_seed, k_short;
+  int32_t seq, dup, masking, cls_id, sep_id, mask_id, vocab_size;
+  double ratio;
+  int64_t* ucnt;        // count pass: pairs of each (duplicate, document) unit
+  const int64_t* uoff;  // emit pass: first pair of each unit (exclusive scan of ucnt)
+  const int64_t* part_base;
+  PairDesc* desc;
+  int32_t* nmask;
+  int32_t* ncand;
+  int32_t* ppart;
+  const int64_t* moff;
+  uint16_t* mpos;
+  int32_t* mtok;
+  int64_t* src;
+  int64_t n_pairs;
+  int32_t words;  // bitmap words per lane (mask kernel)
+};
+
+// token t of the window [front, front + n) of the span starting at kept sentence k
+__device__ inline int32_t win_token(const NativeArgs& A, int64_t k, int32_t front, int32_t t) {
+  return A.dense[A.kscan[k] + front + t];
+}
+
+// Unit u = (duplicate dp, document d) of partition p, numbered dup * kp_off[p] + dp * nd + d_local
+// (the reference's `for _ in range(dup): for doc in docs` order). EMIT = false counts the unit's
+// pairs; EMIT = true replays the identical draws and writes them at uoff[u].
+template <bool EMIT>
+__global__ void __launch_bounds__(256) plan_native_kernel(NativeArgs A) {
+  const int64_t ul = (int64_t)blockIdx.x * 256 + threadIdx.x;  // unit, counted from partition 0
+  if (ul >= A.n_units) return;
+  const int64_t u = ul + A.unit0;
+  int64_t lo = 0, hi = A.n_part;  // largest p with dup * kp_off[p] <= u
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)A.dup * A.kp_off[mid] <= u) lo = mid;
+    else hi = mid;
+  }
+  const int64_t p = lo;
+  const int64_t d0 = A.kp_off[p], nd = A.kp_off[p + 1] - d0;
+  const int64_t r = u - (int64_t)A.dup * d0;
+  const int64_t dl = r % nd;
+  CtrRng rng(part_key(A.native_seed, A.part_seed[p]), r, kStreamWalk);
+  const int64_t s0 = A.kd_off[d0 + dl];
+  const int ns = (int)(A.kd_off[d0 + dl + 1] - s0);
+  const int32_t max_num = A.seq - 3;
+  int32_t target = max_num;
+  if (rng.rand53() < A.k_short) target = (int32_t)rng.randint(2, max_num);
+  const int64_t base = EMIT ? A.uoff[ul] : 0;
+  int64_t np = 0;
+  int chunk0 = 0, chunk_n = 0;
+  int64_t cur_len = 0;
+  for (int i = 0; i < ns; ++i) {
+    if (chunk_n == 0) chunk0 = i;
+    ++chunk_n;
+    cur_len += A.ks_len[s0 + i] & kLenMask;
+    if (!(i == ns - 1 || cur_len >= target)) continue;
+    const int a_end = chunk_n >= 2 ? (int)rng.randint(1, chunk_n - 1) : 1;
+    int64_t la = 0;
+    int32_t flags = 0;
+    for (int j = chunk0; j < chunk0 + a_end; ++j) {
+      const int32_t wd = A.ks_len[s0 + j];
+      la += wd & kLenMask;
+      flags |= wd;
+    }
+    int64_t lb = 0, b_ks;
+    int32_t rn = 0;
+    if (chunk_n == 1 || rng.coin()) {
+      rn = 1;
+      const int64_t target_b = target - la;
+      int64_t rd = 0;
+      for (int t = 0; t < 10; ++t) {
+        rd = rng.randint(0, nd - 1);
+        if (rd != dl) break;
+      }
+      if (rd == dl) rn = 0;
+      const int64_t r0 = A.kd_off[d0 + rd];
+      const int rns = (int)(A.kd_off[d0 + rd + 1] - r0);
+      const int rstart = (int)rng.randint(0, rns - 1);
+      b_ks = r0 + rstart;
+      for (int j = rstart; j < rns; ++j) {
+        const int32_t wd = A.ks_len[r0 + j];
+        lb += wd & kLenMask;
+        flags |= wd;
+        if (lb >= target_b) break;
+      }
+      i -= chunk_n - a_end;
+    } else {
+      b_ks = s0 + chunk0 + a_end;
+      for (int j = chunk0 + a_end; j < chunk0 + chunk_n; ++j) {
+        const int32_t wd = A.ks_len[s0 + j];
+        lb += wd & kLenMask;
+        flags |= wd;
+      }
+    }
+    // _truncate_seq_pair: which side each trim hits is fixed (see WaveRng::trunc_draws); front or
+    // back is a fair coin per trim
+    int32_t na = (int32_t)la, nb = (int32_t)lb, a_front = 0, b_front = 0;
+    const int32_t T = na + nb - max_num;
+    if (T > 0) {
+      const int32_t dd = na - nb, ad = dd < 0 ? -dd : dd;
+      const int32_t nA = (dd > 0 ? min(dd, T) : 0) + (T > ad ? (T - ad) / 2 : 0);
+      a_front = rng.heads(nA);
+      b_front = rng.heads(T - nA);
+      na -= nA;
+      nb -= T - nA;
+    }
+    if (EMIT) {
+      const int64_t q = base + np;
+      A.desc[q] = PairDesc{s0 + chunk0, b_ks, a_front, na, b_front,
+                           nb | (int32_t)((uint32_t)rn << 31)};
+      A.ppart[q] = (int32_t)p;
+      if (A.masking) {
+        int32_t nc = na + nb;
+        if (flags & kLenHasClsSep) {  // literal [CLS]/[SEP] in the text are not candidates
+          nc = 0;
+          for (int32_t t = 0; t < na + nb; ++t) {
+            const int32_t tok = t < na ? win_token(A, s0 + chunk0, a_front, t)
+                                       : win_token(A, b_ks, b_front, t - na);
+            nc += tok != A.cls_id && tok != A.sep_id;
+          }
+        }
+        int32_t num = (int32_t)rint((double)(na + nb + 3) * A.ratio);
+        if (num < 1) num = 1;
+        if (num > nc) num = nc;
+        A.nmask[q] = num;
+        A.ncand[q] = nc;
+      }
+    }
+    ++np;
+    chunk_n = 0;
+    cur_len = 0;
+  }
+  if (!EMIT) A.ucnt[ul] = np;
+}
+
+__global__ void native_part_base_kernel(const int64_t* kp_off, int64_t n_part, int32_t dup,
+                                        const int64_t* uoff, int64_t* part_base) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p <= n_part) part_base[p] = uoff[(int64_t)dup * (kp_off[p] - kp_off[0])];
+}
+
+// Masked positions of pair q (one lane per pair): Floyd's sampling of num candidate indices out of
+// nc into a lane-private LDS bitmap, then the set bits in ascending order (= sorted(masked_lms,
+// key=index)) each with an 80/10/10 decision.
+__global__ void __launch_bounds__(256) mask_native_kernel(NativeArgs A) {
+  extern __shared__ uint32_t s_bm[];  // [wave][word][lane]
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  uint32_t* bm = s_bm + (size_t)(threadIdx.x >> 6) * A.words * 64 + lane;
+  if (q >= A.n_pairs) return;
+  const int32_t num = A.nmask[q];
+  if (num <= 0) return;
+  const int32_t nc = A.ncand[q];
+  const PairDesc d = A.desc[q];
+  const int32_t na = d.na, nb = d.nb_rn & 0x7FFFFFFF;
+  const int64_t p = A.ppart[q];
+  CtrRng rng(part_key(A.native_seed, A.part_seed[p]), q - A.part_base[p], kStreamMask);
+  const int nw = (nc + 31) >> 5;
+  for (int i = 0; i < nw; ++i) bm[i * 64] = 0u;
+  for (int32_t j = nc - num; j < nc; ++j) {
+    const uint32_t t = rng.randbelow((uint32_t)j + 1);
+    const uint32_t wt = bm[(t >> 5) * 64];
+    const uint32_t pick = (wt >> (t & 31)) & 1u ? (uint32_t)j : t;
+    bm[(pick >> 5) * 64] |= 1u << (pick & 31);
+  }
+  const bool fast = nc == na + nb;
+  const int64_t mb = A.moff[q];
+  int32_t m = 0, tcur = 0, ccur = 0;  // slow path: token / candidate cursor
+  for (int i = 0; i < nw; ++i) {
+    uint32_t bits = bm[i * 64];
+    while (bits) {
+      const int32_t ci = i * 32 + __ffs(bits) - 1;
+      bits &= bits - 1;
+      int32_t t = ci;
+      if (!fast) {  // walk to the ci-th non-[CLS]/[SEP] token
+        while (true) {
+          const int32_t tok = tcur < na ? win_token(A, d.a_ks, d.a_front, tcur)
+                                        : win_token(A, d.b_ks, d.b_front, tcur - na);
+          if (tok != A.cls_id && tok != A.sep_id) {
+            if (ccur == ci) break;
+            ++ccur;
+          }
+          ++tcur;
+        }
+        t = tcur++;
+        ++ccur;
+      }
+      int32_t tok;
+      if (rng.rand53() < kLt08) tok = A.mask_id;
+      else if (rng.coin()) tok = kKeep;
+      else tok = (int32_t)rng.randbelow((uint32_t)A.vocab_size);
+      A.mpos[mb + m] = (uint16_t)(t < na ? t + 1 : t + 2);
+      A.mtok[mb + m] = tok;
+      ++m;
+    }
+  }
+}
+
+// random.shuffle(partition_pairs), native: output row k of partition p takes pair perm_p(k), a
+// keyed 4-round Feistel bijection on [0, 4^h) >= np restricted to [0, np) by cycle walking.
+__global__ void __launch_bounds__(256) order_native_kernel(NativeArgs A) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= A.n_pairs) return;
+  const int64_t p = A.ppart[q];
+  const int64_t pb = A.part_base[p], np = A.part_base[p + 1] - pb;
+  const uint64_t key = mix64(part_key(A.native_seed, A.part_seed[p]) ^ kStreamOrder);
+  int bits = 1;
+  while ((1ll << bits) < np) ++bits;
+  const int h = (bits + 1) >> 1;
+  const uint64_t hm = (1ull << h) - 1;
+  uint64_t x = (uint64_t)(q - pb);
+  do {
+    uint64_t L = x >> h, R = x & hm;
+    for (uint64_t rd = 0; rd < 4; ++rd) {
+      const uint64_t f = mix64(R ^ key ^ (rd << 56)) & hm;
+      const uint64_t nl = R;
+      R = L ^ f;
+      L = nl;
+    }
+    x = (L << h) | R;
+  } while (x >= (uint64_t)np);
+  A.src[q] = pb + (int64_t)x;
+}
+
 // total kept tokens (sizing of the mask pool)
 __global__ void __launch_bounds__(256) sum_tokens_kernel(const int32_t* __restrict__ sent_len,
                                                         int64_t n, unsigned long long* out) {
@@ -948,6 +1245,91 @@ static uint64_t short_threshold(double p) {
   return (uint64_t)ceil(ldexp(p, 53));
 }
 
+struct I32 {
+  const int32_t* v;
+  __device__ int64_t operator()(int64_t i) const { return v[i]; }
+};
+
+// LDDL_RNG_NATIVE control plane: count pass, unit scan, emit pass, mask offsets + masks, order.
+static int plan_native(lddl_pairs* P, lddl_ctx* c, const lddl_pair_params* prm,
+                       const int64_t* d_part_seed, int64_t n_part, hipStream_t st) {
+  NativeArgs A{};
+  A.ks_len = P->ks_len;
+  A.kd_off = P->kd_off;
+  A.kp_off = P->kp_off;
+  A.kscan = P->kscan;
+  A.dense = P->dense;
+  A.part_seed = d_part_seed;
+  A.n_part = n_part;
+  int64_t kp_ends[2] = {0, 0};  // kept documents covered by the partitions
+  LDDL_HIP(hipMemcpyAsync(&kp_ends[0], P->kp_off, 8, hipMemcpyDeviceToHost, st));
+  LDDL_HIP(hipMemcpyAsync(&kp_ends[1], P->kp_off + n_part, 8, hipMemcpyDeviceToHost, st));
+  LDDL_HIP(hipStreamSynchronize(st));
+  A.unit0 = (int64_t)prm->dup * kp_ends[0];
+  A.n_units = (int64_t)prm->dup * (kp_ends[1] - kp_ends[0]);
+  A.native_seed = prm->native_seed;
+  A.k_short = short_threshold(prm->short_seq_prob);
+  A.seq = prm->seq;
+  A.dup = prm->dup;
+  A.masking = prm->masking;
+  A.cls_id = c->tab.special_id[kCls];
+  A.sep_id = c->tab.special_id[kSep];
+  A.mask_id = c->tab.special_id[kMask];
+  A.vocab_size = c->vocab_size;
+  A.ratio = prm->masked_lm_ratio;
+  const int64_t nu = A.n_units;
+  int64_t *uoff, *scr;
+  int rc;
+  if ((rc = P->alloc(&A.ucnt, nu, st)) || (rc = P->alloc(&uoff, nu + 1, st)) ||
+      (rc = P->alloc(&scr, scan_scratch_elems(nu + 1), st)))
+    return rc;
+  LDDL_HIP(hipEventRecord(P->ev[0], st));
+  const unsigned gu = (unsigned)((nu + 255) / 256);
+  if (nu) hipLaunchKernelGGL(plan_native_kernel<false>, dim3(gu), dim3(256), 0, st, A);
+  LDDL_HIP(hipGetLastError());
+  LDDL_HIP(scan_exclusive(Identity{A.ucnt}, nu, uoff, scr, st));
+  LDDL_HIP(hipMemcpyAsync(&P->n_pairs, uoff + nu, 8, hipMemcpyDeviceToHost, st));
+  LDDL_HIP(hipStreamSynchronize(st));
+  const int64_t n = P->n_pairs;
+  A.uoff = uoff;
+  A.n_pairs = n;
+  if ((rc = P->alloc(&P->part_base, n_part + 1, st)) || (rc = P->alloc(&P->desc, n, st)) ||
+      (rc = P->alloc(&A.ppart, n, st)) || (rc = P->alloc(&P->src, n, st)))
+    return rc;
+  if (prm->masking &&
+      ((rc = P->alloc(&P->nmask, n, st)) || (rc = P->alloc(&A.ncand, n, st)) ||
+       (rc = P->alloc(&P->moff, n + 1, st)) || (rc = P->alloc(&scr, scan_scratch_elems(n + 1), st))))
+    return rc;
+  hipLaunchKernelGGL(native_part_base_kernel, dim3((unsigned)((n_part + 256) / 256)), dim3(256), 0,
+                     st, P->kp_off, n_part, prm->dup, uoff, P->part_base);
+  A.part_base = P->part_base;
+  A.desc = P->desc;
+  A.nmask = P->nmask;
+  if (nu) hipLaunchKernelGGL(plan_native_kernel<true>, dim3(gu), dim3(256), 0, st, A);
+  LDDL_HIP(hipGetLastError());
+  const unsigned gp = (unsigned)((n + 255) / 256);
+  if (prm->masking) {
+    LDDL_HIP(scan_exclusive(I32{P->nmask}, n, P->moff, scr, st));
+    LDDL_HIP(hipMemcpyAsync(&P->n_masked, P->moff + n, 8, hipMemcpyDeviceToHost, st));
+    LDDL_HIP(hipStreamSynchronize(st));
+    if ((rc = P->alloc(&P->mpos, P->n_masked, st)) || (rc = P->alloc(&P->mtok, P->n_masked, st)))
+      return rc;
+    A.moff = P->moff;
+    A.mpos = P->mpos;
+    A.mtok = P->mtok;
+    A.words = (prm->seq + 31) / 32;
+    if (n)
+      hipLaunchKernelGGL(mask_native_kernel, dim3(gp), dim3(256), (size_t)4 * 64 * 4 * A.words, st,
+                         A);
+    LDDL_HIP(hipGetLastError());
+  }
+  A.src = P->src;
+  if (n) hipLaunchKernelGGL(order_native_kernel, dim3(gp), dim3(256), 0, st, A);
+  LDDL_HIP(hipGetLastError());
+  LDDL_HIP(hipEventRecord(P->ev[1], st));
+  return 0;
+}
+
 extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params* prm,
                                const int64_t* d_sent_off, const int32_t* d_ids,
                                const int32_t* d_sent_len, int64_t n_sent,
@@ -958,7 +1340,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   if (!c || !prm) LDDL_FAIL(-1, "null argument");
   if (prm->seq < 5 || prm->seq > 65535) LDDL_FAIL(-1, "target_seq_length %d out of range", prm->seq);
   if (prm->dup < 1) LDDL_FAIL(-1, "duplicate_factor must be >= 1");
-  if (prm->rng != LDDL_RNG_REPLAY) LDDL_FAIL(-1, "rng mode %d not available", prm->rng);
+  if (prm->rng != LDDL_RNG_REPLAY && prm->rng != LDDL_RNG_NATIVE)
+    LDDL_FAIL(-1, "unknown rng mode %d", prm->rng);
   const int32_t cls = c->tab.special_id[kCls], sep = c->tab.special_id[kSep],
                 msk = c->tab.special_id[kMask];
   if (prm->masking && prm->seq > kMaxSeqGather)
@@ -1023,6 +1406,9 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     if (max_pred > kMaxPredLds) TRY((set_error("masked_lm_ratio * seq too large"), -1));
   }
   P->max_pred = max_pred;
+  if (prm->rng == LDDL_RNG_NATIVE) {
+    TRY(plan_native(P, c, prm, d_part_seed, n_part, st));
+  } else {
   int32_t* jseq;
   TRY(P->alloc(&P->desc, slots, st));
   TRY(P->alloc(&P->order, slots, st));
@@ -1144,12 +1530,13 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   if (scan_exclusive(Identity{part_npairs}, n_part, part_base, scratch, st) != hipSuccess) TRY(-100);
   LDDL_HIP(hipMemcpyAsync(&P->n_pairs, part_base + n_part, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
-  const int64_t npairs = P->n_pairs;
-  TRY(P->alloc(&P->src, npairs, st));
-  TRY(P->alloc(&P->tok_off, npairs + 1, st));
+  TRY(P->alloc(&P->src, P->n_pairs, st));
   if (n_part)
     hipLaunchKernelGGL(map_pairs_kernel, dim3((unsigned)n_part), dim3(256), 0, st, P->kd_off,
                        P->kp_off, prm->dup, part_base, P->order, P->src);
+  }  // replay
+  const int64_t npairs = P->n_pairs;
+  TRY(P->alloc(&P->tok_off, npairs + 1, st));
   int64_t* scr2;
   TRY(P->alloc(&scr2, scan_scratch_elems(npairs), st));
   if (scan_exclusive(PairTokens{P->src, P->desc}, npairs, P->tok_off, scr2, st) != hipSuccess)
