@@ -99,6 +99,8 @@ def main():
     ap.add_argument('--gen-threads', type=int, default=16)
     ap.add_argument('--cpu-sample-bytes', type=int, default=48 << 20)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-alt-rng', dest='alt_rng', action='store_false',
+                    help='skip timing the other RNG mode (reported as alt_rng)')
     ap.add_argument('--rng', choices=['replay', 'native'], default='replay',
                     help='replay: CPython MT19937 per partition, bit-exact with the reference; '
                          'native: Philox counter RNG, documents and pairs in parallel')
@@ -127,15 +129,15 @@ def main():
 
     diag = {}  # {'balance': {}}: balance() records synchronised phase times (untimed step only)
 
-    def step(ev=None):
+    def step(ev=None, rng=args.rng):
         if ev is not None:
             ev[0].record()
         ids, sent_len = ctx.tokenize(text, sent_off)
         if ev is not None:
             ev[1].record()
         pb = make_pairs(ctx, sent_off, ids, sent_len, doc_off, part_off, part_seed, seq=args.seq,
-                        dup=5, masking=True, short_seq_prob=0.1, masked_lm_ratio=0.15,
-                        rng=args.rng)
+                        dup=5, masking=True, short_seq_prob=0.1, masked_lm_ratio=0.15, rng=rng)
+        del ids
         if args.workload == 'c4':
             bb = balance(ctx, pb, 8, args.seq // 8, timings=diag.get('balance'))
             n_tok = int(bb.tokens.numel()) + 3 * bb.n_rows
@@ -149,24 +151,37 @@ def main():
         del pb  # nothing of a step outlives it (HBM is reused by the next step)
         return n_tok, st, sent_len
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    out_tokens = 0
-    stats = []
-    for k in range(args.steps):
-        n, st, sent_len = step(evs[k])
-        out_tokens += n
-        stats.append(st)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    def timed(rng):
+        """W untimed steps, then exactly K steps between barrier + synchronize; max over ranks."""
+        for _ in range(args.warmup):
+            step(rng=rng)
+        torch.cuda.synchronize()
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out_tokens = 0
+        stats = []
+        sent_len = None
+        for k in range(args.steps):
+            n, st, sent_len = step(evs[k], rng=rng)
+            out_tokens += n
+            stats.append(st)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+            n = torch.tensor([out_tokens], dtype=torch.float64, device=dev)
+            dist.all_reduce(n, op=dist.ReduceOp.SUM)
+            out_tokens = int(n.item())
+        return dt, out_tokens, evs, stats, sent_len
+
+    dt, out_tokens, evs, stats, sent_len = timed(args.rng)
     tok_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     pair_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     plan_ms = float(np.mean([s['plan_ms'] for s in stats]))
@@ -180,18 +195,19 @@ def main():
         bt = diag.pop('balance')
         keys = list(bt)
         bal_ms = {k: (bt[k] - bt[p]) * 1e3 for p, k in zip(keys, keys[1:])}
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        n = torch.tensor([out_tokens], dtype=torch.float64, device=dev)
-        dist.all_reduce(n, op=dist.ReduceOp.SUM)
-        out_tokens = int(n.item())
+    alt = None
+    if args.alt_rng:  # the other RNG mode on the same batch, reported beside the headline
+        other = 'native' if args.rng == 'replay' else 'replay'
+        adt, atok, _, astats, _ = timed(other)
+        alt = {'rng': other, 'value': atok / adt, 'ms_per_step': adt / args.steps * 1e3,
+               'plan_ms': float(np.mean([x['plan_ms'] for x in astats]))}
+    mem = torch.cuda.memory_stats()
     if rank != 0:
         dist.destroy_process_group()
         return
-    # Rooflines. Dominant kernel = plan_replay_kernel (CPython-exact pair/mask
-    # planner); its algorithmic bytes per launch: sentence lengths read per duplicate pass
+    # Rooflines of the planner and the tokenizer; `roofline` is the dominant one
+    # (the replay planner at C2/C4, the tokenizer under the native RNG). Planner algorithmic
+    # bytes per launch: sentence lengths read per duplicate pass
     # (4 B x dup x kept sentences) + document offsets (8 B x dup x kept documents) + per pair a
     # 32-B descriptor, 4-B shuffle draw, 4-B mask count and 8-B mask offset + 6 B per masked
     # position (2-B position + 4-B token) — all writes to HBM, the MT19937 state stays in LDS.
@@ -203,16 +219,35 @@ def main():
     # + sent_len (4 B / sentence)
     tok_bytes = n_bytes + 8 * (n_sent + 1) + 4 * pieces + 4 * n_sent
     achieved = tok_bytes / (tok_ms * 1e-3) / 1e9
-    prof_traffic = None
-    pmc = os.path.join(REPO, 'profiles', 'tokenize_pmc.json')
+    # HBM bytes per launch from the committed PMC passes (profiles/pmc_traffic.json, made by
+    # tools/make_pmc_json.py) when they were taken on the same batch size
+    pmc_kernels = {}
+    pmc = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
     if os.path.exists(pmc):
         try:
             with open(pmc) as f:
                 rec = json.load(f)
             if rec.get('batch_bytes') == args.batch_bytes:
-                prof_traffic = rec.get('hbm_bytes_per_launch')
-        except Exception:
-            prof_traffic = None
+                pmc_kernels = rec.get('kernels', {})
+        except (OSError, ValueError):
+            pmc_kernels = {}
+
+    def traffic(kernel):
+        return pmc_kernels.get(kernel, {}).get('hbm_bytes_per_launch')
+
+    plan_roof = {'kernel': 'plan_replay_kernel' if args.rng == 'replay' else
+                 'plan_native_kernel x2 + mask_native_kernel + order_native_kernel (HIP events '
+                 'around the native plan, host syncs included)',
+                 'bound': 'hbm', 'achieved': plan_gbs,
+                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': plan_gbs / HBM_PEAK_GBS,
+                 'traffic': traffic('plan_replay_kernel') if args.rng == 'replay' else None,
+                 'algorithmic_bytes_per_launch': plan_bytes, 'launch_ms': plan_ms,
+                 'note': ('issue-bound on the CU scalar unit, not HBM (DESIGN.md 4)'
+                          if args.rng == 'replay' else 'DESIGN.md 4')}
+    tok_roof = {'kernel': 'tokenize_batch_kernel', 'bound': 'hbm', 'achieved': achieved,
+                'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
+                'traffic': traffic('tokenize_batch_kernel'), 'algorithmic_bytes_per_launch': tok_bytes,
+                'launch_ms': tok_ms}
     res = {
         'metric': 'WordPiece+MLM tokens/sec (1/2/4/8 MI355X) and % of HBM roofline',
         'value': out_tokens / dt,
@@ -247,18 +282,16 @@ def main():
                        'pairs_bin_and_balance'): pair_ms,
                       'per_step_pairs': [round(e[1].elapsed_time(e[2]), 2) for e in evs],
                       'per_step_plan': [round(x['plan_ms'], 2) for x in stats]},
-        'roofline': {'kernel': 'plan_replay_kernel', 'bound': 'hbm', 'achieved': plan_gbs,
-                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': plan_gbs / HBM_PEAK_GBS,
-                     'traffic': None, 'algorithmic_bytes_per_launch': plan_bytes,
-                     'launch_ms': plan_ms,
-                     'note': 'issue-bound on the CU scalar unit, not HBM (DESIGN.md 4)'},
-        'roofline_tokenizer': {'kernel': 'tokenize_batch_kernel', 'bound': 'hbm',
-                               'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                               'frac': achieved / HBM_PEAK_GBS, 'traffic': prof_traffic,
-                               'algorithmic_bytes_per_launch': tok_bytes, 'launch_ms': tok_ms},
+        'roofline': None,  # the dominant kernel's, filled below
+        'roofline_planner': plan_roof,
+        'roofline_tokenizer': tok_roof,
     }
+    res['roofline'] = plan_roof if plan_ms >= tok_ms else tok_roof
     if bal_ms is not None:
         res['balance_phases_ms_untimed_step'] = bal_ms
+    if alt is not None:
+        res['alt_rng'] = alt
+    res['torch_alloc_retries'] = int(mem.get('num_alloc_retries', 0))
     if world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(corp, part, seeds, args)
     print(json.dumps(res), flush=True)
