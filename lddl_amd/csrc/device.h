@@ -113,6 +113,15 @@ struct Philox {
   }
 };
 
+// Lane mask of a predicate. The bool overload lets the compiler use the condition's lane mask
+// directly (HIP's __ballot(int) re-materialises it through a compare against zero).
+__device__ inline uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// Set bits of m below the calling lane (v_mbcnt).
+__device__ inline uint32_t popc_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // LDS written by some lanes of a wave becomes visible to all lanes of that wave
 __device__ inline void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -80,12 +80,12 @@ __global__ void __launch_bounds__(kBinThreads) bin_partitions_kernel(
     const int64_t r = c0 + lane;
     const bool in = r < r1;
     const int32_t b = in ? bin_of(num_tokens[r], bin_size, nbins) : -1;
-    uint64_t match = __ballot(in);
+    uint64_t match = ballot(in);
     for (int k = 0; k < nbits; ++k) {
-      const uint64_t bk = __ballot(in && ((b >> k) & 1));
+      const uint64_t bk = ballot(in && ((b >> k) & 1));
       match &= ((b >> k) & 1) ? bk : ~bk;
     }
-    const int rank = __popcll(match & below);
+    const int rank = (int)popc_below(match);
     int64_t base = 0;
     if (in) base = s_cnt[b];
     __builtin_amdgcn_wave_barrier();
@@ -135,16 +135,16 @@ __global__ void __launch_bounds__(64) bin_tile_scatter_kernel(
     const int64_t r = c0 + lane;
     const bool in = r < r1;
     const int32_t b = in ? bin_of(num_tokens[r], bin_size, nbins) : -1;
-    uint64_t match = __ballot(in);
+    uint64_t match = ballot(in);
     for (int k = 0; k < nbits; ++k) {
-      const uint64_t bk = __ballot(in && ((b >> k) & 1));
+      const uint64_t bk = ballot(in && ((b >> k) & 1));
       match &= ((b >> k) & 1) ? bk : ~bk;
     }
     int64_t base = 0;
     if (in) base = s_run[b];
     __builtin_amdgcn_wave_barrier();
     if (in) {
-      const int64_t dst = base + __popcll(match & below);
+      const int64_t dst = base + (int)popc_below(match);
       perm[dst] = r;
       bin_id[dst] = b;
       if ((match & below) == 0) s_run[b] = base + __popcll(match);

@@ -221,27 +221,28 @@ struct WaveRng {
   template <typename Sink>
   __device__ void fy_draws(int64_t n, Sink sink) {
     const int lane = threadIdx.x;
-    const uint64_t lt_mask = (1ull << lane) - 1;
     int32_t s0 = (int32_t)(n - 1);  // next step (uniform); n < 2^30 (host-checked)
     while (s0 >= 1) {
       if (mti >= kN) twist();
       const int L = min(64, kN - mti);
       const uint32_t w = lane < L ? temper(mt[mti + lane]) : 0u;
-      int32_t R = 0;
-      uint64_t rej = ~0ull;
-      int32_t i = 0;
-      uint32_t x = 0;
-      for (int it = 0; it < 66; ++it) {
+      const uint64_t Lm = L >= 64 ? ~0ull : ((1ull << L) - 1);
+      int32_t R = 0, i;
+      uint64_t rej = 0;
+      uint32_t x;
+      while (true) {  // R = 0 is the first guess; at most L + 1 passes (causality)
         i = s0 - lane + R;
         const int k = 32 - __clz((uint32_t)(i + 1));
-        x = i >= 1 ? w >> (32 - k) : 0u;
-        const uint64_t bm = __ballot(lane < L && i >= 1 && x > (uint32_t)i);
+        x = w >> ((32 - k) & 31);  // meaningful for i >= 1 only
+        // lane masks straight from the compares (no boolean round trip through a VGPR)
+        const uint64_t bm = Lm & __builtin_amdgcn_sicmp(i, 0, 38 /* sgt */) &
+                            __builtin_amdgcn_uicmp(x, (uint32_t)i, 34 /* ugt */);
         if (bm == rej) break;
         rej = bm;
-        R = __popcll(rej & lt_mask);
+        R = (int32_t)popc_below(rej);
       }
       // words consumed: up to the first lane past the last step (i < 1) or the window end
-      const uint64_t fin = __ballot(lane < L && i < 1);
+      const uint64_t fin = Lm & __builtin_amdgcn_sicmp(i, 1, 40 /* slt */);
       const int E = fin ? __ffsll((unsigned long long)fin) - 1 : L;
       if (lane < E && !((rej >> lane) & 1ull)) sink((int64_t)i, x);
       mti += E;
@@ -280,8 +281,8 @@ struct WaveRng {
       const int32_t t = done + lane;
       const bool front = lane < cnt && temper(mt[mti + 2 * lane]) < 0x80000000u;
       const bool sa = t < d || (t >= ad && ((t - ad) & 1));
-      a_front += __popcll(__ballot(front && sa));
-      b_front += __popcll(__ballot(front && !sa));
+      a_front += __popcll(ballot(front && sa));
+      b_front += __popcll(ballot(front && !sa));
       mti = uni(mti + 2 * cnt);
       done += cnt;
     }
@@ -388,11 +389,13 @@ struct PlanArgs {
   PairDesc* desc;
   int32_t* jseq;       // per slot: j_i draws of the final partition shuffle
   int32_t* nmask;      // per slot
-  uint16_t* mpos;      // mask pool: positions of slot s at moff[s] .. + nmask[s]
-  int32_t* mtok;       // mask pool: replacement tokens (kKeep = keep)
+  int32_t* mtok;       // mask pool: slot s's decisions at moff[s] .. + nmask[s] (shuffled order)
   int64_t* moff;       // per slot
-  unsigned long long* pool_used;
-  int64_t pool_cap;
+  uint16_t* jpool;     // draw pool: j_i of random.shuffle(cand_indexes) at joff[s] + i
+  int64_t* joff;       // per slot
+  int32_t* ncand;      // per slot: candidates (len(A) + len(B) minus literal [CLS]/[SEP])
+  unsigned long long* pool_used;  // [0] masks, [1] overflow flag, [2] draws
+  int64_t pool_cap, jpool_cap;
   int32_t* overflow;   // set when the pool is too small (the host re-plans with a larger one)
   int64_t* part_npairs;
   uint64_t* stamps;  // diagnostic build: [n_part][8]
@@ -426,16 +429,7 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* s_mt = reinterpret_cast<uint32_t*>(smem);
   uint32_t* s_tw = nullptr;
-  int32_t* s_doc = reinterpret_cast<int32_t*>(s_mt + kN);                 // [kDocLds + 1]
-  uint16_t* jarr = reinterpret_cast<uint16_t*>(s_doc + kDocLds + 4);     // [seq rounded to 64]
-  uint16_t* cand = jarr + A.seq_r64;                                       // [seq] (slow path)
-  uint16_t* tpos = cand + A.seq_r64;                                       // [max_pred]
-  int32_t* ttok = reinterpret_cast<int32_t*>(tpos + ((A.max_pred + 7) & ~7));
-  // traceback structures: nxt[v] = first later step that picks position v; pm[v] = lanes of the
-  // current slot chunk whose first pick is v (64-bit, two words); first[l] = lane l's first step
-  uint32_t* s_nxt = reinterpret_cast<uint32_t*>(ttok + ((A.max_pred + 3) & ~3));
-  uint32_t* s_pm = s_nxt + A.seq_r64;
-  uint32_t* s_first = s_pm + 2 * A.seq_r64;
+  int32_t* s_doc = reinterpret_cast<int32_t*>(s_mt + kN);  // [kDocLds + 1]
   const int p = blockIdx.x;
   const int lane = threadIdx.x;
   const bool leader = lane == 0;
@@ -456,7 +450,8 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
   };
   const int64_t base = (int64_t)A.dup * kbase;
   const int32_t max_num = A.seq - 3;
-  int64_t pool_cur = 0, pool_end = 0;  // this wave's current chunk of the mask pool
+  int64_t pool_cur = 0, pool_end = 0;    // this wave's current chunk of the mask pool
+  int64_t jpool_cur = 0, jpool_end = 0;  // ... and of the shuffle-draw pool
   LenWin La, Lb;
   int64_t np = 0;
   for (int dp = 0; dp < A.dup; ++dp) {
@@ -520,120 +515,68 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
         if (leader) A.desc[slot] = PairDesc{s0 + chunk0, b_ks, a_front, na, b_front,
                                             nb | (int32_t)((uint32_t)rn << 31)};
         if (A.masking) {
-          // candidates = positions of [CLS] A [SEP] B [SEP] whose token is not [CLS]/[SEP]
+          // candidates = positions of [CLS] A [SEP] B [SEP] whose token is not [CLS]/[SEP]; only
+          // their count matters here (fy_resolve_kernel recovers the positions)
           int32_t nc = na + nb;
-          const bool slow = (flags & kLenHasClsSep) != 0;
-          if (slow) {  // literal [CLS]/[SEP] inside A or B: inspect the tokens
+          if (flags & kLenHasClsSep) {  // literal [CLS]/[SEP] inside A or B: inspect the tokens
             int32_t c = 0;
             for (int32_t t = 0; t < na + nb; ++t) {
               const int32_t tok = uni(t < na ? span_token(A, s0 + chunk0, a_front + t)
                                              : span_token(A, b_ks, b_front + (t - na)));
-              if (tok != A.cls_id && tok != A.sep_id) {
-                if (leader) cand[c] = (uint16_t)(t < na ? t + 1 : t + 2);
-                ++c;
-              }
+              c += tok != A.cls_id && tok != A.sep_id;
             }
             nc = uni(c);
-            __syncthreads();
           }
           STAMP_ADD(1, st_t);
-          // random.shuffle(cand_indexes): draws j_i (i = nc-1 .. 1) into jarr
-          rng.fy_draws(nc, [&](int64_t i, uint32_t j) { jarr[i] = (uint16_t)j; });
-          STAMP_ADD(2, st_t);
           int32_t num = (int32_t)rint((double)(na + nb + 3) * A.ratio);  // round(): half-even
           if (num < 1) num = 1;
           if (num > nc) num = nc;
-          // Final slot pp of the shuffled candidates holds original index y: start at v0 = j_pp
-          // (j_0 = 0); the first later step i > pp with j_i = v0 moves it to i, after which
-          // only nxt[] applies (a step i' > i picking position i). nxt[] and the first steps are
-          // built with LDS atomics, so each slot is a short pointer chase instead of a pass over
-          // all nc steps.
-          constexpr uint32_t kNone = 0xFFFFFFFFu;
-          for (int i = lane; i < nc; i += 64) {
-            s_nxt[i] = kNone;
-            s_pm[2 * i] = 0u;
-            s_pm[2 * i + 1] = 0u;
-          }
-          __syncthreads();
-          for (int i = lane + 1; i < nc; i += 64) {
-            const uint32_t v = jarr[i];
-            if (v < (uint32_t)i) atomicMin(&s_nxt[v], (uint32_t)i);
-          }
-          for (int32_t c0 = 0; c0 < num; c0 += 64) {
-            const int pp = c0 + lane;
-            const bool act = pp < num;
-            const int v0 = act && pp > 0 ? (int)jarr[pp] : 0;
-            s_first[lane] = kNone;
-            if (act) atomicOr(&s_pm[2 * v0 + (lane >> 5)], 1u << (lane & 31));
-            __syncthreads();
-            for (int i = lane + 1; i < nc; i += 64) {
-              const int v = jarr[i];
-              const int lim = i - c0;  // lanes with pp < i
-              if (lim <= 0) continue;
-              uint64_t m = ((uint64_t)s_pm[2 * v + 1] << 32) | s_pm[2 * v];
-              if (lim < 64) m &= (1ull << lim) - 1;
-              while (m) {
-                const int b = __ffsll((unsigned long long)m) - 1;
-                atomicMin(&s_first[b], (uint32_t)i);
-                m &= m - 1;
-              }
-            }
-            __syncthreads();
-            int y = v0;
-            if (act) {
-              const uint32_t f = s_first[lane];
-              if (f != kNone) {
-                y = (int)f;
-                for (uint32_t nx = s_nxt[y]; nx != kNone; nx = s_nxt[y]) y = (int)nx;
-              }
-              s_pm[2 * v0 + (lane >> 5)] = 0u;  // reset for the next chunk
-            }
-            __syncthreads();
-            const int cval = slow ? (int)cand[y < nc ? y : 0] : (y < na ? y + 1 : y + 2);
-            STAMP_ADD(3, st_t);
-            const int cmax = min(64, num - c0);
-            int32_t mytok = 0;
-            rng.mask_decisions(cmax, kLt08, A.vocab_size, A.mask_id,
-                               [&](int c, int32_t tok) { mytok = lane == c ? tok : mytok; });
-            if (lane < cmax) {
-              tpos[c0 + lane] = (uint16_t)cval;
-              ttok[c0 + lane] = mytok;
-            }
-            STAMP_ADD(4, st_t);
-          }
-          __syncthreads();
-          // pool space for this pair's masks (bump allocation; order of pairs is irrelevant since
-          // each slot records its own offset)
-          if (pool_cur + num > pool_end) {  // a new chunk: one atomic per kPoolChunk masks
-            const int64_t sz = num > kPoolChunk ? num : kPoolChunk;
+          // pool space for this pair's shuffle draws (nc) and masks (num): bump allocation in
+          // per-wave chunks (one atomic per kPoolChunk entries); each slot records its offsets
+          if (pool_cur + num > pool_end) {
+            const int64_t sz = num > kPoolChunk ? (num + 7) & ~7 : kPoolChunk;
             int64_t nb0 = 0;
-            if (leader) nb0 = (int64_t)atomicAdd(A.pool_used, (unsigned long long)sz);
+            if (leader) nb0 = (int64_t)atomicAdd(&A.pool_used[0], (unsigned long long)sz);
             nb0 = ((int64_t)__shfl((int)(nb0 >> 32), 0, 64) << 32) |
                   (uint32_t)__shfl((int)(uint32_t)nb0, 0, 64);
             pool_cur = nb0;
             pool_end = nb0 + sz;
           }
-          const int64_t mb = pool_cur;
-          pool_cur += num;
-          const bool fits = pool_end <= A.pool_cap;
-          // sorted(masked_lms, key=index): rank sort (positions are distinct)
-          if (fits) {
-            for (int32_t c = lane; c < num; c += 64) {
-              const uint16_t v = tpos[c];
-              int32_t r = 0;
-              for (int32_t o = 0; o < num; ++o) r += tpos[o] < v;
-              A.mpos[mb + r] = v;
-              A.mtok[mb + r] = ttok[c];
-            }
-          } else if (leader) {
-            *A.overflow = 1;
+          if (jpool_cur + nc > jpool_end) {
+            const int64_t sz = nc > kPoolChunk ? (nc + 7) & ~7 : kPoolChunk;
+            int64_t nb0 = 0;
+            if (leader) nb0 = (int64_t)atomicAdd(&A.pool_used[2], (unsigned long long)sz);
+            nb0 = ((int64_t)__shfl((int)(nb0 >> 32), 0, 64) << 32) |
+                  (uint32_t)__shfl((int)(uint32_t)nb0, 0, 64);
+            jpool_cur = nb0;
+            jpool_end = nb0 + sz;
           }
+          const int64_t mb = pool_cur, jb = jpool_cur;
+          pool_cur += (num + 7) & ~7;  // 16-byte aligned regions (fy_resolve_kernel's uint4 I/O)
+          jpool_cur += (nc + 7) & ~7;
+          const bool fits = pool_end <= A.pool_cap && jpool_end <= A.jpool_cap;
+          if (!fits && leader) *A.overflow = 1;
+          // random.shuffle(cand_indexes): draws j_i (i = nc-1 .. 1) to the pool
+          uint16_t* jd = A.jpool + jb;
+          rng.fy_draws(nc, [&](int64_t i, uint32_t j) {
+            if (fits) jd[i] = (uint16_t)j;
+          });
+          STAMP_ADD(2, st_t);
+          // decisions of the masked candidates in shuffled order (pretrain.py:208-221)
+          for (int32_t c0 = 0; c0 < num; c0 += 64) {
+            const int cmax = min(64, num - c0);
+            int32_t mytok = 0;
+            rng.mask_decisions(cmax, kLt08, A.vocab_size, A.mask_id,
+                               [&](int c, int32_t tok) { mytok = lane == c ? tok : mytok; });
+            if (fits && lane < cmax) A.mtok[mb + c0 + lane] = mytok;
+          }
+          STAMP_ADD(4, st_t);
           if (leader) {
             A.nmask[slot] = num;
             A.moff[slot] = mb;
+            A.joff[slot] = jb;
+            A.ncand[slot] = nc;
           }
-          __syncthreads();
-          STAMP_ADD(5, st_t);
         }
         ++np;
         chunk_n = 0;
@@ -1076,9 +1019,10 @@ struct GatherArgs {
   const int64_t* src;
   const PairDesc* desc;
   const int32_t* nmask;
+  const int64_t* moff;
+  // masks: positions + replacements at moff (any order; ranks are taken from the map)
   const uint16_t* mpos;
   const int32_t* mtok;
-  const int64_t* moff;
   int32_t max_pred, masking, seq;
   int64_t n_pairs;
   const int64_t* tok_off;
@@ -1094,22 +1038,109 @@ constexpr int kMaxPredLds = 1024;
 constexpr int kMaxSeqGather = 4096;  // LDS position -> mask map per pair
 constexpr int kGWaves = 4;
 
+// Per-wave LDS of the gather: K maps (position -> 1 + mask index) and K decision tables.
+struct GatherLds {
+  int32_t map_len, max_pred;
+  __host__ __device__ static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+  __host__ __device__ size_t maps_bytes(int K) const { return align16((size_t)K * map_len * 2); }
+  __host__ __device__ size_t toks_bytes(int K) const { return align16((size_t)K * max_pred * 4); }
+  __host__ __device__ size_t per_wave(int K) const { return maps_bytes(K) + toks_bytes(K); }
+};
+
+// Replay masks, off the planner's sequential chain: one LANE per pair replays the recorded swaps
+// of random.shuffle(cand_indexes) (draws j_i, i = nc-1 .. 1) on a lane-private LDS column and
+// writes the candidates that end in slots 0 .. num-1, as positions of [CLS] A [SEP] B [SEP], in
+// slot order (= the order of the planner's decisions) over the mask pool. Steps i >= num only
+// move x[i] to x[j_i] (slot i is never read again); steps i < num finalise slot i = x[j_i].
+// Column layout x[k * 64 + lane] keeps the 64 lanes' accesses in distinct banks.
+struct ResolveArgs {
+  const int64_t* src;
+  int64_t n_pairs;
+  const PairDesc* desc;
+  const int32_t* nmask;
+  const int32_t* ncand;
+  const int64_t* moff;
+  const int64_t* joff;
+  const uint16_t* jpool;
+  uint16_t* mpos;
+  const int64_t* kscan;
+  const int32_t* dense;
+  int32_t cls_id, sep_id;
+};
+
+__global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
+  extern __shared__ uint16_t s_x[];
+  const int lane = threadIdx.x;
+  uint16_t* x = s_x + lane;
+  const int64_t q = (int64_t)blockIdx.x * 64 + lane;
+  if (q >= R.n_pairs) return;
+  const int64_t slot = R.src[q];
+  const int32_t num = R.nmask[slot];
+  if (num <= 0) return;
+  const int32_t nc = R.ncand[slot];
+  const int64_t jb = R.joff[slot], mb = R.moff[slot];  // both multiples of 8 (planner)
+  const PairDesc d = R.desc[slot];
+  const int32_t na = d.na, nb = d.nb_rn & 0x7FFFFFFF;
+  const bool fast = nc == na + nb;
+  for (int k = 0; k < nc; ++k) x[k * 64] = (uint16_t)k;
+  const uint4* jp = reinterpret_cast<const uint4*>(R.jpool + jb);
+  uint4* mp = reinterpret_cast<uint4*>(R.mpos + mb);
+  uint4 acc = make_uint4(0u, 0u, 0u, 0u);  // slots [8h, 8h+8) collected from the top down
+  uint4 nxt = jp[(nc - 1) >> 3];
+  for (int h = (nc - 1) >> 3; h >= 0; --h) {
+    const uint4 jv = nxt;
+    if (h > 0) nxt = jp[h - 1];  // next group of draws in flight
+    const uint32_t jw[4] = {jv.x, jv.y, jv.z, jv.w};
+#pragma unroll
+    for (int u = 7; u >= 0; --u) {
+      const int i = 8 * h + u;
+      if (i >= nc) continue;
+      const int j = (int)((jw[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
+      const int xi = x[i * 64];
+      if (i >= num) {
+        if (i >= 1) x[j * 64] = (uint16_t)xi;
+      } else {
+        const int y = i >= 1 ? (int)x[j * 64] : xi;  // slot 0 keeps x[0]
+        if (i >= 1) x[j * 64] = (uint16_t)xi;
+        const uint32_t pos = (uint32_t)(fast ? (y < na ? y + 1 : y + 2) : y);
+        // 128-bit shift register, newest at slot offset 0 (slots arrive in descending order)
+        acc = make_uint4((acc.x << 16) | pos, (acc.y << 16) | (acc.x >> 16),
+                         (acc.z << 16) | (acc.y >> 16), (acc.w << 16) | (acc.z >> 16));
+      }
+    }
+    if (8 * h < num) mp[h] = acc;  // slots [8h, 8h+8) complete (the top group zero-padded)
+  }
+  if (!fast) {  // literal [CLS]/[SEP] in the pair: candidate index -> position via the tokens
+    const int64_t ao = R.kscan[d.a_ks] + d.a_front, bo = R.kscan[d.b_ks] + d.b_front;
+    int k = 0;
+    for (int t = 0; t < na + nb; ++t) {
+      const int32_t tok = t < na ? R.dense[ao + t] : R.dense[bo + (t - na)];
+      if (tok != R.cls_id && tok != R.sep_id) x[(k++) * 64] = (uint16_t)(t < na ? t + 1 : t + 2);
+    }
+    uint16_t* m16 = R.mpos + mb;
+    for (int c = 0; c < num; ++c) m16[c] = x[m16[c] * 64];
+  }
+}
+
 // Gather: each wave emits K consecutive output pairs (their tokens are contiguous in the output).
 // Per pair: A = dense[kscan[a_ks] + a_front ..+ na), B likewise; output token x < na + nb comes from
-// A (x < na) or B. The masks of each pair go to an LDS map (position -> 1 + mask index) so each
-// output lane finds its own decision; labels take the original token. All K*C token loads of the
-// wave are issued before any is consumed (the kernel is bound by load latency and cache lines).
+// A (x < na) or B. The masks of each pair go to an LDS map (position -> 1 + mask index); each
+// output lane finds its own decision, and a ballot prefix over the map gives each masked token
+// its rank, i.e. its place in the position-sorted masked_lm_positions / labels (labels take the
+// original token). All K*C token loads of the wave are issued before any is consumed (the
+// kernel is bound by load latency and cache lines).
 template <int K, int C>
-__global__ void __launch_bounds__(64 * kGWaves) gather_kernel(GatherArgs G, int32_t map_len) {
+__global__ void __launch_bounds__(64 * kGWaves) gather_kernel(GatherArgs G, GatherLds Lg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  uint16_t* maps = reinterpret_cast<uint16_t*>(g_smem) + (size_t)w * K * map_len;
-  int32_t* toks = reinterpret_cast<int32_t*>(g_smem + (size_t)kGWaves * K * map_len * 2) +
-                  (size_t)w * K * G.max_pred;
+  uint8_t* wbase = g_smem + (size_t)w * Lg.per_wave(K);
+  uint16_t* maps = reinterpret_cast<uint16_t*>(wbase);
+  int32_t* toks = reinterpret_cast<int32_t*>(wbase + Lg.maps_bytes(K));
+  const int map_len = Lg.map_len;
   const int64_t qb = ((int64_t)blockIdx.x * kGWaves + w) * K;
 
-  int64_t slot[K], tof[K], aoff[K], boff[K];
-  int32_t na[K], nb[K], rn[K], nm[K];
+  int64_t slot[K], tof[K], aoff[K], boff[K], po[K];
+  int32_t na[K], nb[K], rn[K], nm[K], rk[K];
   bool act[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -1127,6 +1158,8 @@ __global__ void __launch_bounds__(64 * kGWaves) gather_kernel(GatherArgs G, int3
     boff[k] = act[k] ? G.kscan[d.b_ks] + d.b_front : 0;
     tof[k] = act[k] ? G.tok_off[qb + k] : 0;
     nm[k] = (G.masking && act[k]) ? G.nmask[slot[k]] : 0;
+    po[k] = (G.masking && act[k]) ? G.pos_off[qb + k] : 0;
+    rk[k] = 0;
   }
   for (int32_t cb = 0;; cb += 64 * C) {  // one pass for seq <= 64 * C + 3
     int32_t tok[K][C];
@@ -1145,12 +1178,12 @@ __global__ void __launch_bounds__(64 * kGWaves) gather_kernel(GatherArgs G, int3
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         if (!nm[k]) continue;
-        const int64_t mb = G.moff[slot[k]], po = G.pos_off[qb + k];
+        uint16_t* map = maps + k * map_len;
+        int32_t* tk = toks + k * G.max_pred;
+        const int64_t mb = G.moff[slot[k]];
         for (int j = lane; j < nm[k]; j += 64) {
-          const uint16_t pv = G.mpos[mb + j];
-          maps[k * map_len + pv] = (uint16_t)(j + 1);
-          toks[k * G.max_pred + j] = G.mtok[mb + j];
-          G.out_pos[po + j] = pv;
+          map[G.mpos[mb + j]] = (uint16_t)(j + 1);
+          tk[j] = G.mtok[mb + j];
         }
       }
       wave_sync();
@@ -1166,17 +1199,21 @@ __global__ void __launch_bounds__(64 * kGWaves) gather_kernel(GatherArgs G, int3
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         const int32_t x = cb + c * 64 + lane;
-        if (x < n) {
-          int32_t v = tok[k][c];
-          if (G.masking) {
-            const int m = map[x < na[k] ? x + 1 : x + 2];
-            if (m) {
-              G.out_lab[G.pos_off[qb + k] + m - 1] = v;
-              if (mt[m - 1] != kKeep) v = mt[m - 1];
-            }
+        const bool in = x < n;
+        const int32_t pos = x < na[k] ? x + 1 : x + 2;
+        int32_t v = tok[k][c];
+        if (G.masking) {
+          const int m = in ? (int)map[pos] : 0;
+          const uint64_t bits = ballot(m != 0);
+          if (m) {
+            const int64_t o = po[k] + rk[k] + (int)popc_below(bits);
+            G.out_pos[o] = (uint16_t)pos;
+            G.out_lab[o] = v;
+            if (mt[m - 1] != kKeep) v = mt[m - 1];
           }
-          out[x] = v;
+          rk[k] += __popcll(bits);
         }
+        if (in) out[x] = v;
       }
       more |= n > cb + 64 * C;
       if (cb == 0 && lane == 0) {
@@ -1196,7 +1233,7 @@ using namespace lddl;
 // Device-resident plan of one batch of partitions (library-owned temporaries).
 struct lddl_pairs {
   int device = 0;
-  int32_t masking = 0, max_pred = 0, seq = 0;
+  int32_t masking = 0, max_pred = 0, seq = 0, cls_id = -1, sep_id = -1;
   int64_t n_part = 0, n_pairs = 0, n_tokens = 0, n_masked = 0, n_kept_sent = 0, n_kept_doc = 0;
   std::vector<void*> allocs;
   // views
@@ -1354,6 +1391,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   P->n_part = n_part;
   P->masking = prm->masking;
   P->seq = prm->seq;
+  P->cls_id = cls;
+  P->sep_id = sep;
   TRY(hipEventCreate(&P->ev[0]) == hipSuccess && hipEventCreate(&P->ev[1]) == hipSuccess
           ? 0 : (set_error("hipEventCreate failed"), -100));
   int64_t *ks_pos, *kd_pos, *scratch, *part_npairs, *part_base;
@@ -1414,9 +1453,13 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   TRY(P->alloc(&P->order, slots, st));
   TRY(P->alloc(&jseq, slots, st));
   TRY(P->alloc(&part_npairs, n_part + 1, st));
+  int64_t* joff = nullptr;
+  int32_t* ncand = nullptr;
   if (prm->masking) {
     TRY(P->alloc(&P->nmask, slots, st));
     TRY(P->alloc(&P->moff, slots, st));
+    TRY(P->alloc(&joff, slots, st));
+    TRY(P->alloc(&ncand, slots, st));
   }
   PlanArgs A{};
   A.kscan = P->kscan;
@@ -1449,16 +1492,18 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   A.stamps = d_stamps;
 #endif
   if (prm->seq > 512) TRY((set_error("replay planner supports target_seq_length <= 512"), -1));
-  const size_t lds = 4 * kN + 4 * (kDocLds + 4) + 4 * (size_t)A.seq_r64 +
-                     2 * ((max_pred + 7) & ~7) + 4 * ((max_pred + 3) & ~3) +
-                     12 * (size_t)A.seq_r64 + 4 * 64 + 16;
-  // mask pool: sized from the kept tokens (expected use ~0.15 * 1.5 * dup * tokens + pairs); a
-  // plan that outgrows it reports the exact size and is planned again (deterministic replay)
-  unsigned long long* pool_ctl;  // [0] used, [1] overflow flag
-  TRY(P->alloc(&pool_ctl, 2, st));
-  int64_t cap = 0;
+  const size_t lds = 4 * kN + 4 * (kDocLds + 4) + 16;
+  A.joff = joff;
+  A.ncand = ncand;
+  // pools: decisions (int32, shuffled order) and shuffle draws (uint16), sized from the kept
+  // tokens (expected use ~0.15 * 1.5 and ~1.5 times dup * tokens); a plan that outgrows them
+  // reports the exact sizes and is planned again (deterministic replay)
+  unsigned long long* pool_ctl;  // [0] masks used, [1] overflow flag, [2] draws used
+  TRY(P->alloc(&pool_ctl, 3, st));
+  int64_t cap = 0, jcap = 0;
+  uint16_t* jpool = nullptr;
   if (prm->masking && n_sent) {
-    LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 16, st));
+    LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 24, st));
     hipLaunchKernelGGL(sum_tokens_kernel, dim3(1024), dim3(256), 0, st, d_sent_len, n_sent,
                        pool_ctl);
     unsigned long long kept_tokens = 0;
@@ -1466,19 +1511,20 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     LDDL_HIP(hipStreamSynchronize(st));
     cap = (int64_t)(2.0 * prm->masked_lm_ratio * prm->dup * (double)kept_tokens) +
           (int64_t)prm->dup * P->n_kept_sent / 2 + kPoolChunk * (n_part + 16);
+    jcap = (int64_t)(1.6 * prm->dup * (double)kept_tokens) + kPoolChunk * (n_part + 16);
     if (const char* e = getenv("LDDL_AMD_MASK_POOL")) cap = atoll(e);  // tests: force a re-plan
   }
   for (int attempt = 0; n_part; ++attempt) {
-    uint16_t* mpos = nullptr;
     int32_t* mtok = nullptr;
     if (prm->masking) {
-      LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 16, st));
-      LDDL_HIP(hipMallocAsync((void**)&mpos, 2 * (size_t)cap + 16, st));
+      LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 24, st));
       LDDL_HIP(hipMallocAsync((void**)&mtok, 4 * (size_t)cap + 16, st));
+      LDDL_HIP(hipMallocAsync((void**)&jpool, 2 * (size_t)jcap + 16, st));
     }
-    A.mpos = mpos;
     A.mtok = mtok;
+    A.jpool = jpool;
     A.pool_cap = cap;
+    A.jpool_cap = jcap;
     A.pool_used = pool_ctl;
     A.overflow = reinterpret_cast<int32_t*>(pool_ctl + 1);
     LDDL_HIP(hipEventRecord(P->ev[0], st));
@@ -1486,20 +1532,22 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     LDDL_HIP(hipGetLastError());
     LDDL_HIP(hipEventRecord(P->ev[1], st));
     if (!prm->masking) break;
-    unsigned long long ctl[2];
-    LDDL_HIP(hipMemcpyAsync(ctl, pool_ctl, 16, hipMemcpyDeviceToHost, st));
+    unsigned long long ctl[3];
+    LDDL_HIP(hipMemcpyAsync(ctl, pool_ctl, 24, hipMemcpyDeviceToHost, st));
     LDDL_HIP(hipStreamSynchronize(st));
     if (!ctl[1]) {
-      P->mpos = mpos;
       P->mtok = mtok;
-      P->allocs.push_back(mpos);
       P->allocs.push_back(mtok);
+      P->allocs.push_back(jpool);
+      TRY(P->alloc(&P->mpos, (int64_t)ctl[0], st));
       break;
     }
-    (void)hipFreeAsync(mpos, st);
     (void)hipFreeAsync(mtok, st);
+    (void)hipFreeAsync(jpool, st);
+    jpool = nullptr;
     if (attempt > 0) TRY((set_error("mask pool overflow after resize"), -1));
     cap = (int64_t)ctl[0] + 1024;
+    jcap = (int64_t)ctl[2] + 1024;
   }
   if (n_part)
     hipLaunchKernelGGL(apply_shuffle_kernel, dim3((unsigned)n_part), dim3(64),
@@ -1534,6 +1582,13 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   if (n_part)
     hipLaunchKernelGGL(map_pairs_kernel, dim3((unsigned)n_part), dim3(256), 0, st, P->kd_off,
                        P->kp_off, prm->dup, part_base, P->order, P->src);
+  if (prm->masking && P->n_pairs) {
+    ResolveArgs RA{P->src, P->n_pairs, P->desc, P->nmask, ncand, P->moff, joff, jpool,
+                   P->mpos, P->kscan, P->dense, cls, sep};
+    hipLaunchKernelGGL(fy_resolve_kernel, dim3((unsigned)((P->n_pairs + 63) / 64)), dim3(64),
+                       (size_t)2 * 64 * (size_t)std::max(prm->seq, 1), st, RA);
+    LDDL_HIP(hipGetLastError());
+  }
   }  // replay
   const int64_t npairs = P->n_pairs;
   TRY(P->alloc(&P->tok_off, npairs + 1, st));
@@ -1572,9 +1627,9 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
   G.src = P->src;
   G.desc = P->desc;
   G.nmask = P->nmask;
+  G.moff = P->moff;
   G.mpos = P->mpos;
   G.mtok = P->mtok;
-  G.moff = P->moff;
   G.max_pred = P->max_pred;
   G.masking = P->masking;
   G.seq = P->seq;
@@ -1586,12 +1641,12 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
   G.is_rn = d_is_rn;
   G.out_pos = d_pos;
   G.out_lab = d_lab;
-  const int32_t map_len = (P->seq + 1) & ~1;
+  GatherLds Lg{(P->seq + 1) & ~1, P->max_pred};
   auto launch = [&](auto kern, int K) {
     const int64_t per_wg = (int64_t)K * kGWaves;
-    const size_t lds = P->masking ? (size_t)kGWaves * K * (2 * map_len + 4 * P->max_pred) : 0;
+    const size_t lds = P->masking ? (size_t)kGWaves * Lg.per_wave(K) : 0;
     hipLaunchKernelGGL(kern, dim3((unsigned)((P->n_pairs + per_wg - 1) / per_wg)),
-                       dim3(64 * kGWaves), lds, st, G, map_len);
+                       dim3(64 * kGWaves), lds, st, G, Lg);
   };
 #ifndef LDDL_GK128
 #define LDDL_GK128 4

@@ -350,7 +350,6 @@ __device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
                                      const uint8_t* __restrict__ text, int64_t pos, int64_t b1,
                                      uint32_t byte, WL& W) {
   const int lane = lane_id();
-  const uint64_t below = lanes_below();
   const int64_t i = pos + lane;
   const bool in = i < b1;
   uint32_t cls = kSpace;  // beyond the sentence: a separator
@@ -375,7 +374,7 @@ __device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
       slow = true;
     }
   }
-  const uint64_t V2 = __ballot(cplen == 2), V3 = __ballot(cplen == 3), V4 = __ballot(cplen == 4);
+  const uint64_t V2 = ballot(cplen == 2), V3 = ballot(cplen == 3), V4 = ballot(cplen == 4);
   const uint64_t C1 = (V2 | V3 | V4) << 1, C2 = (V3 | V4) << 2, C3 = V4 << 3;
   const bool covered = cont && (((C1 | C2 | C3) >> lane) & 1ull);
   const int dist = !covered ? 0 : ((C1 >> lane) & 1ull) ? 1 : ((C2 >> lane) & 1ull) ? 2 : 3;
@@ -386,16 +385,16 @@ __device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
     cplen = 0;
   }
   const bool cp_last = covered ? (dist == (lead_len >> 4) - 1) : (cplen <= 1);
-  const uint64_t S = __ballot(spk >= 0), S6 = __ballot(spk == kMask);
+  const uint64_t S = ballot(spk >= 0), S6 = ballot(spk == kMask);
   const uint64_t inside = (S << 1) | (S << 2) | (S << 3) | (S << 4) | (S6 << 5);
   const bool in_sp = ((S | inside) >> lane) & 1ull;
   const uint32_t cat = in_sp ? kCatSpecial : cls == kSpace ? kCatSep : cls == kIso ? kCatIso : kCatRun;
-  const uint64_t RUN = __ballot(cat == kCatRun);
-  const uint64_t LEAD = __ballot(cplen > 0);
-  const uint64_t ISO = __ballot(cat == kCatIso);
-  const uint64_t CPL = __ballot(cp_last);
+  const uint64_t RUN = ballot(cat == kCatRun);
+  const uint64_t LEAD = ballot(cplen > 0);
+  const uint64_t ISO = ballot(cat == kCatIso);
+  const uint64_t CPL = ballot(cp_last);
   WinResult R;
-  R.slow = __ballot(slow);
+  R.slow = ballot(slow);
   R.fallback = false;
   const bool tail_known = pos + 64 >= b1;  // position 64 is past the sentence end
   const uint64_t US = S | (ISO & LEAD) | (RUN & ~(RUN << 1));
@@ -421,11 +420,11 @@ __device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
     R.next = pos + (hl > hc ? hl : 64);
   }
   if ((US >> lane) & 1ull) {
-    const int k = __popcll(US & below);
+    const int k = (int)popc_below(US);
     W.us[k] = (uint8_t)lane;
     W.uk[k] = (uint8_t)(spk >= 0 ? 2 + spk : cat == kCatIso ? 1 : 0);
   }
-  if ((UE >> lane) & 1ull) W.ue[__popcll(UE & below)] = (uint8_t)lane;
+  if ((UE >> lane) & 1ull) W.ue[popc_below(UE)] = (uint8_t)lane;
   wave_sync();
   return R;
 }
@@ -543,12 +542,12 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
         npc = unit_pieces(T, T.bloom, text, n_bytes, pos + us, ulen, kind, unit_slow, pc,
                           W.nrm + lane * kNorm, cs_flag);
       }
-      if (__ballot(npc < 0)) { fallback = true; break; }
+      if (ballot(npc < 0)) { fallback = true; break; }
       const int incl = wave_incl_scan(npc);
       const int o = emitted + incl - npc;
       for (int q = 0; q < npc; ++q)
         if (o + q < max_pieces) ids[b0 + o + q] = pc.get(q);
-      if (__ballot(cs_flag && o < max_pieces)) flags = kLenHasClsSep;
+      if (ballot(cs_flag && o < max_pieces)) flags = kLenHasClsSep;
       emitted += __shfl(incl, 63, 64);
       pos = R.next;
       wave_sync();
@@ -629,7 +628,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
     const int incl = wave_incl_scan(npc);
     const int excl = incl - npc;
     const int prev_slot = __shfl(slot, lane > 0 ? lane - 1 : 0, 64);
-    const uint64_t F = __ballot(lane < m && (lane == 0 || slot != prev_slot));
+    const uint64_t F = ballot(lane < m && (lane == 0 || slot != prev_slot));
     const int s0 = 63 - __clzll(F & (lane == 63 ? ~0ull : ((2ull << lane) - 1)));
     const int seg_excl = excl - __shfl(excl, s0, 64);
     const int next_slot = __shfl(slot, lane < 63 ? lane + 1 : 63, 64);

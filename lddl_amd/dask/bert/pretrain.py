@@ -131,7 +131,8 @@ def process_batch(ctx, args, partitions, corpus, outdir):
     pb = make_pairs(ctx, d_so, ids, sent_len, torch.from_numpy(doc_sent_off).to(dev),
                     torch.from_numpy(part_doc_off).to(dev), torch.from_numpy(seeds).to(dev),
                     seq=args.target_seq_length, dup=args.duplicate_factor, masking=args.masking,
-                    short_seq_prob=args.short_seq_prob, masked_lm_ratio=args.masked_lm_ratio)
+                    short_seq_prob=args.short_seq_prob, masked_lm_ratio=args.masked_lm_ratio,
+                    rng=getattr(args, 'rng', 'replay'), native_seed=args.seed)
     part_rows = pb.part_off.cpu().numpy()
     index = [p for p, _ in partitions]
     if args.bin_size is not None:
@@ -280,6 +281,11 @@ def attach_args(parser=None):
     parser.add_argument('--masked-lm-ratio', type=float, default=0.15, help='Default: 0.15')
     parser.add_argument('--gpu-batch-bytes', type=int, default=1 << 30,
                         help='lddl_amd: input text bytes per GPU batch of partitions')
+    parser.add_argument('--rng', choices=['replay', 'native'], default='replay',
+                        help="lddl_amd: 'replay' reproduces CPython random per partition "
+                             "(random.seed(partition seed)), bit-exact with the reference; "
+                             "'native' draws the same distributions from Philox counter streams "
+                             "keyed by --seed (documents and pairs in parallel)")
     return parser
 
 

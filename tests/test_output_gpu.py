@@ -170,3 +170,30 @@ def test_bin_stable_single_segment_vs_oracle(ctx):
         np.testing.assert_array_equal(perm.cpu().numpy(), eo)
         np.testing.assert_array_equal(bin_id.cpu().numpy(), eb[eo])
         np.testing.assert_array_equal(counts.cpu().numpy(), ec)
+
+
+def test_pretrain_cli_native_rng(tmp_path):
+    """--rng native: same layout and schema; every row is a valid masked NSP sample."""
+    from lddl_amd.dask.bert import pretrain as P
+    src = tmp_path / 'source'
+    _write_source(str(src))
+    sink = tmp_path / 'out'
+    argv = ['--schedule', 'local', '--wikipedia', str(src), '--sink', str(sink), '--masking',
+            '--target-seq-length', '128', '--num-blocks', '4', '--seed', '7', '--rng', 'native',
+            '--vocab-file', VOCAB_UNCASED, '--local-n-workers', '1', '--duplicate-factor', '2',
+            '--bin-size', '32']
+    P.main(P.attach_args().parse_args(argv))
+    n = 0
+    for p in range(4):
+        for b in range(4):
+            t = pq.read_table(sink / 'part.{}.parquet_{}'.format(p, b)).to_pylist()
+            for r in t:
+                na, nb = len(r['A'].split()), len(r['B'].split())
+                assert r['num_tokens'] == na + nb + 3 <= 128 and na >= 1 and nb >= 1
+                assert r['bin_id'] == b == min((r['num_tokens'] - 1) // 32, 3)
+                pos = np.frombuffer(r['masked_lm_positions'][-2 * len(r['masked_lm_labels'].split()):],
+                                    np.uint16)
+                assert len(pos) == max(1, int(np.round(r['num_tokens'] * 0.15)))
+                assert np.all(np.diff(pos.astype(int)) > 0)
+                n += 1
+    assert n > 50
