@@ -164,7 +164,7 @@ extern "C" int lddl_ctx_create(int device, const uint8_t* norm_table, int64_t ta
     bool lower_ok = true, ident_ok = true;
     for (uint32_t cp = 0; cp < 128; ++cp) {
       const uint32_t e = pg[cp];
-      if ((e >> 30) != kWord) continue;
+      if ((e >> 30) != kWord && (e >> 30) != kIso) continue;  // both take the register path
       const uint32_t outc = (e & kIdent) ? cp : (e & kMulti) ? 0xFFFFFFFFu : (e & 0x1FFFFFu);
       const uint32_t want_lower = (cp >= 'A' && cp <= 'Z') ? cp + 32 : cp;
       lower_ok &= outc == want_lower;

@@ -216,7 +216,7 @@ enum : uint32_t { kCatRun = 0, kCatSep = 1, kCatIso = 2, kCatSpecial = 3 };
 struct alignas(16) WaveLds {
   uint8_t us[64], ue[64], uk[64];  // unit k: first byte, last byte (window-relative), kind
   int32_t pcs[kPcs * 64];          // lane l's pieces at pcs[64 q + l]
-  uint8_t nrm[64 * kNorm];         // lane l's normalised word (generic path)
+  alignas(16) uint8_t nrm[64 * kNorm];  // lane l's normalised word (generic path)
 };
 
 // Order this wave's LDS writes before its later LDS reads of other lanes' data (the waves of a
@@ -229,11 +229,26 @@ __device__ inline int match_special_at(const Tables& T, const uint8_t* b, int64_
   return -1;
 }
 
-// 128-bit little-endian byte string shifted down by `sh` bytes (0..15)
-__device__ inline void shr128(uint64_t lo, uint64_t hi, int sh, uint64_t& a, uint64_t& b) {
-  if (sh == 0) { a = lo; b = hi; }
-  else if (sh < 8) { a = (lo >> (8 * sh)) | (hi << (64 - 8 * sh)); b = hi >> (8 * sh); }
-  else { a = hi >> (8 * (sh - 8)); b = 0; }
+// Up to 32 bytes of a word as four little-endian 64-bit words (bytes past the word: don't care,
+// every use masks by length).
+struct B32 {
+  uint64_t w0, w1, w2, w3;
+};
+
+// bytes [s, 32) moved to the front (s in 0..31)
+__device__ inline B32 shr_bytes(const B32& v, int s) {
+  const int q = s >> 3, r = (s & 7) * 8;
+  uint64_t a0 = q == 0 ? v.w0 : q == 1 ? v.w1 : q == 2 ? v.w2 : v.w3;
+  uint64_t a1 = q == 0 ? v.w1 : q == 1 ? v.w2 : q == 2 ? v.w3 : 0ull;
+  uint64_t a2 = q == 0 ? v.w2 : q == 1 ? v.w3 : 0ull;
+  uint64_t a3 = q == 0 ? v.w3 : 0ull;
+  if (r) {
+    a0 = (a0 >> r) | (a1 << (64 - r));
+    a1 = (a1 >> r) | (a2 << (64 - r));
+    a2 = (a2 >> r) | (a3 << (64 - r));
+    a3 >>= r;
+  }
+  return B32{a0, a1, a2, a3};
 }
 
 // The pieces of one unit: the lane's column of an LDS buffer (lane l's piece q at b[64 q]).
@@ -243,10 +258,11 @@ struct Pcs {
   __device__ int32_t get(int q) const { return b[64 * q]; }
 };
 
-// Vocab probe for a key held in registers: bytes [0,8) in a, [8,16) in b (len <= 16).
-__device__ inline int32_t probe_reg(const Tables& T, uint64_t a, uint64_t b, int len, uint32_t cont) {
-  const uint64_t k0 = keep_bytes(a, len);
-  const uint32_t k1 = (uint32_t)keep_bytes(b, len - 8 < 4 ? len - 8 : 4);
+// Vocab probe of the first `len` (1..32) bytes of a: exact key for <= 12 bytes (k0 = bytes 0..7,
+// k1 = bytes 8..11), longer pieces confirmed against their bytes.
+__device__ inline int32_t probe32(const Tables& T, const B32& a, int len, uint32_t cont) {
+  const uint64_t k0 = keep_bytes(a.w0, len);
+  const uint32_t k1 = (uint32_t)keep_bytes(a.w1, len - 8 < 4 ? len - 8 : 4);
   const uint32_t want = kMetaValid | (cont ? kMetaCont : 0u) | (len > 12 ? kMetaLong : 0u) |
                         ((uint32_t)len << 21);
   for (uint32_t slot = (uint32_t)vhash(k0, k1, len, cont) & T.vmask;; slot = (slot + 1) & T.vmask) {
@@ -257,19 +273,25 @@ __device__ inline int32_t probe_reg(const Tables& T, uint64_t a, uint64_t b, int
       if (len <= 12) return id;
       const uint8_t* p = T.vbytes + T.voff[id];
       bool ok = true;
-      for (int i = 12; i < len; ++i) ok &= p[i] == (uint8_t)(b >> (8 * (i - 8)));
+      for (int i = 12; i < len; ++i) {
+        const uint64_t wv = i < 16 ? a.w1 : i < 24 ? a.w2 : a.w3;
+        ok &= p[i] == (uint8_t)(wv >> (8 * (i & 7)));
+      }
       if (ok) return id;
     }
   }
 }
 
-// Bloom candidates for the pieces starting at the word's first byte held in (a, b): bit L-1 of
-// the result is set iff the filter may contain (cont, bytes[0, L)), L = 1 .. maxl.
-__device__ inline uint32_t bloom_candidates(const uint32_t* bloom, uint64_t a, uint64_t b, int maxl,
-                                            uint32_t cont) {
+// Bloom candidates for the pieces starting at a's first byte: bit L-1 set iff the filter may
+// contain (cont, bytes[0, L)), L = 1 .. maxl (<= 32).
+__device__ inline uint32_t bloom_candidates32(const uint32_t* bloom, const B32& a, int maxl,
+                                              uint32_t cont) {
   uint32_t h = 0, cand = 0;
-  for (int L = 1; L <= maxl; ++L) {
-    const uint32_t byte = (uint32_t)((L <= 8 ? a >> (8 * (L - 1)) : b >> (8 * (L - 9))) & 0xFFu);
+#pragma unroll
+  for (int L = 1; L <= 32; ++L) {
+    if (L > maxl) break;
+    const uint64_t wv = L <= 8 ? a.w0 : L <= 16 ? a.w1 : L <= 24 ? a.w2 : a.w3;
+    const uint32_t byte = (uint32_t)(wv >> (8 * ((L - 1) & 7))) & 0xFFu;
     h = h * kBloomP + byte + 1u;
     const uint32_t x = bloom_mix(h, (uint32_t)L, cont);
     const uint32_t m = bloom_bits(x);
@@ -278,56 +300,37 @@ __device__ inline uint32_t bloom_candidates(const uint32_t* bloom, uint64_t a, u
   return cand;
 }
 
-// Greedy longest-match WordPiece of an ASCII word of nb <= 16 bytes held in (lo, hi).
-// Returns the piece count written to pc (< kPcs), or -1 if more than kPcs pieces. The longest
-// candidate is probed first (most words are one piece); when it misses, the Bloom filter (LDS)
-// rules out the shorter lengths that cannot be pieces, so only likely ones are probed.
-__device__ int wordpiece_reg(const Tables& T, const uint32_t* bloom, uint64_t lo, uint64_t hi,
-                             int nb, Pcs& pc) {
+// Greedy longest-match WordPiece (HF WordPiece::tokenize) of a normalised word of nb <= 32 bytes
+// held in registers. ends: bit e set iff a piece may end at byte e (a UTF-8 character boundary;
+// all bits for ASCII). Returns the piece count written to pc, or -1 if more than kPcs pieces.
+// The longest candidate is probed first (most words are one piece); when it misses, the Bloom
+// filter (LDS) rules out the shorter lengths that cannot be pieces.
+__device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v, int nb,
+                           uint64_t ends, Pcs& pc) {
   int n = 0, start = 0;
   while (start < nb) {
-    uint64_t a, b;
-    shr128(lo, hi, start, a, b);
+    const B32 a = shr_bytes(v, start);
     const uint32_t cont = start > 0;
+    const uint64_t e = ends >> start;  // bit L: a piece of length L may end here
     int len = nb - start < T.max_piece_bytes ? nb - start : T.max_piece_bytes;
-    int32_t id = probe_reg(T, a, b, len, cont);
-    if (id < 0) {
-      uint32_t cand = len > 1 ? bloom_candidates(bloom, a, b, len - 1, cont) : 0u;
+    while (len > 0 && !((e >> len) & 1ull)) --len;
+    int32_t id = len > 0 ? probe32(T, a, len, cont) : -1;
+    if (id < 0 && len > 1) {
+      uint32_t cand = bloom_candidates32(bloom, a, len - 1, cont) & (uint32_t)(e >> 1);
       while (cand) {
         len = 32 - __clz(cand);
-        id = probe_reg(T, a, b, len, cont);
+        id = probe32(T, a, len, cont);
         if (id >= 0) break;
         cand &= ~(1u << (len - 1));
       }
     }
-    if (id < 0) {
+    if (id < 0) {  // no piece: the whole word is [UNK]
       pc.put(0, T.special_id[kUnk]);
       return 1;
     }
     if (n == kPcs) return -1;
     pc.put(n++, id);
     start += len;
-  }
-  return n;
-}
-
-// Greedy longest-match WordPiece of a normalised word in LDS (UTF-8, nb bytes, nc chars).
-__device__ int wordpiece_lds(const Tables& T, const uint8_t* w, int nb, int nc, Pcs& pc) {
-  if (nc == 0) return 0;
-  if (nc > 100) { pc.put(0, T.special_id[kUnk]); return 1; }
-  int n = 0, start = 0;
-  while (start < nb) {
-    int end = nb < start + T.max_piece_bytes ? nb : start + T.max_piece_bytes;
-    int32_t found = -1;
-    for (; end > start; --end) {
-      if (end < nb && (w[end] & 0xC0) == 0x80) continue;  // not a char boundary
-      found = lookup(T, w, start, end - start, start > 0);
-      if (found >= 0) break;
-    }
-    if (found < 0) { pc.put(0, T.special_id[kUnk]); return 1; }
-    if (n == kPcs) return -1;
-    pc.put(n++, found);
-    start = end;
   }
   return n;
 }
@@ -429,38 +432,44 @@ __device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
   return R;
 }
 
-// 16 bytes of text from byte `start` (unaligned) as two little-endian 64-bit words; bytes at or
-// past `n_bytes` read as 0 and are never loaded.
-__device__ inline void load16(const uint8_t* __restrict__ text, int64_t n_bytes, int64_t start,
-                              uint64_t& lo, uint64_t& hi) {
+// 32 bytes of text from byte `start` (unaligned); bytes at or past `n_bytes` read as 0 and are
+// never loaded.
+__device__ inline B32 load32(const uint8_t* __restrict__ text, int64_t n_bytes, int64_t start) {
   const int64_t a = start & ~(int64_t)3;
   const int r = (int)(start & 3);
-  uint32_t d[5];
-  if (a + 20 <= n_bytes) {
+  uint32_t d[9];
+  if (a + 36 <= n_bytes) {
     const uint32_t* p = reinterpret_cast<const uint32_t*>(text + a);
 #pragma unroll
-    for (int k = 0; k < 5; ++k) d[k] = p[k];
+    for (int k = 0; k < 9; ++k) d[k] = p[k];
   } else {
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < 9; ++k) {
       uint32_t v = 0;
       for (int q = 0; q < 4; ++q)
         if (a + 4 * k + q < n_bytes) v |= (uint32_t)text[a + 4 * k + q] << (8 * q);
       d[k] = v;
     }
   }
-  const uint32_t a0 = __builtin_amdgcn_alignbyte(d[1], d[0], r);
-  const uint32_t a1 = __builtin_amdgcn_alignbyte(d[2], d[1], r);
-  const uint32_t a2 = __builtin_amdgcn_alignbyte(d[3], d[2], r);
-  const uint32_t a3 = __builtin_amdgcn_alignbyte(d[4], d[3], r);
-  lo = (uint64_t)a0 | ((uint64_t)a1 << 32);
-  hi = (uint64_t)a2 | ((uint64_t)a3 << 32);
+  uint32_t o[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], r);
+  return B32{(uint64_t)o[0] | ((uint64_t)o[1] << 32), (uint64_t)o[2] | ((uint64_t)o[3] << 32),
+             (uint64_t)o[4] | ((uint64_t)o[5] << 32), (uint64_t)o[6] | ((uint64_t)o[7] << 32)};
+}
+
+__device__ inline uint64_t swar_lower(uint64_t v) {  // A-Z -> a-z on ASCII bytes
+  const uint64_t k3f = 0x3f3f3f3f3f3f3f3full, k25 = 0x2525252525252525ull,
+                 k80 = 0x8080808080808080ull;
+  return v | ((((v + k3f) & ~(v + k25)) & k80) >> 2);
 }
 
 // Pieces of one pre-tokenizer unit (text[start, start+len), kind as classify_window): written to
 // pc[64 * q]; returns the count, or -1 when the unit needs the lane kernel (> kPcs pieces or a
 // normalised word > kNorm bytes). cs_flag: the unit is a literal [CLS] / [SEP].
-__device__ int unit_pieces(const Tables& T, const uint32_t* bloom,
+// ASCII units (words and isolated punctuation, <= 32 bytes) go straight to registers; others are
+// normalised code point by code point into the lane's LDS buffer first (ASCII table in LDS).
+__device__ int unit_pieces(const Tables& T, const uint32_t* bloom, const uint32_t* s_ascii,
                            const uint8_t* __restrict__ text, int64_t n_bytes, int64_t start,
                            int len, int kind, bool unit_slow, Pcs& pc, uint8_t* w,
                            bool& cs_flag) {
@@ -474,42 +483,48 @@ __device__ int unit_pieces(const Tables& T, const uint32_t* bloom,
     cs_flag = kind - 2 == kCls || kind - 2 == kSep;
     return 1;
   }
-  if (kind == 0 && !unit_slow && len <= 16 && T.ascii_mode != 0) {
-    uint64_t lo, hi;
-    load16(text, n_bytes, start, lo, hi);
-    lo = keep_bytes(lo, len);
-    hi = keep_bytes(hi, len - 8);
-    if (T.ascii_mode == 1) {  // SWAR A-Z -> a-z on ASCII bytes
-      const uint64_t k3f = 0x3f3f3f3f3f3f3f3full, k25 = 0x2525252525252525ull,
-                     k80 = 0x8080808080808080ull;
-      lo |= (((lo + k3f) & ~(lo + k25)) & k80) >> 2;
-      hi |= (((hi + k3f) & ~(hi + k25)) & k80) >> 2;
-    }
-    return wordpiece_reg(T, bloom, lo, hi, len, pc);
+  if (!unit_slow && len <= 32 && T.ascii_mode != 0) {
+    B32 v = load32(text, n_bytes, start);
+    if (T.ascii_mode == 1) v = B32{swar_lower(v.w0), swar_lower(v.w1), swar_lower(v.w2), swar_lower(v.w3)};
+    return wordpiece32(T, bloom, v, len, ~0ull, pc);
   }
   // generic (rare): normalise the unit's code points into the lane's LDS buffer
-  int nb = 0, nc = 0;
+  int nb = 0;
   int64_t j = start;
   const int64_t je = start + len;
   while (j < je) {
-    const uint32_t cp = utf8_next(text, je, j);
-    const uint32_t e = tab_entry(T, cp);
+    const uint32_t b0 = text[j];
+    uint32_t cp, e;
+    if (b0 < 0x80) {
+      cp = b0;
+      e = s_ascii[b0];
+      ++j;
+    } else {
+      cp = utf8_next(text, je, j);
+      e = tab_entry(T, cp);
+    }
     if ((e >> 30) == kDrop) continue;
     uint8_t ob[12];
-    int olen, ochars = 1;
+    int olen;
     if (e & kIdent) olen = put_utf8(ob, cp);
     else if (e & kMulti) {
       const uint8_t* p = T.pool + (e & 0xFFFFFFu);
       olen = p[0];
-      ochars = p[1];
       for (int q = 0; q < olen; ++q) ob[q] = p[2 + q];
     } else olen = put_utf8(ob, e & 0x1FFFFFu);
     if (nb + olen > kNorm) return -1;
     for (int q = 0; q < olen; ++q) w[nb + q] = ob[q];
     nb += olen;
-    nc += ochars;
   }
-  return wordpiece_lds(T, w, nb, nc, pc);
+  if (nb == 0) return 0;
+  // <= 32 normalised bytes (<= 32 chars, so the 100-char rule cannot apply); pieces may end
+  // only at character boundaries
+  uint64_t ends = 1ull << nb;
+  for (int e = 1; e < nb; ++e)
+    if ((w[e] & 0xC0) != 0x80) ends |= 1ull << e;
+  const uint64_t* w8 = reinterpret_cast<const uint64_t*>(w);
+  const B32 v{w8[0], w8[1], w8[2], w8[3]};
+  return wordpiece32(T, bloom, v, nb, ends, pc);
 }
 
 __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
@@ -539,7 +554,7 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
         const int us = W.us[lane], ue = W.ue[lane], kind = W.uk[lane];
         const int ulen = ue - us + 1;
         const bool unit_slow = ((R.slow >> us) & (ulen >= 64 ? ~0ull : ((1ull << ulen) - 1))) != 0;
-        npc = unit_pieces(T, T.bloom, text, n_bytes, pos + us, ulen, kind, unit_slow, pc,
+        npc = unit_pieces(T, T.bloom, s_ascii, text, n_bytes, pos + us, ulen, kind, unit_slow, pc,
                           W.nrm + lane * kNorm, cs_flag);
       }
       if (ballot(npc < 0)) { fallback = true; break; }
@@ -577,7 +592,7 @@ struct alignas(16) BatchLds {
   int64_t r_b0[kRing];
   int32_t r_sent[kRing], r_count[kRing], r_flags[kRing], r_pending[kRing], r_state[kRing];
   int32_t pcs[kPcs * 64];  // lane l's pieces at pcs[64 q + l]
-  uint8_t nrm[64 * kNorm];  // lane l's normalised word (generic path)
+  alignas(16) uint8_t nrm[64 * kNorm];  // lane l's normalised word (generic path)
 };
 
 enum : int32_t { kClosed = 1, kFallback = 2 };
@@ -612,13 +627,19 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
 
   auto flush = [&]() {
     const int m = qn < 64 ? qn : 64;
+#ifdef LDDL_TOK_COUNT_FLUSH  // diagnostics: flushes and units per flush, in fb_n[1..2]
+    if (lane == 0) {
+      atomicAdd(fb_n + 1, 1u);
+      atomicAdd(fb_n + 2, (uint32_t)m);
+    }
+#endif
     int npc = 0;
     bool cs_flag = false;
     int slot = -1;
     Pcs pc{W.pcs + lane};
     if (lane < m) {
       slot = W.q_slot[lane];
-      npc = unit_pieces(T, s_bloom, text, n_bytes, W.r_b0[slot] + W.q_rel[lane], W.q_len[lane],
+      npc = unit_pieces(T, s_bloom, s_ascii, text, n_bytes, W.r_b0[slot] + W.q_rel[lane], W.q_len[lane],
                         W.q_kind[lane], W.q_slow[lane] != 0, pc, W.nrm + lane * kNorm, cs_flag);
       if (npc < 0) {
         atomicOr(&W.r_state[slot], kFallback);
@@ -793,8 +814,13 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
   }
   // fallback list: [0] = count, then sentence indices
   int32_t* fb;
-  LDDL_HIP(hipMallocAsync((void**)&fb, sizeof(int32_t) * (size_t)(n_sent + 1), st));
-  LDDL_HIP(hipMemsetAsync(fb, 0, sizeof(int32_t), st));
+#ifdef LDDL_TOK_COUNT_FLUSH
+  constexpr int kFbHead = 3;  // [0] fallback count, [1] flushes, [2] units flushed
+#else
+  constexpr int kFbHead = 1;
+#endif
+  LDDL_HIP(hipMallocAsync((void**)&fb, sizeof(int32_t) * (size_t)(n_sent + kFbHead), st));
+  LDDL_HIP(hipMemsetAsync(fb, 0, sizeof(int32_t) * kFbHead, st));
   int n_cu = 256;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
   // grid-stride over sentences with exactly the resident workgroups (a second wave of
@@ -805,7 +831,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     const int64_t want = (n_sent + kTW - 1) / kTW;
     const int64_t grid = std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1));
     hipLaunchKernelGGL(tokenize_wave_kernel, dim3((unsigned)grid), dim3(64 * kTW), 0, st, c->tab,
-                       d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + 1,
+                       d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + kFbHead,
                        reinterpret_cast<uint32_t*>(fb));
   } else {
     LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_batch_kernel, 64 * kBW, 0));
@@ -813,14 +839,22 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     const int64_t want = (n_sent + 16 * kBW - 1) / (16 * kBW);
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1)));
     hipLaunchKernelGGL(tokenize_batch_kernel, dim3((unsigned)grid), dim3(64 * kBW), 0, st, c->tab,
-                       d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + 1,
+                       d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + kFbHead,
                        reinterpret_cast<uint32_t*>(fb));
   }
   const int64_t fgrid = std::min<int64_t>((n_sent + kBlock - 1) / kBlock, (int64_t)n_cu * 2);
   hipLaunchKernelGGL(tokenize_lane_kernel, dim3((unsigned)fgrid), dim3(kBlock), 0, st, c->tab,
-                     d_text, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + 1,
+                     d_text, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + kFbHead,
                      reinterpret_cast<const uint32_t*>(fb));
   LDDL_HIP(hipGetLastError());
+#ifdef LDDL_TOK_COUNT_FLUSH
+  {
+    uint32_t h[3];
+    LDDL_HIP(hipMemcpyAsync(h, fb, 12, hipMemcpyDeviceToHost, st));
+    LDDL_HIP(hipStreamSynchronize(st));
+    fprintf(stderr, "[tok] flushes=%u units=%u (%.1f per flush)\n", h[1], h[2], (double)h[2] / (h[1] + 1e-9));
+  }
+#endif
   LDDL_HIP(hipFreeAsync(fb, st));
   return 0;
 }
