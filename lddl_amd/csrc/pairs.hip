@@ -295,12 +295,14 @@ struct WaveRng {
   // Decisions of create_masked_lm_predictions (pretrain.py:208-221) for cnt masked tokens:
   // random() < 0.8 -> [MASK]; else random() < 0.5 -> keep; else vocab_words[randint(0, V-1)].
   // Lane t tabulates the decision and word count of a token whose first word is mti + t; the
-  // tokens then follow as a pointer chase through that table (two readlanes per token). A table
+  // chain of decision starts p_0 = 0, p_{k+1} = p_k + len[p_k] is then resolved for every k at
+  // once by pointer doubling (ds_bpermute), so lane k learns where decision k starts. A table
   // entry that would read past the MT block is left empty and that token is drawn the scalar way.
-  template <typename Out>
-  __device__ void mask_decisions(int cnt, uint64_t lt08, int32_t V, int32_t mask_id, Out out) {
+  // cnt <= 64; returns decision `lane` in each lane < cnt.
+  __device__ int32_t mask_decisions(int cnt, uint64_t lt08, int32_t V, int32_t mask_id) {
     const int lane = threadIdx.x;
     const int kV = 32 - __clz((uint32_t)V);
+    int32_t res = 0;
     int c = 0;
     while (c < cnt) {
       if (mti >= kN) twist();
@@ -329,26 +331,43 @@ struct WaveRng {
           }
         }
       }
-      int pos = 0;
-      while (c < cnt && pos < 64) {
-        const int l = (int)rdlane((uint32_t)len, pos);
-        if (l == 0) break;
-        out(c, (int32_t)rdlane((uint32_t)tok, pos));
-        pos = uni(pos + l);
-        ++c;
+      // J_b[t] = start after 2^b decisions from t (64: stop, absorbing)
+      int Jd[6];
+      Jd[0] = len ? min(lane + len, 64) : 64;
+#pragma unroll
+      for (int b = 1; b < 6; ++b) {
+        const int y = __shfl(Jd[b - 1], Jd[b - 1] & 63, 64);
+        Jd[b] = Jd[b - 1] >= 64 ? 64 : y;
       }
+      int p = 0;  // start of decision `lane`
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        const int t = __shfl(Jd[b], p & 63, 64);
+        if ((lane >> b) & 1) p = p >= 64 ? 64 : t;
+      }
+      const int lp = __shfl(len, p & 63, 64);
+      const int32_t tp = __shfl(tok, p & 63, 64);
+      const uint64_t okm = ballot(p < 64 && lp > 0);  // a prefix of the lanes
+      int take = okm == ~0ull ? 64 : __ffsll((unsigned long long)~okm) - 1;
+      if (take > cnt - c) take = cnt - c;
+      const int32_t tk = __shfl(tp, (lane - c) & 63, 64);  // decision k goes to lane c + k
+      if (lane >= c && lane < c + take) res = tk;
+      int pos = 0;
+      if (take > 0) pos = (int)rdlane((uint32_t)p, take - 1) + (int)rdlane((uint32_t)lp, take - 1);
       mti = uni(mti + pos);
+      c += take;
       wbase = -1024;
-      if (c < cnt && pos < 64) {
+      if (c < cnt && pos < 64) {  // the next decision's words straddle the block end
         int32_t t2;
         if (rand53() < lt08) t2 = mask_id;
         else if (below_half()) t2 = kKeep;
         else t2 = (int32_t)randint(0, V - 1);
-        out(c, t2);
+        if (lane == c) res = t2;
         ++c;
         wbase = -1024;
       }
     }
+    return res;
   }
 
   // random() = N / 2^53 with N = (w1 >> 5) * 2^26 + (w2 >> 6). `random() < p` is decided exactly
@@ -565,9 +584,7 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
           // decisions of the masked candidates in shuffled order (pretrain.py:208-221)
           for (int32_t c0 = 0; c0 < num; c0 += 64) {
             const int cmax = min(64, num - c0);
-            int32_t mytok = 0;
-            rng.mask_decisions(cmax, kLt08, A.vocab_size, A.mask_id,
-                               [&](int c, int32_t tok) { mytok = lane == c ? tok : mytok; });
+            const int32_t mytok = rng.mask_decisions(cmax, kLt08, A.vocab_size, A.mask_id);
             if (fits && lane < cmax) A.mtok[mb + c0 + lane] = mytok;
           }
           STAMP_ADD(4, st_t);
