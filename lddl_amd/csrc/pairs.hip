@@ -423,19 +423,64 @@ struct PlanArgs {
 constexpr int kDocLds = 512;  // partitions with <= this many documents cache offsets in LDS
 constexpr uint64_t kLt08 = 7205759403792794ull;  // ceil(0.8 (binary64) * 2^53): random() < 0.8
 
-// Sentence lengths of one document through a 64-entry register window.
+// Sentence lengths of one document through a 64-entry register window (lane l: sentence
+// wbase + l) with their inclusive prefix sum, so a chunk end is one ballot and a span's length
+// two readlanes. Lengths are < 2^24 (lddl_tokenize caps max_pieces), so 64 of them fit int32.
 struct LenWin {
   const int32_t* len;  // ks_len + first kept sentence of the doc
   int n, wbase;
-  int32_t win;
+  int32_t win, pre;
+  uint64_t fl;  // lanes whose sentence holds a literal [CLS]/[SEP]
   __device__ void reset(const int32_t* p, int nn) { len = p; n = nn; wbase = -1024; }
+  __device__ bool has(int j) const { return j >= wbase && j < wbase + 64; }
+  __device__ void load(int j) {
+    wbase = j;
+    const int k = j + (int)threadIdx.x;
+    win = k < n ? len[k] : 0;
+    pre = wave_incl_scan(win & kLenMask);
+    fl = ballot((win & kLenHasClsSep) != 0);
+  }
   __device__ int32_t at(int j) {  // raw length word (flags included)
-    if (j < wbase || j >= wbase + 64) {
-      wbase = j;
-      const int k = j + (int)threadIdx.x;
-      win = k < n ? len[k] : 0;
-    }
+    if (!has(j)) load(j);
     return (int32_t)rdlane((uint32_t)win, j - wbase);
+  }
+  // total length of sentences [a, b) (a < b); ORs their flags into `flags`
+  __device__ int64_t sum(int a, int b, int32_t& flags) {
+    if (!has(a)) load(a);
+    if (!has(b - 1)) {  // longer than a window: sequential
+      int64_t s = 0;
+      for (int j = a; j < b; ++j) {
+        const int32_t w = at(j);
+        s += w & kLenMask;
+        flags |= w;
+      }
+      return s;
+    }
+    const int32_t hi = (int32_t)rdlane((uint32_t)pre, b - 1 - wbase);
+    const int32_t lo = a > wbase ? (int32_t)rdlane((uint32_t)pre, a - 1 - wbase) : 0;
+    const int cnt = b - a;
+    const uint64_t m = fl >> (a - wbase);
+    if ((cnt >= 64 ? m : (m & ((1ull << cnt) - 1))) != 0) flags |= kLenHasClsSep;
+    return hi - lo;
+  }
+  // the smallest i in [a, lim) with length(a .. i) >= T, else lim - 1 (a < lim <= n): the end of
+  // the reference's accumulate-until-target loops (pretrain.py:276-280, 314-317)
+  __device__ int find(int a, int lim, int64_t T) {
+    if (!has(a)) load(a);
+    for (int pass = 0; pass < 2; ++pass) {
+      const int32_t base = a > wbase ? (int32_t)rdlane((uint32_t)pre, a - 1 - wbase) : 0;
+      const int j = wbase + (int)threadIdx.x;
+      const uint64_t m = ballot(j >= a && j < lim && (int64_t)(pre - base) >= T);
+      if (m) return wbase + __ffsll((unsigned long long)m) - 1;
+      if (wbase + 64 >= lim) return lim - 1;
+      if (pass == 0 && wbase != a) load(a);  // restart the window at a and look again
+      else break;
+    }
+    int64_t s = 0;  // more than 64 sentences: sequential
+    for (int i = a;; ++i) {
+      s += at(i) & kLenMask;
+      if (i == lim - 1 || s >= T) return i;
+    }
   }
 };
 
@@ -480,23 +525,19 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
       La.reset(A.ks_len + s0, ns);
       int32_t target = max_num;
       if (rng.rand53() < A.k_short) target = (int32_t)rng.randint(2, max_num);
-      int chunk0 = 0, chunk_n = 0;
-      int64_t cur_len = 0;
-      for (int i = 0; i < ns; ++i) {
-        if (chunk_n == 0) chunk0 = i;
-        ++chunk_n;
-        cur_len += La.at(i) & kLenMask;
-        if (!(i == ns - 1 || cur_len >= target)) continue;
+      // chunks: sentences are accumulated until the target length or the document end
+      // (pretrain.py:276-280); after a random-next pair the unused sentences are put back
+      // (320-321), so the next chunk starts right after A
+      for (int chunk0 = 0; chunk0 < ns;) {
+        const int i = La.find(chunk0, ns, target);  // the chunk is [chunk0, i]
+        const int chunk_n = i - chunk0 + 1;
         const int a_end = chunk_n >= 2 ? (int)rng.randint(1, chunk_n - 1) : 1;
-        int64_t la = 0;
         int32_t flags = 0;
-        for (int j = chunk0; j < chunk0 + a_end; ++j) {
-          const int32_t w = La.at(j);
-          la += w & kLenMask;
-          flags |= w;
-        }
+        const int64_t la = La.sum(chunk0, chunk0 + a_end, flags);
         int64_t lb = 0, b_ks;
         int32_t rn = 0;
+        int next0;
+        STAMP_ADD(0, st_t);
         if (chunk_n == 1 || rng.below_half()) {
           rn = 1;
           const int64_t target_b = target - la;
@@ -511,25 +552,19 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
           const int rstart = (int)rng.randint(0, rns - 1);
           b_ks = r0 + rstart;
           Lb.reset(A.ks_len + r0, rns);
-          for (int j = rstart; j < rns; ++j) {
-            const int32_t w = Lb.at(j);
-            lb += w & kLenMask;
-            flags |= w;
-            if (lb >= target_b) break;
-          }
-          i -= chunk_n - a_end;
+          const int jb = Lb.find(rstart, rns, target_b);  // B is [rstart, jb] (314-317)
+          lb = Lb.sum(rstart, jb + 1, flags);
+          next0 = chunk0 + a_end;
         } else {
           b_ks = s0 + chunk0 + a_end;
-          for (int j = chunk0 + a_end; j < chunk0 + chunk_n; ++j) {
-            const int32_t w = La.at(j);
-            lb += w & kLenMask;
-            flags |= w;
-          }
+          lb = La.sum(chunk0 + a_end, i + 1, flags);
+          next0 = i + 1;
         }
+        STAMP_ADD(3, st_t);
         // _truncate_seq_pair
         int32_t a_front = 0, b_front = 0, na = (int32_t)la, nb = (int32_t)lb;
         rng.trunc_draws(na, nb, max_num, a_front, b_front);
-        STAMP_ADD(0, st_t);
+        STAMP_ADD(5, st_t);
         const int64_t slot = base + np;
         if (leader) A.desc[slot] = PairDesc{s0 + chunk0, b_ks, a_front, na, b_front,
                                             nb | (int32_t)((uint32_t)rn << 31)};
@@ -596,8 +631,7 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
           }
         }
         ++np;
-        chunk_n = 0;
-        cur_len = 0;
+        chunk0 = next0;
       }
     }
   }
@@ -1579,8 +1613,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     double tot[kStampRegions] = {0};
     for (int64_t q = 0; q < n_part; ++q)
       for (int r = 0; r < kStampRegions; ++r) tot[r] += (double)h[q * kStampRegions + r];
-    const char* names[kStampRegions] = {"plan", "cand", "shuffle_draws", "traceback", "decisions",
-                                        "sort_write", "final_shuffle_draws", "-"};
+    const char* names[kStampRegions] = {"plan", "cand", "shuffle_draws", "random_next", "decisions",
+                                        "trunc", "final_shuffle_draws", "-"};
     double all = 0;
     for (double t : tot) all += t;
     fprintf(stderr, "[stamps] plan_replay_kernel mean cycles per partition:");

@@ -800,7 +800,8 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
                              const int64_t* d_sent_off, int64_t n_sent, int32_t max_pieces,
                              int32_t* d_ids, int32_t* d_sent_len) {
   if (!c) LDDL_FAIL(-1, "null ctx");
-  if (n_sent < 0 || n_bytes < 0 || max_pieces <= 0) LDDL_FAIL(-1, "bad sizes");
+  if (n_sent < 0 || n_bytes < 0 || max_pieces <= 0 || max_pieces > (1 << 24))
+    LDDL_FAIL(-1, "bad sizes (max_pieces must be in 1 .. 2^24)");
   if (n_sent >= (int64_t)INT32_MAX) LDDL_FAIL(-1, "too many sentences in one call (%lld)", (long long)n_sent);
   if (n_sent == 0) return 0;
   hipStream_t st = as_stream(stream);
