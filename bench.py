@@ -292,6 +292,11 @@ def main():
     if alt is not None:
         res['alt_rng'] = alt
     res['torch_alloc_retries'] = int(mem.get('num_alloc_retries', 0))
+    free_b, total_b = torch.cuda.mem_get_info()
+    res['memory_gb'] = {'torch_max_reserved': round(torch.cuda.max_memory_reserved() / 1e9, 1),
+                        'torch_max_allocated': round(torch.cuda.max_memory_allocated() / 1e9, 1),
+                        'device_free_at_end': round(free_b / 1e9, 1),
+                        'device_total': round(total_b / 1e9, 1)}
     if world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(corp, part, seeds, args)
     print(json.dumps(res), flush=True)

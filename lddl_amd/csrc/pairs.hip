@@ -958,31 +958,43 @@ __global__ void __launch_bounds__(256) sum_tokens_kernel(const int32_t* __restri
 }
 
 // Perform the final per-partition Fisher-Yates swaps (draws from plan_replay_kernel). One
-// workgroup per partition; the permutation lives in LDS when it fits, else in global memory.
-constexpr int kShufLds = 32768;
+// workgroup per partition: the permutation lives in LDS (Idx = uint16_t when every partition has
+// <= 65536 pairs, else int32_t; cap = the largest partition) and the draws are staged through LDS
+// in coalesced blocks, top down, so the one swapping lane only ever waits on LDS. Partitions
+// beyond `cap` (never, as launched) would use global memory.
+constexpr int kShufStage = 2048;
 
+template <typename Idx>
 __global__ void __launch_bounds__(64) apply_shuffle_kernel(const int64_t* kd_off, const int64_t* kp_off,
                                                           int32_t dup, const int64_t* part_npairs,
-                                                          const int32_t* jseq, int32_t* order) {
-  extern __shared__ __attribute__((aligned(16))) int32_t s_ord[];
+                                                          const int32_t* jseq, int32_t* order,
+                                                          int64_t cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sh_smem[];
+  Idx* s_ord = reinterpret_cast<Idx*>(sh_smem);
+  Idx* s_js = s_ord + cap;
   const int p = blockIdx.x;
   const int64_t base = (int64_t)dup * kd_off[kp_off[p]];
   const int64_t np = part_npairs[p];
   const int32_t* js = jseq + base;
   int32_t* ord = order + base;
-  if (np <= kShufLds) {
-    for (int64_t k = threadIdx.x; k < np; k += 64) s_ord[k] = (int32_t)k;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int64_t i = np - 1; i > 0; --i) {
-        const int32_t j = js[i];
-        const int32_t t = s_ord[i];
-        s_ord[i] = s_ord[j];
-        s_ord[j] = t;
+  if (np <= cap) {
+    for (int64_t k = threadIdx.x; k < np; k += 64) s_ord[k] = (Idx)k;
+    for (int64_t hi = np - 1; hi > 0; hi -= kShufStage) {
+      const int64_t lo = hi - kShufStage + 1 > 1 ? hi - kShufStage + 1 : 1;
+      __syncthreads();
+      for (int64_t k = lo + threadIdx.x; k <= hi; k += 64) s_js[k - lo] = (Idx)js[k];
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        for (int64_t i = hi; i >= lo; --i) {
+          const int32_t j = (int32_t)s_js[i - lo];
+          const Idx t = s_ord[i];
+          s_ord[i] = s_ord[j];
+          s_ord[j] = t;
+        }
       }
     }
     __syncthreads();
-    for (int64_t k = threadIdx.x; k < np; k += 64) ord[k] = s_ord[k];
+    for (int64_t k = threadIdx.x; k < np; k += 64) ord[k] = (int32_t)s_ord[k];
   } else if (threadIdx.x == 0) {
     for (int64_t k = 0; k < np; ++k) ord[k] = (int32_t)k;
     for (int64_t i = np - 1; i > 0; --i) {
@@ -1286,7 +1298,8 @@ struct lddl_pairs {
   int device = 0;
   int32_t masking = 0, max_pred = 0, seq = 0, cls_id = -1, sep_id = -1;
   int64_t n_part = 0, n_pairs = 0, n_tokens = 0, n_masked = 0, n_kept_sent = 0, n_kept_doc = 0;
-  std::vector<void*> allocs;
+  DevArena* arena = nullptr;  // the context's block cache (the context outlives its plans)
+  std::vector<DevArena::Block> allocs;
   // views
   int64_t *ks_start = nullptr, *kd_off = nullptr, *kp_off = nullptr, *kscan = nullptr;
   int32_t* ks_len = nullptr;
@@ -1301,12 +1314,22 @@ struct lddl_pairs {
 
   template <typename T>
   int alloc(T** p, int64_t n, hipStream_t st) {
-    LDDL_HIP(hipMallocAsync((void**)p, sizeof(T) * (size_t)(n > 0 ? n : 1), st));
-    allocs.push_back(*p);
+    DevArena::Block b;
+    LDDL_HIP(arena->take(sizeof(T) * (size_t)(n > 0 ? n : 1), st, b));
+    *p = static_cast<T*>(b.p);
+    allocs.push_back(b);
     return 0;
   }
+  void free_one(void* p, hipStream_t st) {  // return one block early (re-plan)
+    for (size_t i = 0; i < allocs.size(); ++i)
+      if (allocs[i].p == p) {
+        arena->give(allocs[i], st);
+        allocs.erase(allocs.begin() + (ptrdiff_t)i);
+        return;
+      }
+  }
   void release(hipStream_t st) {
-    for (void* p : allocs) (void)hipFreeAsync(p, st);
+    for (DevArena::Block& b : allocs) arena->give(b, st);
     allocs.clear();
     for (hipEvent_t& e : ev)
       if (e) {
@@ -1439,6 +1462,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   hipStream_t st = as_stream(stream);
   auto* P = new lddl_pairs();
   P->device = c->device;
+  P->arena = &c->arena;
   P->n_part = n_part;
   P->masking = prm->masking;
   P->seq = prm->seq;
@@ -1569,8 +1593,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     int32_t* mtok = nullptr;
     if (prm->masking) {
       LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 24, st));
-      LDDL_HIP(hipMallocAsync((void**)&mtok, 4 * (size_t)cap + 16, st));
-      LDDL_HIP(hipMallocAsync((void**)&jpool, 2 * (size_t)jcap + 16, st));
+      TRY(P->alloc(&mtok, cap + 4, st));
+      TRY(P->alloc(&jpool, jcap + 8, st));
     }
     A.mtok = mtok;
     A.jpool = jpool;
@@ -1588,22 +1612,36 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     LDDL_HIP(hipStreamSynchronize(st));
     if (!ctl[1]) {
       P->mtok = mtok;
-      P->allocs.push_back(mtok);
-      P->allocs.push_back(jpool);
       TRY(P->alloc(&P->mpos, (int64_t)ctl[0], st));
       break;
     }
-    (void)hipFreeAsync(mtok, st);
-    (void)hipFreeAsync(jpool, st);
+    P->free_one(mtok, st);
+    P->free_one(jpool, st);
     jpool = nullptr;
     if (attempt > 0) TRY((set_error("mask pool overflow after resize"), -1));
     cap = (int64_t)ctl[0] + 1024;
     jcap = (int64_t)ctl[2] + 1024;
   }
-  if (n_part)
-    hipLaunchKernelGGL(apply_shuffle_kernel, dim3((unsigned)n_part), dim3(64),
-                       sizeof(int32_t) * kShufLds, st, P->kd_off, P->kp_off, prm->dup,
-                       part_npairs, jseq, P->order);
+  if (n_part) {
+    std::vector<int64_t> h_np(n_part);
+    LDDL_HIP(hipMemcpyAsync(h_np.data(), part_npairs, 8 * n_part, hipMemcpyDeviceToHost, st));
+    LDDL_HIP(hipStreamSynchronize(st));
+    int64_t cap = 1;
+    for (int64_t v : h_np) cap = std::max(cap, v);
+    const size_t kLdsBudget = 150 * 1024;
+    if (cap <= 65536 && 2 * (size_t)(cap + kShufStage) <= kLdsBudget)
+      hipLaunchKernelGGL(apply_shuffle_kernel<uint16_t>, dim3((unsigned)n_part), dim3(64),
+                         2 * (size_t)(cap + kShufStage), st, P->kd_off, P->kp_off, prm->dup,
+                         part_npairs, jseq, P->order, cap);
+    else if (4 * (size_t)(cap + kShufStage) <= kLdsBudget)
+      hipLaunchKernelGGL(apply_shuffle_kernel<int32_t>, dim3((unsigned)n_part), dim3(64),
+                         4 * (size_t)(cap + kShufStage), st, P->kd_off, P->kp_off, prm->dup,
+                         part_npairs, jseq, P->order, cap);
+    else  // partitions too large for LDS: swaps in global memory
+      hipLaunchKernelGGL(apply_shuffle_kernel<int32_t>, dim3((unsigned)n_part), dim3(64),
+                         4 * (size_t)kShufStage, st, P->kd_off, P->kp_off, prm->dup, part_npairs,
+                         jseq, P->order, (int64_t)0);
+  }
   LDDL_HIP(hipGetLastError());
 #ifdef LDDL_STAMPS
   {

@@ -814,13 +814,14 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     return 0;
   }
   // fallback list: [0] = count, then sentence indices
-  int32_t* fb;
 #ifdef LDDL_TOK_COUNT_FLUSH
   constexpr int kFbHead = 3;  // [0] fallback count, [1] flushes, [2] units flushed
 #else
   constexpr int kFbHead = 1;
 #endif
-  LDDL_HIP(hipMallocAsync((void**)&fb, sizeof(int32_t) * (size_t)(n_sent + kFbHead), st));
+  DevArena::Block fbb;
+  LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)(n_sent + kFbHead), st, fbb));
+  int32_t* fb = static_cast<int32_t*>(fbb.p);
   LDDL_HIP(hipMemsetAsync(fb, 0, sizeof(int32_t) * kFbHead, st));
   int n_cu = 256;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -856,6 +857,6 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     fprintf(stderr, "[tok] flushes=%u units=%u (%.1f per flush)\n", h[1], h[2], (double)h[2] / (h[1] + 1e-9));
   }
 #endif
-  LDDL_HIP(hipFreeAsync(fb, st));
+  c->arena.give(fbb, st);
   return 0;
 }
