@@ -146,7 +146,7 @@ def main():
             n_tok = int(pb.tokens.numel()) + 3 * pb.n_pairs
         if ev is not None:
             ev[2].record()
-        st = {'pairs': pb.n_pairs, 'masked': pb.n_masked, 'plan_ms': pb.plan_ms,
+        st = {'pairs': pb.n_pairs, 'masked': pb.n_masked, 'plan_ms': pb.plan_ms, 'tokens': n_tok,
               'kept_sent': pb.n_kept_sentences, 'kept_doc': pb.n_kept_documents}
         del pb  # nothing of a step outlives it (HBM is reused by the next step)
         return n_tok, st, sent_len
@@ -209,11 +209,13 @@ def main():
     # (the replay planner at C2/C4, the tokenizer under the native RNG). Planner algorithmic
     # bytes per launch: sentence lengths read per duplicate pass
     # (4 B x dup x kept sentences) + document offsets (8 B x dup x kept documents) + per pair a
-    # 32-B descriptor, 4-B shuffle draw, 4-B mask count and 8-B mask offset + 6 B per masked
-    # position (2-B position + 4-B token) — all writes to HBM, the MT19937 state stays in LDS.
+    # 32-B descriptor, 4-B partition-shuffle draw, 4-B mask count, 4-B candidate count and two
+    # 8-B pool offsets (60 B) + the recorded cand_indexes shuffle draws (2 B per candidate, i.e.
+    # per A/B token) + 4 B per masked decision — all writes to HBM, the MT19937 state stays in LDS.
     n_bytes, n_sent = corp.text.size, corp.n_sent
-    plan_bytes = (4 * 5 * st['kept_sent'] + 8 * 5 * st['kept_doc'] + 48 * n_pairs +
-                  6 * st['masked'])
+    pair_tokens = st['tokens'] - 3 * n_pairs  # sum of len(A) + len(B) of this rank's step
+    plan_bytes = (4 * 5 * st['kept_sent'] + 8 * 5 * st['kept_doc'] + 60 * n_pairs +
+                  2 * pair_tokens + 4 * st['masked'])
     plan_gbs = plan_bytes / (plan_ms * 1e-3) / 1e9 if plan_ms > 0 else 0.0
     # tokenizer: text bytes read + sentence offsets read (8 B each) + ids written (4 B / piece)
     # + sent_len (4 B / sentence)
