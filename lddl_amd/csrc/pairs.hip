@@ -129,6 +129,9 @@ struct WaveRng {
   int mti;       // next word of the block (uniform)
   int wbase;     // window base (uniform)
   uint32_t win;  // this lane's tempered word temper(mt[wbase + lane])
+#ifdef LDDL_STAMPS
+  uint64_t n_pass = 0, n_win = 0;  // diagnostics: Jacobi passes / Fisher-Yates windows
+#endif
 
   __device__ static uint32_t twist1(uint32_t a, uint32_t b, uint32_t c) {
     const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
@@ -237,10 +240,16 @@ struct WaveRng {
         // lane masks straight from the compares (no boolean round trip through a VGPR)
         const uint64_t bm = Lm & __builtin_amdgcn_sicmp(i, 0, 38 /* sgt */) &
                             __builtin_amdgcn_uicmp(x, (uint32_t)i, 34 /* ugt */);
+#ifdef LDDL_STAMPS
+        ++n_pass;
+#endif
         if (bm == rej) break;
         rej = bm;
         R = (int32_t)popc_below(rej);
       }
+#ifdef LDDL_STAMPS
+      ++n_win;
+#endif
       // words consumed: up to the first lane past the last step (i < 1) or the window end
       const uint64_t fin = Lm & __builtin_amdgcn_sicmp(i, 1, 40 /* slt */);
       const int E = fin ? __ffsll((unsigned long long)fin) - 1 : L;
@@ -501,7 +510,11 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
   uint64_t st_acc[kStampRegions] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   [[maybe_unused]] uint64_t st_t = STAMP_T();
-  WaveRng rng{s_mt, s_tw, 0, 0, 0u};
+  WaveRng rng{s_mt, s_tw, 0, 0, 0u
+#ifdef LDDL_STAMPS
+              , 0, 0
+#endif
+  };
   rng.seed_i64(A.part_seed[p]);
   const int64_t d0 = A.kp_off[p], nd = A.kp_off[p + 1] - d0;
   const int64_t kbase = A.kd_off[d0];
@@ -644,6 +657,7 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
   }
   STAMP_ADD(6, st_t);
 #ifdef LDDL_STAMPS
+  st_acc[7] = rng.n_pass * 1000000 / (rng.n_win ? rng.n_win : 1);  // passes per window x 1e6
   if (leader && A.stamps)
     for (int r = 0; r < kStampRegions; ++r) A.stamps[(int64_t)p * kStampRegions + r] = st_acc[r];
 #endif
@@ -1652,13 +1666,13 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     for (int64_t q = 0; q < n_part; ++q)
       for (int r = 0; r < kStampRegions; ++r) tot[r] += (double)h[q * kStampRegions + r];
     const char* names[kStampRegions] = {"plan", "cand", "shuffle_draws", "random_next", "decisions",
-                                        "trunc", "final_shuffle_draws", "-"};
+                                        "trunc", "final_shuffle_draws", "fy_jacobi_passes_per_window"};
     double all = 0;
-    for (double t : tot) all += t;
+    for (int r = 0; r < kStampRegions - 1; ++r) all += tot[r];
     fprintf(stderr, "[stamps] plan_replay_kernel mean cycles per partition:");
-    for (int r = 0; r < kStampRegions; ++r)
+    for (int r = 0; r < kStampRegions - 1; ++r)
       fprintf(stderr, " %s=%.3g (%.1f%%)", names[r], tot[r] / n_part, 100.0 * tot[r] / (all + 1e-9));
-    fprintf(stderr, "\n");
+    fprintf(stderr, " %s=%.3f\n", names[kStampRegions - 1], tot[kStampRegions - 1] / n_part / 1e6);
   }
 #endif
   // layout
