@@ -1031,22 +1031,50 @@ __global__ void map_pairs_kernel(const int64_t* kd_off, const int64_t* kp_off, i
   for (int64_t k = threadIdx.x; k < n; k += blockDim.x) src[q0 + k] = base + order[base + k];
 }
 
-struct PairTokens {
-  const int64_t* src;
-  const PairDesc* desc;
-  __device__ int64_t operator()(int64_t q) const {
-    const PairDesc d = desc[src[q]];
-    return (int64_t)d.na + (d.nb_rn & 0x7FFFFFFF);
-  }
-};
 struct Identity {
   const int64_t* v;
   __device__ int64_t operator()(int64_t i) const { return v[i]; }
 };
+
+// Per output pair, everything the gather needs, in output order: the A and B windows in the dense
+// token array, the lengths and is_random_next, and the masks' place in the mask pool. Built one
+// lane per pair (src -> descriptor -> sentence offsets: every load of a wave in flight at once),
+// so the scans and the gather read it front to back instead of chasing src[q] themselves.
+struct alignas(16) GatherRec {
+  int64_t aoff, boff, moff;
+  int32_t na, nb_rn, nm, pad;
+};
+
+__global__ void __launch_bounds__(256) pair_prep_kernel(const int64_t* __restrict__ src, int64_t n,
+                                                        const PairDesc* __restrict__ desc,
+                                                        const int64_t* __restrict__ kscan,
+                                                        const int32_t* __restrict__ nmask,
+                                                        const int64_t* __restrict__ moff,
+                                                        GatherRec* __restrict__ rec) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= n) return;
+  const int64_t slot = src[q];
+  const PairDesc d = desc[slot];
+  GatherRec r;
+  r.aoff = kscan[d.a_ks] + d.a_front;
+  r.boff = kscan[d.b_ks] + d.b_front;
+  r.moff = nmask ? moff[slot] : 0;
+  r.na = d.na;
+  r.nb_rn = d.nb_rn;
+  r.nm = nmask ? nmask[slot] : 0;
+  r.pad = 0;
+  rec[q] = r;
+}
+
+struct PairTokens {
+  const GatherRec* r;
+  __device__ int64_t operator()(int64_t q) const {
+    return (int64_t)r[q].na + (r[q].nb_rn & 0x7FFFFFFF);
+  }
+};
 struct PairMasks {
-  const int64_t* src;
-  const int32_t* nmask;
-  __device__ int64_t operator()(int64_t q) const { return nmask[src[q]]; }
+  const GatherRec* r;
+  __device__ int64_t operator()(int64_t q) const { return r[q].nm; }
 };
 
 // Kept tokens packed densely in kept-sentence order: kept sentence k's pieces are
@@ -1091,13 +1119,9 @@ struct KeptLen {
 };
 
 struct GatherArgs {
-  const int64_t* kscan;  // dense offset of each kept sentence
   const int32_t* dense;  // kept tokens, packed
-  const int64_t* src;
-  const PairDesc* desc;
-  const int32_t* nmask;
-  const int64_t* moff;
-  // masks: positions + replacements at moff (any order; ranks are taken from the map)
+  const GatherRec* rec;  // per output pair (pair_prep_kernel)
+  // masks: positions + replacements at rec.moff (any order; ranks are taken from the map)
   const uint16_t* mpos;
   const int32_t* mtok;
   int32_t max_pred, masking, seq;
@@ -1216,25 +1240,22 @@ __global__ void __launch_bounds__(64 * kGWaves) gather_kernel(GatherArgs G, Gath
   const int map_len = Lg.map_len;
   const int64_t qb = ((int64_t)blockIdx.x * kGWaves + w) * K;
 
-  int64_t slot[K], tof[K], aoff[K], boff[K], po[K];
+  int64_t mbase[K], tof[K], aoff[K], boff[K], po[K];
   int32_t na[K], nb[K], rn[K], nm[K], rk[K];
   bool act[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     act[k] = qb + k < G.n_pairs;
-    slot[k] = act[k] ? G.src[qb + k] : 0;
-  }
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    PairDesc d{0, 0, 0, 0, 0, 0};
-    if (act[k]) d = G.desc[slot[k]];
-    na[k] = d.na;
-    nb[k] = d.nb_rn & 0x7FFFFFFF;
-    rn[k] = (int32_t)((uint32_t)d.nb_rn >> 31);
-    aoff[k] = act[k] ? G.kscan[d.a_ks] + d.a_front : 0;
-    boff[k] = act[k] ? G.kscan[d.b_ks] + d.b_front : 0;
+    GatherRec r{0, 0, 0, 0, 0, 0, 0};
+    if (act[k]) r = G.rec[qb + k];
+    na[k] = r.na;
+    nb[k] = r.nb_rn & 0x7FFFFFFF;
+    rn[k] = (int32_t)((uint32_t)r.nb_rn >> 31);
+    aoff[k] = r.aoff;
+    boff[k] = r.boff;
+    mbase[k] = r.moff;
     tof[k] = act[k] ? G.tok_off[qb + k] : 0;
-    nm[k] = (G.masking && act[k]) ? G.nmask[slot[k]] : 0;
+    nm[k] = G.masking ? r.nm : 0;
     po[k] = (G.masking && act[k]) ? G.pos_off[qb + k] : 0;
     rk[k] = 0;
   }
@@ -1257,7 +1278,7 @@ __global__ void __launch_bounds__(64 * kGWaves) gather_kernel(GatherArgs G, Gath
         if (!nm[k]) continue;
         uint16_t* map = maps + k * map_len;
         int32_t* tk = toks + k * G.max_pred;
-        const int64_t mb = G.moff[slot[k]];
+        const int64_t mb = mbase[k];
         for (int j = lane; j < nm[k]; j += 64) {
           map[G.mpos[mb + j]] = (uint16_t)(j + 1);
           tk[j] = G.mtok[mb + j];
@@ -1323,6 +1344,7 @@ struct lddl_pairs {
   uint16_t* mpos = nullptr;
   int64_t* moff = nullptr;
   int64_t *src = nullptr, *tok_off = nullptr, *pos_off = nullptr;
+  GatherRec* rec = nullptr;  // per output pair (pair_prep_kernel)
   int64_t* part_base = nullptr;  // [n_part + 1] first output pair of each partition
   hipEvent_t ev[2] = {nullptr, nullptr};  // around the last plan_replay_kernel launch
 
@@ -1695,14 +1717,20 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   }  // replay
   const int64_t npairs = P->n_pairs;
   TRY(P->alloc(&P->tok_off, npairs + 1, st));
+  TRY(P->alloc(&P->rec, npairs, st));
+  if (npairs)
+    hipLaunchKernelGGL(pair_prep_kernel, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, st,
+                       P->src, npairs, P->desc, P->kscan, prm->masking ? P->nmask : nullptr,
+                       P->moff, P->rec);
+  LDDL_HIP(hipGetLastError());
   int64_t* scr2;
   TRY(P->alloc(&scr2, scan_scratch_elems(npairs), st));
-  if (scan_exclusive(PairTokens{P->src, P->desc}, npairs, P->tok_off, scr2, st) != hipSuccess)
+  if (scan_exclusive(PairTokens{P->rec}, npairs, P->tok_off, scr2, st) != hipSuccess)
     TRY(-100);
   LDDL_HIP(hipMemcpyAsync(&P->n_tokens, P->tok_off + npairs, 8, hipMemcpyDeviceToHost, st));
   if (prm->masking) {
     TRY(P->alloc(&P->pos_off, npairs + 1, st));
-    if (scan_exclusive(PairMasks{P->src, P->nmask}, npairs, P->pos_off, scr2, st) != hipSuccess)
+    if (scan_exclusive(PairMasks{P->rec}, npairs, P->pos_off, scr2, st) != hipSuccess)
       TRY(-100);
     LDDL_HIP(hipMemcpyAsync(&P->n_masked, P->pos_off + npairs, 8, hipMemcpyDeviceToHost, st));
   }
@@ -1725,12 +1753,8 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
   hipStream_t st = as_stream(stream);
   if (P->n_pairs == 0) return 0;
   GatherArgs G{};
-  G.kscan = P->kscan;
   G.dense = P->dense;
-  G.src = P->src;
-  G.desc = P->desc;
-  G.nmask = P->nmask;
-  G.moff = P->moff;
+  G.rec = P->rec;
   G.mpos = P->mpos;
   G.mtok = P->mtok;
   G.max_pred = P->max_pred;
