@@ -1169,10 +1169,41 @@ struct ResolveArgs {
   int32_t cls_id, sep_id;
 };
 
+// A lane's column of LDS entries; 16-bit: x[k * 64 + lane]; 8-bit (seq <= 256): dword k/4 of
+// lane l at (k/4) * 64 + l, so every access of the wave hits 64 distinct banks either way.
+template <typename T>
+struct LaneCol;
+template <>
+struct LaneCol<uint16_t> {
+  uint16_t* base;
+  int lane;
+  __device__ uint32_t get(int k) const { return base[k * 64 + lane]; }
+  __device__ void set(int k, uint32_t v) { base[k * 64 + lane] = (uint16_t)v; }
+  __device__ void iota(int n) {
+    for (int k = 0; k < n; ++k) set(k, (uint32_t)k);
+  }
+};
+template <>
+struct LaneCol<uint8_t> {
+  uint8_t* base;
+  int lane;
+  __device__ int at(int k) const { return ((k >> 2) << 8) | (lane << 2) | (k & 3); }
+  __device__ uint32_t get(int k) const { return base[at(k)]; }
+  __device__ void set(int k, uint32_t v) { base[at(k)] = (uint8_t)v; }
+  __device__ void iota(int n) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(base);
+    for (int k = 0; k < n; k += 4)
+      w[(k >> 2) * 64 + lane] = (uint32_t)k | (uint32_t)(k + 1) << 8 | (uint32_t)(k + 2) << 16 |
+                                (uint32_t)(k + 3) << 24;
+  }
+};
+
+// NG > 0: all of a pair's draws (nc <= 8 NG) are loaded up front, NG uint4 in flight per lane
+template <typename T, int NG>
 __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
-  extern __shared__ uint16_t s_x[];
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_xb[];
   const int lane = threadIdx.x;
-  uint16_t* x = s_x + lane;
+  LaneCol<T> x{reinterpret_cast<T*>(s_xb), lane};
   const int64_t q = (int64_t)blockIdx.x * 64 + lane;
   if (q >= R.n_pairs) return;
   const int64_t slot = R.src[q];
@@ -1183,26 +1214,24 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   const PairDesc d = R.desc[slot];
   const int32_t na = d.na, nb = d.nb_rn & 0x7FFFFFFF;
   const bool fast = nc == na + nb;
-  for (int k = 0; k < nc; ++k) x[k * 64] = (uint16_t)k;
+  x.iota(nc);
   const uint4* jp = reinterpret_cast<const uint4*>(R.jpool + jb);
   uint4* mp = reinterpret_cast<uint4*>(R.mpos + mb);
   uint4 acc = make_uint4(0u, 0u, 0u, 0u);  // slots [8h, 8h+8) collected from the top down
-  uint4 nxt = jp[(nc - 1) >> 3];
-  for (int h = (nc - 1) >> 3; h >= 0; --h) {
-    const uint4 jv = nxt;
-    if (h > 0) nxt = jp[h - 1];  // next group of draws in flight
+  // step i of group h: swap, or (i < num) finalise slot i
+  auto group = [&](int h, const uint4& jv) {
     const uint32_t jw[4] = {jv.x, jv.y, jv.z, jv.w};
 #pragma unroll
     for (int u = 7; u >= 0; --u) {
       const int i = 8 * h + u;
       if (i >= nc) continue;
       const int j = (int)((jw[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
-      const int xi = x[i * 64];
+      const uint32_t xi = x.get(i);
       if (i >= num) {
-        if (i >= 1) x[j * 64] = (uint16_t)xi;
+        if (i >= 1) x.set(j, xi);
       } else {
-        const int y = i >= 1 ? (int)x[j * 64] : xi;  // slot 0 keeps x[0]
-        if (i >= 1) x[j * 64] = (uint16_t)xi;
+        const int y = i >= 1 ? (int)x.get(j) : (int)xi;  // slot 0 keeps x[0]
+        if (i >= 1) x.set(j, xi);
         const uint32_t pos = (uint32_t)(fast ? (y < na ? y + 1 : y + 2) : y);
         // 128-bit shift register, newest at slot offset 0 (slots arrive in descending order)
         acc = make_uint4((acc.x << 16) | pos, (acc.y << 16) | (acc.x >> 16),
@@ -1210,16 +1239,32 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
       }
     }
     if (8 * h < num) mp[h] = acc;  // slots [8h, 8h+8) complete (the top group zero-padded)
+  };
+  if (NG > 0) {
+    uint4 jv[NG > 0 ? NG : 1];
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+      if (8 * g < nc) jv[g] = jp[g];
+#pragma unroll
+    for (int h = NG - 1; h >= 0; --h)
+      if (8 * h < nc) group(h, jv[h]);
+  } else {
+    uint4 nxt = jp[(nc - 1) >> 3];
+    for (int h = (nc - 1) >> 3; h >= 0; --h) {
+      const uint4 jv = nxt;
+      if (h > 0) nxt = jp[h - 1];  // next group of draws in flight
+      group(h, jv);
+    }
   }
   if (!fast) {  // literal [CLS]/[SEP] in the pair: candidate index -> position via the tokens
     const int64_t ao = R.kscan[d.a_ks] + d.a_front, bo = R.kscan[d.b_ks] + d.b_front;
     int k = 0;
     for (int t = 0; t < na + nb; ++t) {
       const int32_t tok = t < na ? R.dense[ao + t] : R.dense[bo + (t - na)];
-      if (tok != R.cls_id && tok != R.sep_id) x[(k++) * 64] = (uint16_t)(t < na ? t + 1 : t + 2);
+      if (tok != R.cls_id && tok != R.sep_id) x.set(k++, (uint32_t)(t < na ? t + 1 : t + 2));
     }
     uint16_t* m16 = R.mpos + mb;
-    for (int c = 0; c < num; ++c) m16[c] = x[m16[c] * 64];
+    for (int c = 0; c < num; ++c) m16[c] = (uint16_t)x.get(m16[c]);
   }
 }
 
@@ -1710,8 +1755,16 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   if (prm->masking && P->n_pairs) {
     ResolveArgs RA{P->src, P->n_pairs, P->desc, P->nmask, ncand, P->moff, joff, jpool,
                    P->mpos, P->kscan, P->dense, cls, sep};
-    hipLaunchKernelGGL(fy_resolve_kernel, dim3((unsigned)((P->n_pairs + 63) / 64)), dim3(64),
-                       (size_t)2 * 64 * (size_t)std::max(prm->seq, 1), st, RA);
+    const dim3 grid((unsigned)((P->n_pairs + 63) / 64));
+    if (prm->seq <= 131)  // nc <= 128: all draws in registers
+      hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, 16>), grid, dim3(64),
+                         (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
+    else if (prm->seq <= 256)  // candidate indices and positions fit a byte
+      hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, 0>), grid, dim3(64),
+                         (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
+    else
+      hipLaunchKernelGGL((fy_resolve_kernel<uint16_t, 0>), grid, dim3(64),
+                         (size_t)2 * 64 * (size_t)prm->seq, st, RA);
     LDDL_HIP(hipGetLastError());
   }
   }  // replay
