@@ -65,16 +65,15 @@ struct Tables {
 // pass), mixed with its length and continuation flag; two bits in one 32-bit word.
 constexpr int kBloomWords = 8192;  // 32 KB
 constexpr uint32_t kBloomP = 0x01000193u;
+// One multiply: the word index comes from the top 13 bits of the product and the two bit
+// positions from its middle bits (the prefix hash h is already well mixed; in the longest-match
+// scan this runs once per candidate length, so it is kept short).
 __host__ __device__ inline uint32_t bloom_mix(uint32_t h, uint32_t len, uint32_t cont) {
-  uint32_t x = h + len * 0x9E3779B9u + cont * 0x7F4A7C15u;
-  x ^= x >> 16;
-  x *= 0x85EBCA6Bu;
-  x ^= x >> 13;
-  return x;
+  return (h ^ (len << 24) ^ (cont << 31)) * 0x85EBCA6Bu;
 }
 __host__ __device__ inline uint32_t bloom_word(uint32_t x) { return x >> 19; }
 __host__ __device__ inline uint32_t bloom_bits(uint32_t x) {
-  return (1u << (x & 31u)) | (1u << ((x >> 5) & 31u));
+  return (1u << ((x >> 9) & 31u)) | (1u << ((x >> 14) & 31u));
 }
 
 // sent_len flag: the kept pieces contain a literal [CLS] or [SEP] (matters for static masking
