@@ -86,6 +86,73 @@ def cpu_baseline(corp, part, seeds, args):
                           n_part, b1 / 1e6, dt)}
 
 
+def timed_segmented(args, rank, world, ctx, dev):
+    """The step from raw document text (what the reference hands to sent_tokenize,
+    pretrain.py:86): GPU Punkt segmentation (untrained parameters, as offline nltk runs) ->
+    WordPiece -> pairs + static masking, same synthetic documents (sentences joined by spaces)."""
+    from lddl_amd import punkt, synth
+    from lddl_amd.pairs import make_pairs
+    text, doc_off = synth.generate_doc_text(seed=args.seed, n_bytes=args.batch_bytes,
+                                            doc_begin=rank * 50_000_000, nonascii_frac=0.01,
+                                            threads=args.gen_threads)
+    cuts = np.searchsorted(doc_off, np.arange(0, doc_off[-1], args.partition_bytes), 'left')
+    part = np.unique(np.concatenate([[0], cuts, [len(doc_off) - 1]])).astype(np.int64)
+    seeds = (np.arange(len(part) - 1, dtype=np.int64) + rank * 10_000_000) * 7919 + args.seed
+    d_text = torch.from_numpy(text).to(dev)
+    d_doc = torch.from_numpy(doc_off).to(dev)
+    d_part = torch.from_numpy(part).to(dev)
+    d_seed = torch.from_numpy(seeds).to(dev)
+    punkt.set_params(ctx, None)
+    info = {}
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        so, ds = punkt.segment(ctx, d_text, d_doc)
+        if ev is not None:
+            ev[1].record()
+        ids, sl = ctx.tokenize(d_text, so)
+        pb = make_pairs(ctx, so, ids, sl, ds, d_part, d_seed, seq=args.seq, dup=5, masking=True,
+                        short_seq_prob=0.1, masked_lm_ratio=0.15, rng=args.rng)
+        del ids, sl
+        if args.workload == 'c4':
+            from lddl_amd.balance import balance
+            bb = balance(ctx, pb, 8, args.seq // 8)
+            n = int(bb.tokens.numel()) + 3 * bb.n_rows
+            del bb
+        else:
+            n = int(pb.tokens.numel()) + 3 * pb.n_pairs
+        info['sentences'] = int(so.numel()) - 1
+        del pb, so, ds
+        return n
+    for _ in range(args.warmup):
+        step()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n_tok = 0
+    for k in range(args.steps):
+        n_tok += step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt, float(n_tok)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        dt, n_tok = float(t[0].item()), int(t[1].item())
+    seg_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    return {'value': n_tok / dt, 'unit': 'output tokens/s', 'ms_per_step': dt / args.steps * 1e3,
+            'segment_ms': seg_ms, 'segment_text_gbs': len(text) / (seg_ms * 1e-3) / 1e9,
+            'documents': int(len(doc_off) - 1), 'sentences': info['sentences'],
+            'batch_bytes': int(len(text)),
+            'note': 'input = raw document text; segment_ms includes the host sync for the '
+                    'sentence count (lddl_segment_count)'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -101,6 +168,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-alt-rng', dest='alt_rng', action='store_false',
                     help='skip timing the other RNG mode (reported as alt_rng)')
+    ap.add_argument('--no-segmented-line', dest='segmented_line', action='store_false',
+                    help='skip timing the raw-document input (GPU Punkt segmentation in the step)')
     ap.add_argument('--rng', choices=['replay', 'native'], default='replay',
                     help='replay: CPython MT19937 per partition, bit-exact with the reference; '
                          'native: Philox counter RNG, documents and pairs in parallel')
@@ -201,6 +270,9 @@ def main():
         adt, atok, _, astats, _ = timed(other)
         alt = {'rng': other, 'value': atok / adt, 'ms_per_step': adt / args.steps * 1e3,
                'plan_ms': float(np.mean([x['plan_ms'] for x in astats]))}
+    seg = None
+    if args.segmented_line:  # the same hot path from raw document text: GPU Punkt first
+        seg = timed_segmented(args, rank, world, ctx, dev)
     mem = torch.cuda.memory_stats()
     if rank != 0:
         dist.destroy_process_group()
@@ -293,6 +365,8 @@ def main():
         res['balance_phases_ms_untimed_step'] = bal_ms
     if alt is not None:
         res['alt_rng'] = alt
+    if seg is not None:
+        res['with_segmentation'] = seg
     res['torch_alloc_retries'] = int(mem.get('num_alloc_retries', 0))
     free_b, total_b = torch.cuda.mem_get_info()
     res['memory_gb'] = {'torch_max_reserved': round(torch.cuda.max_memory_reserved() / 1e9, 1),

@@ -44,6 +44,11 @@ int64_t lddl_synth_corpus(uint64_t seed, int64_t doc_begin, int64_t target_bytes
                           int64_t* sent_off, int64_t sent_cap, int64_t* doc_sent_off,
                           int64_t doc_cap, int64_t* n_sent_out, int64_t* n_doc_out,
                           int n_threads);
+/* The same synthetic documents as raw document text (sentences joined by one space), for the
+ * segmentation path: text[doc_off[d] .. doc_off[d+1]). Returns the byte count (< 0: capacity). */
+int64_t lddl_synth_doc_text(uint64_t seed, int64_t doc_begin, int64_t target_bytes,
+                            double nonascii_frac, uint8_t* text, int64_t text_cap, int64_t* doc_off,
+                            int64_t doc_cap, int64_t* n_doc_out, int n_threads);
 
 /* ---------------------------------------------------------------------------------------------
  * Context = device-resident tokenizer tables.
@@ -73,6 +78,33 @@ int lddl_ctx_render_table(const lddl_ctx* ctx, const uint8_t** d_bytes, const in
 int lddl_tokenize(lddl_ctx* ctx, void* stream, const uint8_t* d_text, int64_t n_bytes,
                   const int64_t* d_sent_off, int64_t n_sent, int32_t max_pieces, int32_t* d_ids,
                   int32_t* d_sent_len);
+
+/* ---------------------------------------------------------------------------------------------
+ * Punkt sentence segmentation (device in, device out).
+ * Replaces `nltk.tokenize.sent_tokenize(text)` + `strip()` + dropping empty sentences
+ * (lddl/dask/bert/pretrain.py:86-88) for every document of a batch: nltk 3.6.5's
+ * PunktSentenceTokenizer(params).span_tokenize (nltk/tokenize/punkt.py:1316-1391, realign
+ * 1351-1379, annotation 582-630 / 1516-1650), segment.hip.
+ * lddl_punkt_set_params: `table` = lddl_amd/assets/punkt_props.bin (Python's character classes),
+ *   `records` = the PunktParameters (abbrev_types, sent_starters, ortho_context, collocations)
+ *   as records (u8 kind 1/2/3/4, u8 value = ortho flags, u16 len_a, u16 len_b, UTF-8 bytes a, b);
+ *   records_bytes = 0 is the untrained PunktSentenceTokenizer(). Keys longer than 255 bytes are
+ *   rejected. Must be called once before lddl_segment_count.
+ * lddl_segment_count: documents d_text[d_doc_off[d] .. d_doc_off[d+1]) (the text after the
+ *   document id, readers.py:131-136; documents contiguous); returns the sentence count
+ *   (synchronises the stream). Exactly one lddl_segment_fill must follow on the same ctx.
+ * lddl_segment_fill -> d_sent_off[n_sent+1], d_doc_sent_off[n_doc+1]: sentence k of document d
+ *   is d_text[sent_off[doc_sent_off[d]+k] .. sent_off[...+1]); it equals the reference's
+ *   stripped sentence up to leading/trailing whitespace (sentences are contiguous: whitespace
+ *   between sentences is attached to the left one, which the BERT tokenizer ignores), and a
+ *   whitespace-only sentence stands for the reference's dropped empty string (0 pieces, dropped
+ *   by the pair builder exactly like pretrain.py:92-97). The output feeds lddl_tokenize.
+ * ------------------------------------------------------------------------------------------- */
+int lddl_punkt_set_params(lddl_ctx* ctx, const uint8_t* table, int64_t table_bytes,
+                          const uint8_t* records, int64_t records_bytes);
+int lddl_segment_count(lddl_ctx* ctx, void* stream, const uint8_t* d_text, int64_t n_bytes,
+                       const int64_t* d_doc_off, int64_t n_doc, int64_t* n_sent);
+int lddl_segment_fill(lddl_ctx* ctx, void* stream, int64_t* d_sent_off, int64_t* d_doc_sent_off);
 
 /* ---------------------------------------------------------------------------------------------
  * NSP pairs + static masking for a batch of partitions (device in, device out).

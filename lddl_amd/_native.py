@@ -24,6 +24,12 @@ SIGNATURES = {
     'lddl_ctx_destroy': (ctypes.c_int, [c_vp]),
     'lddl_ctx_info': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
     'lddl_ctx_render_table': (ctypes.c_int, [c_vp, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp)]),
+    'lddl_synth_doc_text': (c_i64, [c_u64, c_i64, c_i64, c_dbl, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                    ctypes.c_int]),
+    'lddl_punkt_set_params': (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_i64]),
+    'lddl_segment_count': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                          ctypes.POINTER(c_i64)]),
+    'lddl_segment_fill': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
     'lddl_tokenize': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp]),
     'lddl_pairs_plan': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
                                        c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),

@@ -99,7 +99,9 @@ struct lddl_ctx {
   int32_t vocab_size = 0;
   std::vector<std::string> tokens;  // host copy of the vocab lines
   lddl::DevArena arena;             // per-call temporaries (pair plans)
+  void* punkt = nullptr;            // lddl_punkt_state (segment.hip), created by lddl_punkt_set_params
 };
+extern "C" void lddl_punkt_release(lddl_ctx* c);
 
 namespace lddl {
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

@@ -205,3 +205,42 @@ extern "C" int64_t lddl_synth_corpus(uint64_t seed, int64_t doc_begin, int64_t t
   *n_doc_out = ndoc;
   return nbytes;
 }
+
+// The same documents as raw document text (what the reference hands to sent_tokenize): each
+// document's sentences joined by one space, documents back to back, doc_off[n_doc+1] byte offsets.
+extern "C" int64_t lddl_synth_doc_text(uint64_t seed, int64_t doc_begin, int64_t target_bytes,
+                                       double nonascii_frac, uint8_t* text, int64_t text_cap,
+                                       int64_t* doc_off, int64_t doc_cap, int64_t* n_doc_out,
+                                       int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  const int64_t kBlock = 256;
+  const Lexicon& lex = lexicon(seed);
+  int64_t nbytes = 0, ndoc = 0;
+  doc_off[0] = 0;
+  std::vector<std::vector<std::string>> blocks(n_threads * kBlock);
+  int64_t next_doc = doc_begin;
+  while (nbytes < target_bytes) {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < n_threads; ++t)
+      pool.emplace_back([&, t]() {
+        for (int64_t k = 0; k < kBlock; ++k)
+          make_doc(lex, seed, next_doc + t * kBlock + k, nonascii_frac, blocks[t * kBlock + k]);
+      });
+    for (auto& th : pool) th.join();
+    for (auto& doc : blocks) {
+      if (nbytes >= target_bytes) break;
+      if (ndoc + 1 >= doc_cap) return -2;
+      for (size_t k = 0; k < doc.size(); ++k) {
+        const std::string& s = doc[k];
+        if (nbytes + (int64_t)s.size() + 1 > text_cap) return -1;
+        if (k) text[nbytes++] = ' ';
+        std::memcpy(text + nbytes, s.data(), s.size());
+        nbytes += (int64_t)s.size();
+      }
+      doc_off[++ndoc] = nbytes;
+    }
+    next_doc += n_threads * kBlock;
+  }
+  *n_doc_out = ndoc;
+  return nbytes;
+}

@@ -53,6 +53,18 @@ def generate(seed=1234, n_bytes=1 << 20, doc_begin=0, nonascii_frac=0.01, thread
     return Corpus(text[:n], so[:ns.value + 1].copy(), do[:nd.value + 1].copy())
 
 
+def generate_doc_text(seed=1234, n_bytes=1 << 20, doc_begin=0, nonascii_frac=0.01, threads=8):
+    """The documents of `generate` as raw text (sentences joined by one space): (text uint8,
+    doc_off int64[n_doc+1]) -- the input of sentence segmentation."""
+    cap = n_bytes + (1 << 20)
+    text = np.empty(cap, np.uint8)
+    do = np.empty(n_bytes // 64 + 1024, np.int64)
+    nd = ctypes.c_int64()
+    n = check(lib.lddl_synth_doc_text(seed, doc_begin, n_bytes, nonascii_frac, text.ctypes.data,
+                                      cap, do.ctypes.data, len(do), ctypes.byref(nd), threads))
+    return text[:n], do[:nd.value + 1].copy()
+
+
 def from_documents(docs):
     """Build a Corpus from a list of documents (lists of sentence strings)."""
     chunks, so, do = [], [0], [0]

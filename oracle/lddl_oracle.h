@@ -63,6 +63,17 @@ int64_t orc_partition_pairs(const orc_pair_params* p, int64_t seed, const int64_
                             int32_t* out_lab, int64_t pos_cap, int64_t* out_pos_off);
 
 /* Binning (binning.py:63-93): bin id per sample and the stable by-bin row order. */
+/* nltk Punkt sentence spans (PunktSentenceTokenizer.span_tokenize), oracle/punkt_oracle.c.
+ * table = lddl_amd/assets/punkt_props.bin; params = records (u8 kind 1 abbrev / 2 sentence
+ * starter / 3 ortho context / 4 collocation, u8 value, u16 len_a, u16 len_b, bytes a, bytes b).
+ * Spans are byte offsets relative to each document. */
+typedef struct orc_punkt orc_punkt;
+orc_punkt* orc_punkt_create(const uint8_t* table, int64_t table_bytes, const uint8_t* params,
+                            int64_t params_bytes);
+void orc_punkt_destroy(orc_punkt* o);
+int64_t orc_punkt_spans(orc_punkt* o, const uint8_t* text, const int64_t* doc_off, int64_t n_doc,
+                        int64_t* span_start, int64_t* span_end, int64_t* doc_count);
+
 void orc_bin(const int32_t* num_tokens, int64_t n, int32_t bin_size, int32_t nbins,
              int32_t* bin_id, int64_t* order, int64_t* bin_counts);
 

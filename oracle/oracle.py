@@ -42,6 +42,9 @@ def _load():
         'orc_partition_pairs': (i64, [ctypes.POINTER(PairParams), i64, P, i64, P, P, P, i64, P, P,
                                       P, i64, P, P, i64, P]),
         'orc_bin': (None, [P, i64, i32, i32, P, P, P]),
+        'orc_punkt_create': (P, [P, i64, P, i64]),
+        'orc_punkt_destroy': (None, [P]),
+        'orc_punkt_spans': (i64, [P, P, P, i64, P, P, P]),
     }
     for k, (r, a) in sig.items():
         f = getattr(lib, k)
@@ -158,3 +161,50 @@ def bin_samples(num_tokens, bin_size, nbins):
     counts = np.empty(nbins, np.int64)
     lib.orc_bin(_p(nt), n, bin_size, nbins, _p(bin_id), _p(order), _p(counts))
     return bin_id, order, counts
+
+
+def punkt_params_blob(params):
+    """Records of a Punkt parameter dict {abbrev_types, sent_starters, ortho_context,
+    collocations} in the oracle's layout (lddl_oracle.h)."""
+    import struct
+    out = []
+
+    def rec(kind, value, a, b=''):
+        a, b = a.encode('utf-8'), b.encode('utf-8')
+        out.append(struct.pack('<BBHH', kind, value, len(a), len(b)) + a + b)
+    for t in (params or {}).get('abbrev_types', []):
+        rec(1, 0, t)
+    for t in (params or {}).get('sent_starters', []):
+        rec(2, 0, t)
+    for t, v in (params or {}).get('ortho_context', {}).items():
+        rec(3, int(v), t)
+    for a, b in (params or {}).get('collocations', []):
+        rec(4, 0, a, b)
+    return b''.join(out)
+
+
+class Punkt:
+    """nltk PunktSentenceTokenizer(params) spans, per document (byte offsets)."""
+
+    def __init__(self, params=None):
+        table = np.fromfile(os.path.join(ASSETS, 'punkt_props.bin'), np.uint8)
+        blob = np.frombuffer(punkt_params_blob(params) or b'\0', np.uint8)
+        self._keep = (table, blob)
+        self.h = lib.orc_punkt_create(_p(table), len(table), _p(blob),
+                                      len(punkt_params_blob(params)))
+        assert self.h
+
+    def __del__(self):
+        if getattr(self, 'h', None):
+            lib.orc_punkt_destroy(self.h)
+
+    def spans(self, text, doc_off):
+        text = np.ascontiguousarray(text, np.uint8)
+        doc_off = np.ascontiguousarray(doc_off, np.int64)
+        n_doc = len(doc_off) - 1
+        cap = int(doc_off[-1] - doc_off[0]) + n_doc + 1
+        st = np.empty(cap, np.int64)
+        en = np.empty(cap, np.int64)
+        cnt = np.empty(max(n_doc, 1), np.int64)
+        n = lib.orc_punkt_spans(self.h, _p(text), _p(doc_off), n_doc, _p(st), _p(en), _p(cnt))
+        return st[:n].copy(), en[:n].copy(), cnt[:n_doc].copy()
