@@ -5,7 +5,9 @@ Pipeline (reference call stack in SURVEY.md §3.1):
   read `*.txt` sources into blocks (readers.py)            -> lddl_amd.dask.readers (host)
   random shuffle of documents over partitions (100-111)    -> seeded permutation (host; the
                                                               reference's is unseeded)
-  split_id_text + sent_tokenize + strip (82-88)            -> host (segment.py)
+  split_id_text (readers.py:131-136)                       -> host, per line
+  sent_tokenize + strip + drop empty (86-88)               -> lddl_segment_* (HIP Punkt; host
+                                                              segment.py with --sentence-splitter host)
   tokenizer.tokenize(s, max_length=512, truncation=True)   -> lddl_tokenize (HIP)
   _to_partition_pairs / create_pairs_from_document /
     create_masked_lm_predictions (386-402, 241-365, 182-238) -> lddl_pairs_plan / emit (HIP)
@@ -116,19 +118,57 @@ def build_corpus(partitions, workers=1):
     return text, sent_off, doc_sent_off, part_doc_off
 
 
+def build_doc_corpus(partitions):
+    """Raw document texts for the GPU segmenter: the text after each line's id
+    (split_id_text, readers.py:131-136), documents back to back, plus document byte offsets and
+    partition document offsets."""
+    chunks, part_nd = [], []
+    for _, lines in partitions:
+        part_nd.append(len(lines))
+        for raw in lines:
+            chunks.append(readers.split_id_text(raw)[1].encode('utf-8'))
+    text = np.frombuffer(b''.join(chunks), np.uint8) if chunks else np.zeros(0, np.uint8)
+    doc_off = np.zeros(len(chunks) + 1, np.int64)
+    np.cumsum([len(c) for c in chunks], out=doc_off[1:])
+    part_doc_off = np.zeros(len(part_nd) + 1, np.int64)
+    np.cumsum(part_nd, out=part_doc_off[1:])
+    return 'documents', text, doc_off, part_doc_off
+
+
+def punkt_params(args):
+    """--punkt-params JSON, else nltk's English model when nltk can load it locally (the
+    reference's sent_tokenize), else the untrained parameters (what offline nltk runs)."""
+    from ...punkt import PunktParams
+    if getattr(args, 'punkt_params', None):
+        return PunktParams.from_json(args.punkt_params)
+    try:
+        import nltk
+        return PunktParams.from_nltk(nltk.data.load('tokenizers/punkt/english.pickle'))
+    except Exception:  # nltk or its English model unavailable offline
+        return PunktParams()
+
+
 def process_batch(ctx, args, partitions, corpus, outdir):
     """Run the GPU hot path over a group of partitions and write their files."""
     import torch
     from ...pairs import make_pairs
     from ... import output
-    text, sent_off, doc_sent_off, part_doc_off = corpus
     dev = ctx.device
-    d_text = torch.from_numpy(text).to(dev) if len(text) else torch.zeros(1, dtype=torch.uint8,
-                                                                         device=dev)[:0]
-    d_so = torch.from_numpy(sent_off).to(dev)
+    if corpus[0] == 'documents':  # GPU Punkt: sentences of every document of the batch
+        from ... import punkt
+        _, text, doc_off, part_doc_off = corpus
+        d_text = torch.from_numpy(text).to(dev) if len(text) else torch.zeros(
+            1, dtype=torch.uint8, device=dev)[:0]
+        d_so, d_dso = punkt.segment(ctx, d_text, torch.from_numpy(doc_off).to(dev))
+    else:
+        _, text, sent_off, doc_sent_off, part_doc_off = corpus
+        d_text = torch.from_numpy(text).to(dev) if len(text) else torch.zeros(
+            1, dtype=torch.uint8, device=dev)[:0]
+        d_so = torch.from_numpy(sent_off).to(dev)
+        d_dso = torch.from_numpy(doc_sent_off).to(dev)
     ids, sent_len = ctx.tokenize(d_text, d_so, max_pieces=512)
     seeds = np.asarray([partition_seed(args.seed, p) for p, _ in partitions], np.int64)
-    pb = make_pairs(ctx, d_so, ids, sent_len, torch.from_numpy(doc_sent_off).to(dev),
+    pb = make_pairs(ctx, d_so, ids, sent_len, d_dso,
                     torch.from_numpy(part_doc_off).to(dev), torch.from_numpy(seeds).to(dev),
                     seq=args.target_seq_length, dup=args.duplicate_factor, masking=args.masking,
                     short_seq_prob=args.short_seq_prob, masked_lm_ratio=args.masked_lm_ratio,
@@ -213,14 +253,19 @@ def main(args):
     tic = time.perf_counter()
     outdir = expand_outdir_and_mkdir(args.sink)
     partitions = get_partitions(args, rank, world)
-    # host segmentation first: its process pool forks before this process touches the GPU
-    batches = [(b, build_corpus(b, args.local_n_workers))
-               for b in _batches(partitions, args.gpu_batch_bytes)]
+    if args.sentence_splitter == 'gpu':
+        batches = [(b, build_doc_corpus(b)) for b in _batches(partitions, args.gpu_batch_bytes)]
+    else:  # host segmentation first: its process pool forks before this process touches the GPU
+        batches = [(b, ('sentences',) + build_corpus(b, args.local_n_workers))
+                   for b in _batches(partitions, args.gpu_batch_bytes)]
     import torch
     if world > 1:
         torch.cuda.set_device(local)
     from ...context import Context
     ctx = Context(vocab, do_lower_case=True)  # BertTokenizerFast default, SURVEY H5
+    if args.sentence_splitter == 'gpu':
+        from ... import punkt
+        punkt.set_params(ctx, punkt_params(args))
     n_files = 0
     for batch, corpus in batches:
         n_files += len(process_batch(ctx, args, batch, corpus, outdir))
@@ -281,6 +326,13 @@ def attach_args(parser=None):
     parser.add_argument('--masked-lm-ratio', type=float, default=0.15, help='Default: 0.15')
     parser.add_argument('--gpu-batch-bytes', type=int, default=1 << 30,
                         help='lddl_amd: input text bytes per GPU batch of partitions')
+    parser.add_argument('--sentence-splitter', choices=['gpu', 'host'], default='gpu',
+                        help='gpu: Punkt on the GPU (exact nltk PunktSentenceTokenizer); host: '
+                             'lddl_amd.dask.bert.segment (nltk if importable, else rules)')
+    parser.add_argument('--punkt-params', type=str, default=None,
+                        help='JSON PunktParameters (abbrev_types, collocations, sent_starters, '
+                             'ortho_context); default: nltk English model if loadable, else '
+                             'untrained')
     parser.add_argument('--rng', choices=['replay', 'native'], default='replay',
                         help="lddl_amd: 'replay' reproduces CPython random per partition "
                              "(random.seed(partition seed)), bit-exact with the reference; "

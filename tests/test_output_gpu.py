@@ -114,6 +114,7 @@ def _write_source(root, n_docs=300, seed=11):
 
 @pytest.mark.parametrize('binned', [False, True])
 def test_pretrain_cli_vs_oracle(tmp_path, binned):
+    from lddl_amd import synth
     from lddl_amd.dask.bert import pretrain as P
     from oracle import oracle as O
     src = tmp_path / 'source'
@@ -132,8 +133,18 @@ def test_pretrain_cli_vs_oracle(tmp_path, binned):
     tok = O.Tokenizer(VOCAB_UNCASED, lowercase=True)
     vocab = [l.rstrip('\n') for l in open(VOCAB_UNCASED, encoding='utf-8')]
     cls, sep, msk = (tok.token_id(t) for t in ('[CLS]', '[SEP]', '[MASK]'))
+    punkt = O.Punkt()  # the CLI segments on the GPU: nltk's untrained Punkt, exactly
     for p, lines in parts:
-        text, so, dso, pdo = P.build_corpus([(p, lines)])
+        _, dtext, doc_off, _ = P.build_doc_corpus([(p, lines)])
+        st, en, cnt = punkt.spans(dtext, doc_off)
+        docs, k = [], 0
+        for d in range(len(doc_off) - 1):
+            ss = [bytes(dtext[doc_off[d] + st[j]:doc_off[d] + en[j]]).decode().strip()
+                  for j in range(k, k + cnt[d])]
+            docs.append([x for x in ss if x])
+            k += cnt[d]
+        corp = synth.from_documents(docs)
+        text, so, dso = corp.text, corp.sent_off, corp.doc_sent_off
         ids, off = tok.tokenize(text, so)
         lens = np.diff(off)
         keep = lens > 0
