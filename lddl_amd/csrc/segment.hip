@@ -109,7 +109,15 @@ struct Src {
   }
 };
 
+// class bits of an ASCII code point, computed (the table agrees: tests/test_punkt.py)
+__device__ __forceinline__ uint32_t ascii_props(uint32_t c) {
+  const bool up = c - 'A' < 26u, lo = c - 'a' < 26u;
+  return (ascii_space(c) ? kPSpace : 0u) | (up ? kPUpper : 0u) | (lo ? kPLower : 0u) |
+         ((up || lo || c == '_') ? kPAlnod : 0u) | (c - '0' < 10u ? kPDigit : 0u);
+}
+
 __device__ __forceinline__ uint32_t props(const PunktTab& t, uint32_t cp) {
+  if (cp < 128u) return ascii_props(cp);
   if (cp >= 0x110000u) return 0;
   return t.pages[(uint32_t)t.l1[cp >> 8] * 256u + (cp & 255u)];
 }
@@ -262,8 +270,9 @@ __device__ inline void make_tok(const PunktTab& t, const Src& x, int64_t s, int6
   k.s = s;
   k.e = e;
   k.c0 = decode(x, s, e, &k.c0len);
-  k.numeric = is_numeric(t, x, s, e);
   k.period_final = x[e - 1] == '.';
+  // the type ("##number##" or not) is only consulted for period-final tokens and parameter keys
+  k.numeric = (k.period_final || t.n_rec) ? is_numeric(t, x, s, e) : false;
   k.sentbreak = k.abbr = k.ellipsis = false;
   // _first_pass_annotation
   const int64_t n = e - s;
@@ -411,18 +420,24 @@ __device__ inline bool contains_sentbreak(const PunktTab& t, const Src& x, int64
 }
 
 constexpr int kSegWaves = 4;
-constexpr int kSlab = 6144;     // LDS bytes per wave: [blk - kSlabBack, blk + kSlab - kSlabBack)
-constexpr int kSlabBack = 256;  // look-behind kept for run starts / contexts
-constexpr int kBlk = kSlab - 2 * kSlabBack;  // bytes classified per slab (look-ahead = kSlabBack)
-constexpr int kQ = 128;         // queued candidate contexts per wave
+constexpr int kSlab = 4096;     // LDS bytes per classifying wave
+constexpr int kCtx = 64;        // context bytes staged per candidate lane
+constexpr int kRowW = 17;       // LDS row stride in dwords (68 B: conflict-free byte walks)
+constexpr int kEvalBlock = 256;
 
-// One selected sentence ender q (with the start of its whitespace-free run): evaluate its
-// period context, and if it is a cut, its realigned boundary.
+// One qualified sentence ender q: if it is the match of its run (the last qualified ender
+// before the next whitespace), evaluate its period context; for a cut, its realigned boundary.
 template <bool kParams>
-__device__ inline bool eval_candidate(const PunktTab& t, const Src& src, int64_t i, int64_t run_start,
-                                      int64_t b0, int64_t b1, int64_t rs, int64_t* bound) {
+__device__ inline bool eval_candidate(const PunktTab& t, const Src& src, int64_t i, int64_t b0, int64_t b1,
+                                      int64_t rs, int64_t* bound) {
   int64_t s2 = 0, e2 = 0, e1 = i + 1, next_start;
   if (non_word(src[i + 1])) {
+    // finditer takes the LAST qualified ender of the run: any later one in the run wins
+    for (int64_t k = i + 1; k < rs; ++k) {
+      if (space_at(t, src, k, b0, b1)) break;
+      if (sent_end(src[k]) && k + 1 < rs && (non_word(src[k + 1]) || space_at(t, src, k + 1, b0, b1)))
+        return false;
+    }
     e1 = i + 2;  // context = match + the NonWord char
     next_start = i + 1;
   } else {
@@ -432,6 +447,8 @@ __device__ inline bool eval_candidate(const PunktTab& t, const Src& src, int64_t
     while (e2 < b1 && !space_at(t, src, e2, b0, b1)) ++e2;
     next_start = s2;
   }
+  int64_t run_start = i;  // the match starts at the run's first byte
+  while (run_start > b0 && !space_at(t, src, run_start - 1, b0, b1)) --run_start;
   if (!contains_sentbreak(t, src, run_start, e1, s2, e2)) return false;
   // _realign_boundaries: a closing run followed by whitespace, "--" or the end moves left
   int64_t k = next_start;
@@ -442,30 +459,22 @@ __device__ inline bool eval_candidate(const PunktTab& t, const Src& src, int64_t
   return true;
 }
 
-// one wavefront per document; rel[] receives the cut positions (relative to the document start)
-// at slot base (doc_off[d] - doc_off[0]) / 2 + d, cnt[d] = 1 + number of cuts.
-// The document streams through a per-wave LDS slab (16 B per lane per load). Lanes classify one
-// byte each per 64-byte window and queue the selected enders (position + run start) in LDS; the
-// queue is evaluated one candidate per lane (the sequential context walk reads the slab; bytes
-// outside it come from global memory through Src) and the cuts are appended in order.
-// kParams = false: the untrained tokenizer (no parameter lookups, no private key buffers)
-template <bool kParams>
-__global__ void __launch_bounds__(64 * kSegWaves) segment_kernel(PunktTab t, const uint8_t* __restrict__ x,
-                                                                  int64_t n_bytes,
-                                                                  const int64_t* __restrict__ doc_off,
-                                                                  int64_t n_doc, int32_t* __restrict__ rel,
-                                                                  int32_t* __restrict__ cnt) {
+// K1: one wavefront per document streams it through a 4-KB LDS slab (16 B per lane per load),
+// one byte per lane per 64-byte window, and appends every lookahead-qualified sentence ender
+// (text[q] in .?! and text[q+1] NonWord, or whitespace with non-whitespace later) in order to
+// the document's slot range cand[(doc_off[d] - doc_off[0]) / 2 + d ..] (a document of L bytes
+// has at most L/2 + 1 whitespace-free runs, the bound of both candidates and cuts).
+__global__ void __launch_bounds__(64 * kSegWaves) segment_classify_kernel(
+    PunktTab t, const uint8_t* __restrict__ x, int64_t n_bytes, const int64_t* __restrict__ doc_off,
+    int64_t n_doc, int32_t* __restrict__ cand, int32_t* __restrict__ ccnt, int32_t* __restrict__ rs_rel,
+    int32_t* __restrict__ cnt) {
   __shared__ uint4 slab_all[kSegWaves][kSlab / 16];
-  __shared__ int32_t queue_all[kSegWaves][2][kQ];
   const int64_t d = (int64_t)blockIdx.x * kSegWaves + (threadIdx.x >> 6);
   if (d >= n_doc) return;  // wave-uniform
-  if (!kParams) t.n_rec = 0;
   const int lane = lane_id();
   uint4* slab = slab_all[threadIdx.x >> 6];
-  int32_t* qpos = queue_all[threadIdx.x >> 6][0];
-  int32_t* qrun = queue_all[threadIdx.x >> 6][1];
   const int64_t b0 = doc_off[d], b1 = doc_off[d + 1];
-  int32_t* out = rel + ((b0 - doc_off[0]) >> 1) + d;
+  int32_t* out = cand + ((b0 - doc_off[0]) >> 1) + d;
   const Src g{x, reinterpret_cast<const uint8_t*>(slab), 0, 0};  // global only
   // rstrip end: one past the last non-whitespace byte
   int64_t rs = b0;
@@ -479,13 +488,12 @@ __global__ void __launch_bounds__(64 * kSegWaves) segment_kernel(PunktTab t, con
     }
   }
   const bool aligned = ((uintptr_t)x & 15u) == 0;
-  int32_t nb = 0;
-  int64_t last_sp = b0 - 1;  // last whitespace byte before the window
-  for (int64_t blk = b0; blk < rs; blk += kBlk) {
-    // slab [lo, hi): 16-byte aligned, inside the text buffer
-    const int64_t lo = std::max<int64_t>(0, (blk - kSlabBack) & ~(int64_t)15);
+  int32_t nc = 0;
+  for (int64_t blk = b0; blk < rs;) {
+    const int64_t lo = blk & ~(int64_t)15;
     const int64_t hi = std::min<int64_t>(n_bytes, lo + kSlab);
-    wave_sync();  // previous slab and queue fully consumed
+    wave_sync();  // previous slab consumed
+#pragma unroll
     for (int r = lane; r < kSlab / 16; r += 64) {
       const int64_t a = lo + 16 * (int64_t)r;
       uint4 v = make_uint4(0, 0, 0, 0);
@@ -500,61 +508,28 @@ __global__ void __launch_bounds__(64 * kSegWaves) segment_kernel(PunktTab t, con
     }
     wave_sync();
     const Src src{x, reinterpret_cast<const uint8_t*>(slab), lo, hi};
-    const int64_t bend = std::min<int64_t>(rs, blk + kBlk);
-    int qn = 0;
-    for (int64_t base = blk;; base += 64) {
-      const bool more = base < bend;
-      if (more) {
-        const int64_t i = base + lane;
-        const bool valid = i < rs;
-        const uint32_t c = valid ? src[i] : 0u;
-        const bool sp = valid && space_at(t, src, i, b0, b1);
-        // lookahead-qualified sentence ender that is the last one of its run
-        bool sel = false;
-        if (valid && sent_end(c) && i + 1 < rs) {
-          const uint32_t cj = src[i + 1];
-          if (non_word(cj)) {
-            sel = true;  // scan the rest of the run for a later qualified ender
-            for (int64_t k = i + 1; k < rs && sel; ++k) {
-              if (space_at(t, src, k, b0, b1)) break;
-              if (sent_end(src[k]) && k + 1 < rs && (non_word(src[k + 1]) || space_at(t, src, k + 1, b0, b1)))
-                sel = false;
-            }
-          } else {
-            sel = space_at(t, src, i + 1, b0, b1);
-          }
+    const int64_t bend = std::min<int64_t>(rs, hi);
+    for (int64_t base = blk; base < bend; base += 64) {
+      const int64_t i = base + lane;
+      bool q = false;
+      if (i < bend) {
+        const uint32_t c = src[i];
+        if (sent_end(c) && i + 1 < rs) {
+          const uint32_t cn = src[i + 1];
+          q = non_word(cn) || (cn < 0x80 ? ascii_space(cn) : space_at(t, src, i + 1, b0, b1));
         }
-        const uint64_t spm = ballot(sp);
-        const uint64_t below = spm & ((1ull << lane) - 1ull);
-        const int64_t run_start = below ? base + (63 - __builtin_clzll(below)) + 1 : last_sp + 1;
-        if (spm) last_sp = base + (63 - __builtin_clzll(spm));
-        const uint64_t sm = ballot(sel);
-        if (sel) {
-          const int slot = qn + (int)popc_below(sm);
-          qpos[slot] = (int32_t)(i - b0);
-          qrun[slot] = (int32_t)(run_start - b0);
-        }
-        qn += __builtin_popcountll(sm);
       }
-      if (qn > kQ - 64 || (!more && qn > 0)) {  // evaluate the queue, one candidate per lane
-        wave_sync();
-        for (int c0 = 0; c0 < qn; c0 += 64) {
-          bool cut = false;
-          int64_t bound = 0;
-          if (c0 + lane < qn)
-            cut = eval_candidate<kParams>(t, src, b0 + qpos[c0 + lane], b0 + qrun[c0 + lane], b0, b1, rs,
-                                          &bound);
-          const uint64_t cm = ballot(cut);
-          if (cut) out[nb + (int32_t)popc_below(cm)] = (int32_t)(bound - b0);
-          nb += __builtin_popcountll(cm);
-        }
-        wave_sync();
-        qn = 0;
-      }
-      if (!more) break;
+      const uint64_t qm = ballot(q);
+      if (q) out[nc + (int32_t)popc_below(qm)] = (int32_t)(i - b0);
+      nc += __builtin_popcountll(qm);
     }
+    blk = bend;
   }
-  if (lane == 0) cnt[d] = nb + 1;
+  if (lane == 0) {
+    ccnt[d] = nc;
+    rs_rel[d] = (int32_t)(rs - b0);
+    cnt[d] = 1;
+  }
 }
 
 struct CntAt {
@@ -562,17 +537,85 @@ struct CntAt {
   __device__ int64_t operator()(int64_t i) const { return cnt[i]; }
 };
 
-// sent_off[doc_sent_off[d] + k]: document start, then its cuts; sent_off[n_sent] = text end
-__global__ void segment_fill_kernel(const int64_t* __restrict__ doc_off, int64_t n_doc,
-                                    const int32_t* __restrict__ rel, const int64_t* __restrict__ dso,
-                                    int64_t* __restrict__ sent_off) {
+// K1b: candidates into one flat list (position, document), in document order
+__global__ void segment_flatten_kernel(const int64_t* __restrict__ doc_off, int64_t n_doc,
+                                       const int32_t* __restrict__ cand, const int64_t* __restrict__ coff,
+                                       int64_t* __restrict__ fq, int32_t* __restrict__ fdoc) {
   const int64_t d = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (d >= n_doc) return;
   const int64_t b0 = doc_off[d];
-  const int32_t* in = rel + ((b0 - doc_off[0]) >> 1) + d;
-  const int64_t o = dso[d], n = dso[d + 1] - o;
-  for (int64_t k = lane_id(); k < n; k += 64) sent_off[o + k] = k == 0 ? b0 : b0 + in[k - 1];
-  if (d == n_doc - 1 && lane_id() == 0) sent_off[dso[n_doc]] = doc_off[n_doc];
+  const int32_t* in = cand + ((b0 - doc_off[0]) >> 1) + d;
+  const int64_t o = coff[d], n = coff[d + 1] - o;
+  for (int64_t k = lane_id(); k < n; k += 64) {
+    fq[o + k] = b0 + in[k];
+    fdoc[o + k] = (int32_t)d;
+  }
+}
+
+// K2: one lane per candidate. The lane stages 64 bytes around its ender in a private LDS row
+// (four 16-B loads issued together), then walks the context from LDS (Src falls back to global
+// memory outside the row). fbound = realigned cut position, or -1; cnt[d] counts the cuts.
+template <bool kParams>
+__global__ void __launch_bounds__(kEvalBlock) segment_eval_kernel(
+    PunktTab t, const uint8_t* __restrict__ x, int64_t n_bytes, const int64_t* __restrict__ doc_off,
+    const int32_t* __restrict__ rs_rel, const int64_t* __restrict__ fq, const int32_t* __restrict__ fdoc,
+    int64_t n_cand, int64_t* __restrict__ fbound, int32_t* __restrict__ cnt) {
+  __shared__ uint32_t rows[kEvalBlock * kRowW];
+  if (!kParams) t.n_rec = 0;
+  const int64_t c = (int64_t)blockIdx.x * kEvalBlock + threadIdx.x;
+  if (c >= n_cand) return;
+  uint32_t* row = rows + threadIdx.x * kRowW;
+  const int64_t q = fq[c];
+  const int32_t d = fdoc[c];
+  const int64_t b0 = doc_off[d], b1 = doc_off[d + 1], rs = b0 + rs_rel[d];
+  const int64_t w0 = std::max<int64_t>(0, (q - 24) & ~(int64_t)15);
+  const int64_t w1 = std::min<int64_t>(n_bytes, w0 + kCtx);
+  uint4 v[kCtx / 16];
+  const bool aligned = ((uintptr_t)x & 15u) == 0;
+#pragma unroll
+  for (int k = 0; k < kCtx / 16; ++k) {
+    const int64_t a = w0 + 16 * k;
+    v[k] = make_uint4(0, 0, 0, 0);
+    if (a + 16 <= w1 && aligned) {
+      v[k] = *reinterpret_cast<const uint4*>(x + a);
+    } else if (a < w1) {
+      uint8_t tmp[16] = {};
+      for (int j = 0; j < 16 && a + j < w1; ++j) tmp[j] = x[a + j];
+      memcpy(&v[k], tmp, 16);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kCtx / 16; ++k) {
+    row[4 * k] = v[k].x;
+    row[4 * k + 1] = v[k].y;
+    row[4 * k + 2] = v[k].z;
+    row[4 * k + 3] = v[k].w;
+  }
+  const Src src{x, reinterpret_cast<const uint8_t*>(row), w0, w1};
+  int64_t bound = -1;
+  const bool cut = eval_candidate<kParams>(t, src, q, b0, b1, rs, &bound);
+  fbound[c] = cut ? bound : -1;
+  if (cut) atomicAdd(&cnt[d], 1);
+}
+
+// sent_off[doc_sent_off[d] + k]: document start, then its cuts in order; sent_off[n_sent] = end
+__global__ void segment_fill_kernel(const int64_t* __restrict__ doc_off, int64_t n_doc,
+                                    const int64_t* __restrict__ coff, const int64_t* __restrict__ fbound,
+                                    const int64_t* __restrict__ dso, int64_t* __restrict__ sent_off) {
+  const int64_t d = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (d >= n_doc) return;
+  const int lane = lane_id();
+  const int64_t o = dso[d];
+  if (lane == 0) sent_off[o] = doc_off[d];
+  int64_t k = o + 1;
+  for (int64_t base = coff[d], e = coff[d + 1]; base < e; base += 64) {
+    const int64_t j = base + lane;
+    const int64_t bnd = j < e ? fbound[j] : -1;
+    const uint64_t m = ballot(bnd >= 0);
+    if (bnd >= 0) sent_off[k + popc_below(m)] = bnd;
+    k += __builtin_popcountll(m);
+  }
+  if (d == n_doc - 1 && lane == 0) sent_off[dso[n_doc]] = doc_off[n_doc];
 }
 
 }  // namespace
@@ -590,10 +633,13 @@ struct lddl_punkt_state {
   int32_t n_rec = 0;
   uint8_t* keys = nullptr;
   // pending segmentation (between lddl_segment_count and lddl_segment_fill)
-  DevArena::Block rel, cnt, dso, scratch;
+  DevArena::Block cand, ccnt, rs_rel, coff, fq, fdoc, fbound, cnt, dso, scratch;
   const int64_t* doc_off = nullptr;
   int64_t n_doc = -1;
   int64_t n_sent = 0;
+  std::vector<DevArena::Block*> blocks() {
+    return {&cand, &ccnt, &rs_rel, &coff, &fq, &fdoc, &fbound, &cnt, &dso, &scratch};
+  }
   void free_tables() {
     (void)hipFree(l1);
     (void)hipFree(pages);
@@ -617,7 +663,7 @@ extern "C" void lddl_punkt_release(lddl_ctx* c) {
   if (!p) return;
   (void)hipDeviceSynchronize();
   p->free_tables();
-  for (DevArena::Block* b : {&p->rel, &p->cnt, &p->dso, &p->scratch})
+  for (DevArena::Block* b : p->blocks())
     if (b->p) (void)hipFree(b->p);
   delete p;
   c->punkt = nullptr;
@@ -709,25 +755,54 @@ extern "C" int lddl_segment_count(lddl_ctx* c, void* stream, const uint8_t* d_te
   if (n_doc < 0 || n_bytes < 0 || !n_sent) LDDL_FAIL(-1, "bad sizes");
   if (ps->n_doc >= 0) LDDL_FAIL(-1, "a segmentation is pending: call lddl_segment_fill first");
   hipStream_t st = as_stream(stream);
-  const int64_t slots = n_bytes / 2 + n_doc + 2;
-  LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)slots, st, ps->rel));
-  LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)(n_doc + 1), st, ps->cnt));
-  LDDL_HIP(c->arena.take(sizeof(int64_t) * (size_t)(n_doc + 1), st, ps->dso));
-  LDDL_HIP(c->arena.take(sizeof(int64_t) * (size_t)scan_scratch_elems(n_doc), st, ps->scratch));
+  DevArena& A = c->arena;
+  const size_t nd = (size_t)n_doc + 1;
+  LDDL_HIP(A.take(sizeof(int32_t) * (size_t)(n_bytes / 2 + n_doc + 2), st, ps->cand));
+  LDDL_HIP(A.take(sizeof(int32_t) * nd, st, ps->ccnt));
+  LDDL_HIP(A.take(sizeof(int32_t) * nd, st, ps->rs_rel));
+  LDDL_HIP(A.take(sizeof(int32_t) * nd, st, ps->cnt));
+  LDDL_HIP(A.take(sizeof(int64_t) * nd, st, ps->coff));
+  LDDL_HIP(A.take(sizeof(int64_t) * nd, st, ps->dso));
+  LDDL_HIP(A.take(sizeof(int64_t) * (size_t)scan_scratch_elems(n_doc), st, ps->scratch));
+  PunktTab t{ps->l1, ps->pages, ps->lower, ps->n_lower, ps->hash, ps->hmask, ps->n_rec, ps->keys};
+  int32_t* ccnt = static_cast<int32_t*>(ps->ccnt.p);
   int32_t* cnt = static_cast<int32_t*>(ps->cnt.p);
+  int64_t* coff = static_cast<int64_t*>(ps->coff.p);
   int64_t* dso = static_cast<int64_t*>(ps->dso.p);
+  int64_t* scratch = static_cast<int64_t*>(ps->scratch.p);
+  const int64_t dgrid = std::max<int64_t>(1, (n_doc + kSegWaves - 1) / kSegWaves);
   if (n_doc > 0) {
-    PunktTab t{ps->l1, ps->pages, ps->lower, ps->n_lower, ps->hash, ps->hmask, ps->n_rec, ps->keys};
-    const int64_t grid = (n_doc + kSegWaves - 1) / kSegWaves;
-    if (ps->n_rec)
-      hipLaunchKernelGGL(segment_kernel<true>, dim3((unsigned)grid), dim3(64 * kSegWaves), 0, st, t, d_text,
-                         n_bytes, d_doc_off, n_doc, static_cast<int32_t*>(ps->rel.p), cnt);
-    else
-      hipLaunchKernelGGL(segment_kernel<false>, dim3((unsigned)grid), dim3(64 * kSegWaves), 0, st, t, d_text,
-                         n_bytes, d_doc_off, n_doc, static_cast<int32_t*>(ps->rel.p), cnt);
+    hipLaunchKernelGGL(segment_classify_kernel, dim3((unsigned)dgrid), dim3(64 * kSegWaves), 0, st, t, d_text,
+                       n_bytes, d_doc_off, n_doc, static_cast<int32_t*>(ps->cand.p), ccnt,
+                       static_cast<int32_t*>(ps->rs_rel.p), cnt);
     LDDL_HIP(hipGetLastError());
   }
-  LDDL_HIP(scan_exclusive(CntAt{cnt}, n_doc, dso, static_cast<int64_t*>(ps->scratch.p), st));
+  LDDL_HIP(scan_exclusive(CntAt{ccnt}, n_doc, coff, scratch, st));
+  int64_t n_cand = 0;
+  LDDL_HIP(hipMemcpyAsync(&n_cand, coff + n_doc, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  LDDL_HIP(hipStreamSynchronize(st));
+  const size_t ncap = (size_t)std::max<int64_t>(n_cand, 1);
+  LDDL_HIP(A.take(sizeof(int64_t) * ncap, st, ps->fq));
+  LDDL_HIP(A.take(sizeof(int32_t) * ncap, st, ps->fdoc));
+  LDDL_HIP(A.take(sizeof(int64_t) * ncap, st, ps->fbound));
+  if (n_cand > 0) {
+    hipLaunchKernelGGL(segment_flatten_kernel, dim3((unsigned)dgrid), dim3(64 * kSegWaves), 0, st, d_doc_off,
+                       n_doc, static_cast<const int32_t*>(ps->cand.p), coff, static_cast<int64_t*>(ps->fq.p),
+                       static_cast<int32_t*>(ps->fdoc.p));
+    const int64_t egrid = (n_cand + kEvalBlock - 1) / kEvalBlock;
+    if (ps->n_rec)
+      hipLaunchKernelGGL(segment_eval_kernel<true>, dim3((unsigned)egrid), dim3(kEvalBlock), 0, st, t, d_text,
+                         n_bytes, d_doc_off, static_cast<const int32_t*>(ps->rs_rel.p),
+                         static_cast<const int64_t*>(ps->fq.p), static_cast<const int32_t*>(ps->fdoc.p), n_cand,
+                         static_cast<int64_t*>(ps->fbound.p), cnt);
+    else
+      hipLaunchKernelGGL(segment_eval_kernel<false>, dim3((unsigned)egrid), dim3(kEvalBlock), 0, st, t, d_text,
+                         n_bytes, d_doc_off, static_cast<const int32_t*>(ps->rs_rel.p),
+                         static_cast<const int64_t*>(ps->fq.p), static_cast<const int32_t*>(ps->fdoc.p), n_cand,
+                         static_cast<int64_t*>(ps->fbound.p), cnt);
+    LDDL_HIP(hipGetLastError());
+  }
+  LDDL_HIP(scan_exclusive(CntAt{cnt}, n_doc, dso, scratch, st));
   LDDL_HIP(hipMemcpyAsync(&ps->n_sent, dso + n_doc, sizeof(int64_t), hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
   ps->doc_off = d_doc_off;
@@ -746,8 +821,8 @@ extern "C" int lddl_segment_fill(lddl_ctx* c, void* stream, int64_t* d_sent_off,
   if (n_doc > 0) {
     const int64_t grid = (n_doc + 3) / 4;
     hipLaunchKernelGGL(segment_fill_kernel, dim3((unsigned)grid), dim3(256), 0, st, ps->doc_off, n_doc,
-                       static_cast<const int32_t*>(ps->rel.p), static_cast<const int64_t*>(ps->dso.p),
-                       d_sent_off);
+                       static_cast<const int64_t*>(ps->coff.p), static_cast<const int64_t*>(ps->fbound.p),
+                       static_cast<const int64_t*>(ps->dso.p), d_sent_off);
   } else {
     if (hipMemsetAsync(d_sent_off, 0, sizeof(int64_t), st) != hipSuccess) rc = -100;
   }
@@ -755,7 +830,7 @@ extern "C" int lddl_segment_fill(lddl_ctx* c, void* stream, int64_t* d_sent_off,
                      st) != hipSuccess)
     rc = -100;
   if (hipGetLastError() != hipSuccess) rc = -100;
-  for (DevArena::Block* b : {&ps->rel, &ps->cnt, &ps->dso, &ps->scratch}) {
+  for (DevArena::Block* b : ps->blocks()) {
     c->arena.give(*b, st);
     *b = DevArena::Block{};
   }
