@@ -100,12 +100,19 @@ __device__ __forceinline__ bool closing(uint32_t c) {
 }
 
 // Text bytes: the wave's LDS slab when the index falls inside it, else global memory.
+// (Explicit address spaces: a select between the two pointers would become flat loads, which
+// wait on both the vector-memory and the LDS counters.)
+typedef const __attribute__((address_space(3))) uint8_t* lds_u8_ptr;
+typedef const __attribute__((address_space(1))) uint8_t* glb_u8_ptr;
 struct Src {
-  const uint8_t* x;
-  const uint8_t* lds;
+  glb_u8_ptr x;
+  lds_u8_ptr lds;
   int64_t lo, hi;
+  __device__ Src(const uint8_t* gx, const void* l, int64_t lo_, int64_t hi_)
+      : x((glb_u8_ptr)gx), lds((lds_u8_ptr)l), lo(lo_), hi(hi_) {}
   __device__ __forceinline__ uint32_t operator[](int64_t i) const {
-    return (i >= lo && i < hi) ? (uint32_t)lds[i - lo] : (uint32_t)x[i];
+    if (i >= lo && i < hi) return lds[i - lo];
+    return x[i];
   }
 };
 
@@ -475,7 +482,7 @@ __global__ void __launch_bounds__(64 * kSegWaves) segment_classify_kernel(
   uint4* slab = slab_all[threadIdx.x >> 6];
   const int64_t b0 = doc_off[d], b1 = doc_off[d + 1];
   int32_t* out = cand + ((b0 - doc_off[0]) >> 1) + d;
-  const Src g{x, reinterpret_cast<const uint8_t*>(slab), 0, 0};  // global only
+  const Src g(x, slab, 0, 0);  // global only
   // rstrip end: one past the last non-whitespace byte
   int64_t rs = b0;
   for (int64_t we = b1; we > b0; we -= 64) {
@@ -493,35 +500,54 @@ __global__ void __launch_bounds__(64 * kSegWaves) segment_classify_kernel(
     const int64_t lo = blk & ~(int64_t)15;
     const int64_t hi = std::min<int64_t>(n_bytes, lo + kSlab);
     wave_sync();  // previous slab consumed
+    if (aligned && lo + kSlab <= n_bytes) {  // all loads in flight before the LDS writes
+      uint4 v[kSlab / 1024];
 #pragma unroll
-    for (int r = lane; r < kSlab / 16; r += 64) {
-      const int64_t a = lo + 16 * (int64_t)r;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (a + 16 <= hi && aligned) {
-        v = *reinterpret_cast<const uint4*>(x + a);
-      } else if (a < hi) {
+      for (int r = 0; r < kSlab / 1024; ++r)
+        v[r] = *reinterpret_cast<const uint4*>(x + lo + 16 * (int64_t)(lane + 64 * r));
+#pragma unroll
+      for (int r = 0; r < kSlab / 1024; ++r) slab[lane + 64 * r] = v[r];
+    } else {  // end of the text buffer / unaligned text: byte loads
+      for (int r = lane; r < kSlab / 16; r += 64) {
+        const int64_t a = lo + 16 * (int64_t)r;
         uint8_t tmp[16] = {};
         for (int k = 0; k < 16 && a + k < hi; ++k) tmp[k] = x[a + k];
+        uint4 v;
         memcpy(&v, tmp, 16);
+        slab[r] = v;
       }
-      slab[r] = v;
     }
     wave_sync();
-    const Src src{x, reinterpret_cast<const uint8_t*>(slab), lo, hi};
+    const Src src(x, slab, lo, hi);
     const int64_t bend = std::min<int64_t>(rs, hi);
-    for (int64_t base = blk; base < bend; base += 64) {
-      const int64_t i = base + lane;
-      bool q = false;
-      if (i < bend) {
-        const uint32_t c = src[i];
-        if (sent_end(c) && i + 1 < rs) {
-          const uint32_t cn = src[i + 1];
-          q = non_word(cn) || (cn < 0x80 ? ascii_space(cn) : space_at(t, src, i + 1, b0, b1));
+    const uint32_t* slab32 = reinterpret_cast<const uint32_t*>(slab);
+    // 256-byte windows, 4 bytes per lane (one LDS dword); a SWAR test skips words without
+    // '.', '?' or '!' (bytes before b0 -- first slab only -- are masked)
+    for (int64_t base = lo; base < bend; base += 256) {
+      const int64_t i0 = base + 4 * lane;
+      const uint32_t w = slab32[(i0 - lo) >> 2];
+      const uint32_t x1 = w ^ 0x2E2E2E2Eu, x2 = w ^ 0x3F3F3F3Fu, x3 = w ^ 0x21212121u;
+      const uint32_t maybe = ((x1 - 0x01010101u) & ~x1) | ((x2 - 0x01010101u) & ~x2) |
+                             ((x3 - 0x01010101u) & ~x3);
+      uint32_t qb = 0;
+      if (maybe & 0x80808080u) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t pos = i0 + k;
+          const uint32_t c = (w >> (8 * k)) & 255u;
+          if (pos < b0 || pos >= bend || !sent_end(c) || pos + 1 >= rs) continue;
+          const uint32_t cn = k < 3 ? (w >> (8 * k + 8)) & 255u : src[pos + 1];
+          if (non_word(cn) || (cn < 0x80 ? ascii_space(cn) : space_at(t, src, pos + 1, b0, b1)))
+            qb |= 1u << k;
         }
       }
-      const uint64_t qm = ballot(q);
-      if (q) out[nc + (int32_t)popc_below(qm)] = (int32_t)(i - b0);
-      nc += __builtin_popcountll(qm);
+      if (ballot(qb != 0)) {  // append this window's enders in position order
+        const int n = __builtin_popcount(qb);
+        const int incl = wave_incl_scan(n);
+        int slot = nc + incl - n;
+        for (uint32_t m = qb; m; m &= m - 1) out[slot++] = (int32_t)(i0 + __builtin_ctz(m) - b0);
+        nc += __shfl(incl, 63, 64);
+      }
     }
     blk = bend;
   }
@@ -591,7 +617,7 @@ __global__ void __launch_bounds__(kEvalBlock) segment_eval_kernel(
     row[4 * k + 2] = v[k].z;
     row[4 * k + 3] = v[k].w;
   }
-  const Src src{x, reinterpret_cast<const uint8_t*>(row), w0, w1};
+  const Src src(x, row, w0, w1);
   int64_t bound = -1;
   const bool cut = eval_candidate<kParams>(t, src, q, b0, b1, rs, &bound);
   fbound[c] = cut ? bound : -1;
