@@ -56,34 +56,41 @@ def make_batch(rank, args):
 
 
 def cpu_baseline(corp, part, seeds, args):
-    """The oracle (C restatement of the reference algorithm, one core) on a bounded sample of the
-    same workload: the first partitions of the batch, up to ~cpu_sample_bytes of text."""
-    from oracle import oracle as O
-    tok = O.Tokenizer(VOCAB, lowercase=True)
-    cls_id, sep_id, mask_id = (tok.token_id(t) for t in ('[CLS]', '[SEP]', '[MASK]'))
+    """The oracle (C restatement of the reference algorithm) on a bounded sample of the same
+    workload, one single-threaded process per host core used (the reference's
+    Dask/mpi4py pipeline runs one single-threaded worker per core): worker w takes its own run
+    of ~cpu_sample_bytes of consecutive partitions. value = all workers' output tokens / wall."""
+    import multiprocessing as mp
+    from oracle.cpu_worker import cpu_worker
+    n_proc = max(1, min(args.cpu_procs, os.cpu_count() or 1))
     doc_bytes = corp.sent_off[corp.doc_sent_off]
-    n_part = max(1, int(np.searchsorted(doc_bytes[part], args.cpu_sample_bytes)))
-    d1 = part[n_part]
-    s1 = corp.doc_sent_off[d1]
-    b1 = corp.sent_off[s1]
-    t0 = time.perf_counter()
-    ids, off = tok.tokenize(corp.text[:b1], corp.sent_off[:s1 + 1])
-    lens = np.diff(off)
-    keep = lens > 0  # drop empty sentences, then empty documents (pretrain.py:89-97)
-    k_off = np.concatenate([[0], np.cumsum(lens[keep])])  # ids is already compact
-    kept_pos = np.concatenate([[0], np.cumsum(keep)])
-    n_out = 0
-    for p in range(n_part):
-        kd = kept_pos[corp.doc_sent_off[part[p]:part[p + 1] + 1]]
-        kd = np.concatenate([kd[:1], kd[1:][np.diff(kd) > 0]])
-        out = O.partition_pairs(kd, k_off, ids, int(seeds[p]), 5, args.seq, True,
-                                tok.vocab_size, cls_id, sep_id, mask_id)
-        n_out += int(out['num_tokens'].sum())
-    dt = time.perf_counter() - t0
-    return {'value': n_out / dt, 'unit': 'output tokens/s', 'cores': 1, 'kind': 'port',
-            'sample': '{} partitions = {:.1f} MB of the same synthetic batch (tokenize + pairs + '
-                      'static masking, oracle/lddl_oracle.c, 1 thread), {:.1f} s'.format(
-                          n_part, b1 / 1e6, dt)}
+    jobs, p0 = [], 0
+    for _ in range(n_proc):
+        p1 = int(np.searchsorted(doc_bytes[part], doc_bytes[part[p0]] + args.cpu_sample_bytes))
+        p1 = min(max(p1, p0 + 1), len(part) - 1)
+        if p1 <= p0:
+            break
+        d0, d1 = part[p0], part[p1]
+        s0, s1 = corp.doc_sent_off[d0], corp.doc_sent_off[d1]
+        b0, b1 = corp.sent_off[s0], corp.sent_off[s1]
+        jobs.append((corp.text[b0:b1].copy(), corp.sent_off[s0:s1 + 1] - b0,
+                     corp.doc_sent_off[d0:d1 + 1] - s0, part[p0:p1 + 1] - d0, seeds[p0:p1].copy(),
+                     args.seq, VOCAB))
+        p0 = p1
+    with mp.get_context('spawn').Pool(len(jobs)) as pool:  # workers import numpy + oracle only
+        warm = [(j[0][:1 << 16], j[1][:2], j[2][:2], j[3][:1] * 0, j[4][:0], j[5], j[6])
+                for j in jobs]
+        pool.map(cpu_worker, warm, chunksize=1)  # imports and vocab load before the clock
+        t0 = time.perf_counter()
+        res = pool.map(cpu_worker, jobs)
+        wall = time.perf_counter() - t0
+    n_out = sum(r[0] for r in res)
+    mb = sum(len(j[0]) for j in jobs) / 1e6
+    return {'value': n_out / wall, 'unit': 'output tokens/s', 'cores': len(jobs), 'kind': 'port',
+            'sample': '{} single-threaded processes x ~{:.0f} MB of consecutive partitions = {:.1f} '
+                      'MB of the same synthetic batch (tokenize + pairs + static masking, '
+                      'oracle/lddl_oracle.c), {:.1f} s wall; host os.cpu_count() = {}'.format(
+                          len(jobs), args.cpu_sample_bytes / 1e6, mb, wall, os.cpu_count())}
 
 
 def timed_segmented(args, rank, world, ctx, dev):
@@ -165,6 +172,8 @@ def main():
     ap.add_argument('--seed', type=int, default=1234)
     ap.add_argument('--gen-threads', type=int, default=16)
     ap.add_argument('--cpu-sample-bytes', type=int, default=48 << 20)
+    ap.add_argument('--cpu-procs', type=int, default=16,
+                    help='CPU baseline processes (one per host core used; the GPU box grants 16)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-alt-rng', dest='alt_rng', action='store_false',
                     help='skip timing the other RNG mode (reported as alt_rng)')
