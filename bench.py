@@ -152,8 +152,18 @@ def timed_segmented(args, rank, world, ctx, dev):
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         dt, n_tok = float(t[0].item()), int(t[1].item())
     seg_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    # segmentation algorithmic bytes: text read once + document offsets read + sentence offsets
+    # and document sentence offsets written
+    n_doc = len(doc_off) - 1
+    seg_bytes = len(text) + 8 * (n_doc + 1) + 8 * (info['sentences'] + 1) + 8 * (n_doc + 1)
+    seg_gbs = seg_bytes / (seg_ms * 1e-3) / 1e9
     return {'value': n_tok / dt, 'unit': 'output tokens/s', 'ms_per_step': dt / args.steps * 1e3,
             'segment_ms': seg_ms, 'segment_text_gbs': len(text) / (seg_ms * 1e-3) / 1e9,
+            'roofline_segment': {'kernel': 'segment_classify + segment_eval + flatten + fill (HIP '
+                                            'events around lddl_segment_count/fill, 2 host syncs)',
+                                 'bound': 'hbm', 'achieved': seg_gbs, 'peak': HBM_PEAK_GBS,
+                                 'unit': 'GB/s', 'frac': seg_gbs / HBM_PEAK_GBS,
+                                 'algorithmic_bytes_per_launch': seg_bytes},
             'documents': int(len(doc_off) - 1), 'sentences': info['sentences'],
             'batch_bytes': int(len(text)),
             'note': 'input = raw document text; segment_ms includes the host sync for the '
