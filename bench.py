@@ -290,7 +290,7 @@ def main():
         alt = {'rng': other, 'value': atok / adt, 'ms_per_step': adt / args.steps * 1e3,
                'plan_ms': float(np.mean([x['plan_ms'] for x in astats]))}
     seg = None
-    if args.segmented_line:  # the same hot path from raw document text: GPU Punkt first
+    if args.segmented_line and world == 1:  # the same path from raw document text: Punkt first
         seg = timed_segmented(args, rank, world, ctx, dev)
     mem = torch.cuda.memory_stats()
     if rank != 0:
