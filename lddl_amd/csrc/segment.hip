@@ -466,11 +466,13 @@ __device__ inline bool eval_candidate(const PunktTab& t, const Src& src, int64_t
   return true;
 }
 
-// K1: one wavefront per document streams it through a 4-KB LDS slab (16 B per lane per load),
-// one byte per lane per 64-byte window, and appends every lookahead-qualified sentence ender
-// (text[q] in .?! and text[q+1] NonWord, or whitespace with non-whitespace later) in order to
-// the document's slot range cand[(doc_off[d] - doc_off[0]) / 2 + d ..] (a document of L bytes
-// has at most L/2 + 1 whitespace-free runs, the bound of both candidates and cuts).
+// K1: one wavefront per document streams it through a 4-KB LDS slab (four 16-B loads per lane
+// in flight), 4 bytes per lane per 256-byte window, and appends each whitespace-free run's match
+// -- its last lookahead-qualified sentence ender (text[q] in .?! and text[q+1] NonWord, or
+// whitespace with non-whitespace later) -- in order to the document's slot range
+// cand[(doc_off[d] - doc_off[0]) / 2 + d ..] (a document of L bytes has at most L/2 + 1
+// whitespace-free runs, the bound of both candidates and cuts: "?!?!?! x" has five qualified
+// enders in one run, so one per run is what keeps writes inside the range).
 __global__ void __launch_bounds__(64 * kSegWaves) segment_classify_kernel(
     PunktTab t, const uint8_t* __restrict__ x, int64_t n_bytes, const int64_t* __restrict__ doc_off,
     int64_t n_doc, int32_t* __restrict__ cand, int32_t* __restrict__ ccnt, int32_t* __restrict__ rs_rel,
@@ -537,8 +539,19 @@ __global__ void __launch_bounds__(64 * kSegWaves) segment_classify_kernel(
           const uint32_t c = (w >> (8 * k)) & 255u;
           if (pos < b0 || pos >= bend || !sent_end(c) || pos + 1 >= rs) continue;
           const uint32_t cn = k < 3 ? (w >> (8 * k + 8)) & 255u : src[pos + 1];
-          if (non_word(cn) || (cn < 0x80 ? ascii_space(cn) : space_at(t, src, pos + 1, b0, b1)))
+          if (non_word(cn)) {
+            // only the run's LAST qualified ender is a match (finditer): scan the rest of the
+            // run (rare). This also keeps the candidates within the per-document slot range.
+            bool last = true;
+            for (int64_t q = pos + 1; q < rs && last; ++q) {
+              if (space_at(t, src, q, b0, b1)) break;
+              if (sent_end(src[q]) && q + 1 < rs && (non_word(src[q + 1]) || space_at(t, src, q + 1, b0, b1)))
+                last = false;
+            }
+            if (last) qb |= 1u << k;
+          } else if (cn < 0x80 ? ascii_space(cn) : space_at(t, src, pos + 1, b0, b1)) {
             qb |= 1u << k;
+          }
         }
       }
       if (ballot(qb != 0)) {  // append this window's enders in position order

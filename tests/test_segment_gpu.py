@@ -75,6 +75,27 @@ def test_segment_synthetic_vs_oracle(ctx):
     assert got == reference_sentences(text, doc_off, st, en, cnt)
 
 
+def test_segment_dense_enders_vs_oracle(ctx):
+    """Runs of sentence enders (every byte a qualified ender: "?!?!?! x") and long runs that
+    cross the 4-KB slab and the 64-byte context windows; documents back to back, so a write
+    outside a document's candidate slots would corrupt its neighbour."""
+    from oracle import oracle as O
+    import random
+    rng = random.Random(5)
+    docs = ['?!' * 40 + ' x', '?' * 301 + ' Y', '.!?' * 50 + ') Z. ' + '!' * 7, 'a.)' * 100,
+            ('word' * 300 + '. Next. ') * 3, '"' * 70 + 'x.' + ')' * 70 + ' Y',
+            ' '.join('w{}?!'.format(i) for i in range(700)), 'x' * 5000 + '. A ' + 'b' * 4500 + '.']
+    docs += [''.join(rng.choice('?!.) "ab') for _ in range(rng.randint(1, 200))) for _ in range(300)]
+    enc = [d.encode() for d in docs]
+    doc_off = np.concatenate([[0], np.cumsum([len(e) for e in enc])]).astype(np.int64)
+    text = np.frombuffer(b''.join(enc), np.uint8)
+    got = gpu_sentences(ctx, text, doc_off)
+    st, en, cnt = O.Punkt().spans(text, doc_off)
+    exp = reference_sentences(text, doc_off, st, en, cnt)
+    bad = [d for d in range(len(exp)) if got[d] != exp[d]]
+    assert not bad, (bad[:5], [(got[d][:3], exp[d][:3]) for d in bad[:2]])
+
+
 def test_segment_empty_and_whitespace_documents(ctx):
     docs = ['', '   ', 'One. Two.', '　', 'x', 'End.) ', '']
     enc = [d.encode() for d in docs]
