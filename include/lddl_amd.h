@@ -91,7 +91,8 @@ int lddl_tokenize(lddl_ctx* ctx, void* stream, const uint8_t* d_text, int64_t n_
  *   records_bytes = 0 is the untrained PunktSentenceTokenizer(). Keys longer than 255 bytes are
  *   rejected. Must be called once before lddl_segment_count.
  * lddl_segment_count: documents d_text[d_doc_off[d] .. d_doc_off[d+1]) (the text after the
- *   document id, readers.py:131-136; documents contiguous); returns the sentence count
+ *   document id, readers.py:131-136; documents contiguous, each < 2 GiB, valid UTF-8, inside
+ *   [0, n_bytes)); returns the sentence count
  *   (synchronises the stream). Exactly one lddl_segment_fill must follow on the same ctx.
  * lddl_segment_fill -> d_sent_off[n_sent+1], d_doc_sent_off[n_doc+1]: sentence k of document d
  *   is d_text[sent_off[doc_sent_off[d]+k] .. sent_off[...+1]); it equals the reference's

@@ -93,6 +93,10 @@ def segment(ctx, text, doc_off):
     if not hasattr(ctx, '_punkt_params'):
         set_params(ctx)
     n_doc = doc_off.numel() - 1
+    if n_doc > 0:  # kernels index documents with int32 offsets and read text[doc_off[0]:doc_off[-1]]
+        lim = torch.stack([(doc_off[1:] - doc_off[:-1]).max(), doc_off[0], doc_off[-1]]).cpu()
+        if int(lim[0]) >= 1 << 31 or int(lim[1]) < 0 or int(lim[2]) > text.numel():
+            raise ValueError('documents must lie inside the text and be < 2 GiB each')
     n_sent = ctypes.c_int64()
     check(lib.lddl_segment_count(ctx._h, _stream(), _ptr(text), text.numel(), _ptr(doc_off), n_doc,
                                  ctypes.byref(n_sent)))
