@@ -112,8 +112,8 @@ def _write_source(root, n_docs=300, seed=11):
             f.write('\n'.join(chunk) + '\n\n')
 
 
-@pytest.mark.parametrize('binned', [False, True])
-def test_pretrain_cli_vs_oracle(tmp_path, binned):
+@pytest.mark.parametrize('binned,params', [(False, False), (True, False), (False, True)])
+def test_pretrain_cli_vs_oracle(tmp_path, binned, params):
     from lddl_amd import synth
     from lddl_amd.dask.bert import pretrain as P
     from oracle import oracle as O
@@ -125,6 +125,12 @@ def test_pretrain_cli_vs_oracle(tmp_path, binned):
             '--vocab-file', VOCAB_UNCASED, '--local-n-workers', '1', '--duplicate-factor', '2']
     if binned:
         argv += ['--bin-size', '32']
+    prm = None
+    if params:  # trained Punkt parameters through --punkt-params
+        prm_path = os.path.join(GOLDEN, 'punkt_params.json')
+        argv += ['--punkt-params', prm_path]
+        with open(prm_path) as f:
+            prm = json.load(f)
     args = P.attach_args().parse_args(argv)
     P.main(args)
     # CPU replay: the same host partitions, the oracle tokenizer + pair/mask replay
@@ -133,7 +139,7 @@ def test_pretrain_cli_vs_oracle(tmp_path, binned):
     tok = O.Tokenizer(VOCAB_UNCASED, lowercase=True)
     vocab = [l.rstrip('\n') for l in open(VOCAB_UNCASED, encoding='utf-8')]
     cls, sep, msk = (tok.token_id(t) for t in ('[CLS]', '[SEP]', '[MASK]'))
-    punkt = O.Punkt()  # the CLI segments on the GPU: nltk's untrained Punkt, exactly
+    punkt = O.Punkt(prm)  # the CLI segments on the GPU: nltk's Punkt (untrained or params)
     for p, lines in parts:
         _, dtext, doc_off, _ = P.build_doc_corpus([(p, lines)])
         st, en, cnt = punkt.spans(dtext, doc_off)
