@@ -473,7 +473,13 @@ __device__ inline bool eval_candidate(const PunktTab& t, const Src& src, int64_t
 // cand[(doc_off[d] - doc_off[0]) / 2 + d ..] (a document of L bytes has at most L/2 + 1
 // whitespace-free runs, the bound of both candidates and cuts: "?!?!?! x" has five qualified
 // enders in one run, so one per run is what keeps writes inside the range).
-__global__ void __launch_bounds__(64 * kSegWaves) segment_classify_kernel(
+// 6 waves per SIMD (<= 80 VGPRs): 5.8 ms per 2 GiB vs 6.1 at the compiler's 96 VGPRs / 5 waves
+// and 6.3 at 8 waves (64 VGPRs, spills) -- profiles/r01_v14_segment_variants.txt
+#ifndef LDDL_SEG_WPE
+#define LDDL_SEG_WPE 6
+#endif
+#define LDDL_SEG_ATTR __attribute__((amdgpu_waves_per_eu(LDDL_SEG_WPE)))
+__global__ void __launch_bounds__(64 * kSegWaves) LDDL_SEG_ATTR segment_classify_kernel(
     PunktTab t, const uint8_t* __restrict__ x, int64_t n_bytes, const int64_t* __restrict__ doc_off,
     int64_t n_doc, int32_t* __restrict__ cand, int32_t* __restrict__ ccnt, int32_t* __restrict__ rs_rel,
     int32_t* __restrict__ cnt) {
@@ -531,7 +537,7 @@ __global__ void __launch_bounds__(64 * kSegWaves) segment_classify_kernel(
       const uint32_t x1 = w ^ 0x2E2E2E2Eu, x2 = w ^ 0x3F3F3F3Fu, x3 = w ^ 0x21212121u;
       const uint32_t maybe = ((x1 - 0x01010101u) & ~x1) | ((x2 - 0x01010101u) & ~x2) |
                              ((x3 - 0x01010101u) & ~x3);
-      uint32_t qb = 0;
+      uint32_t qb = 0, nwb = 0;
       if (maybe & 0x80808080u) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -539,20 +545,24 @@ __global__ void __launch_bounds__(64 * kSegWaves) segment_classify_kernel(
           const uint32_t c = (w >> (8 * k)) & 255u;
           if (pos < b0 || pos >= bend || !sent_end(c) || pos + 1 >= rs) continue;
           const uint32_t cn = k < 3 ? (w >> (8 * k + 8)) & 255u : src[pos + 1];
-          if (non_word(cn)) {
-            // only the run's LAST qualified ender is a match (finditer): scan the rest of the
-            // run (rare). This also keeps the candidates within the per-document slot range.
-            bool last = true;
-            for (int64_t q = pos + 1; q < rs && last; ++q) {
-              if (space_at(t, src, q, b0, b1)) break;
-              if (sent_end(src[q]) && q + 1 < rs && (non_word(src[q + 1]) || space_at(t, src, q + 1, b0, b1)))
-                last = false;
-            }
-            if (last) qb |= 1u << k;
-          } else if (cn < 0x80 ? ascii_space(cn) : space_at(t, src, pos + 1, b0, b1)) {
+          if (non_word(cn))
+            nwb |= 1u << k;
+          else if (cn < 0x80 ? ascii_space(cn) : space_at(t, src, pos + 1, b0, b1))
             qb |= 1u << k;
-          }
         }
+      }
+      // a NonWord lookahead is a match only if it is the run's LAST qualified ender (finditer):
+      // scan the rest of the run (rare; kept out of the unrolled loop above so its registers do
+      // not cost occupancy). This also keeps the candidates within the per-document slot range.
+      for (uint32_t m = nwb; m; m &= m - 1) {
+        const int64_t pos = i0 + __builtin_ctz(m);
+        bool last = true;
+        for (int64_t q = pos + 1; q < rs && last; ++q) {
+          if (space_at(t, src, q, b0, b1)) break;
+          if (sent_end(src[q]) && q + 1 < rs && (non_word(src[q + 1]) || space_at(t, src, q + 1, b0, b1)))
+            last = false;
+        }
+        if (last) qb |= m & (~m + 1);
       }
       if (ballot(qb != 0)) {  // append this window's enders in position order
         const int n = __builtin_popcount(qb);
