@@ -175,7 +175,10 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--batch-bytes', type=int, default=4 << 30)
+    ap.add_argument('--batch-bytes', type=int, default=None,
+                    help='sentence text per GPU per step (default 6 GiB for c2, 4 GiB for c4: the '
+                         'replay planner runs one wave per partition, so 6144 partitions of 1 MiB '
+                         'fill the CUs better than 4096; c4 keeps 4 GiB for HBM headroom of the balance)')
     ap.add_argument('--partition-bytes', type=int, default=1 << 20)
     ap.add_argument('--seq', type=int, default=None)
     ap.add_argument('--workload', choices=['c2', 'c4'], default='c2')
@@ -195,6 +198,8 @@ def main():
     args = ap.parse_args()
     if args.seq is None:
         args.seq = 128 if args.workload == 'c2' else 512
+    if args.batch_bytes is None:
+        args.batch_bytes = (6 << 30) if args.workload == 'c2' else (4 << 30)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
