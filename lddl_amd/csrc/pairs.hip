@@ -999,11 +999,27 @@ __global__ void __launch_bounds__(64) apply_shuffle_kernel(const int64_t* kd_off
       for (int64_t k = lo + threadIdx.x; k <= hi; k += 64) s_js[k - lo] = (Idx)js[k];
       __syncthreads();
       if (threadIdx.x == 0) {
-        for (int64_t i = hi; i >= lo; --i) {
+        // the draws of 8 steps are read into registers first (s_js is not written here), so
+        // each swap waits on one LDS round trip (x[i], x[j] together) instead of two
+        int64_t i = hi;
+        for (; i - 7 >= lo; i -= 8) {
+          int32_t jr[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) jr[u] = (int32_t)s_js[i - u - lo];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const Idx t = s_ord[i - u];
+            const Idx v = s_ord[jr[u]];
+            s_ord[jr[u]] = t;
+            s_ord[i - u] = v;
+          }
+        }
+        for (; i >= lo; --i) {
           const int32_t j = (int32_t)s_js[i - lo];
           const Idx t = s_ord[i];
-          s_ord[i] = s_ord[j];
+          const Idx v = s_ord[j];
           s_ord[j] = t;
+          s_ord[i] = v;
         }
       }
     }
