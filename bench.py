@@ -125,7 +125,7 @@ def timed_segmented(args, rank, world, ctx, dev):
         if args.workload == 'c4':
             from lddl_amd.balance import balance
             bb = balance(ctx, pb, 8, args.seq // 8)
-            n = int(bb.tokens.numel()) + 3 * bb.n_rows
+            n = bb.n_tokens + 3 * bb.n_rows
             del bb
         else:
             n = int(pb.tokens.numel()) + 3 * pb.n_pairs
@@ -233,7 +233,7 @@ def main():
         del ids
         if args.workload == 'c4':
             bb = balance(ctx, pb, 8, args.seq // 8, timings=diag.get('balance'))
-            n_tok = int(bb.tokens.numel()) + 3 * bb.n_rows
+            n_tok = bb.n_tokens + 3 * bb.n_rows
             del bb
         else:
             n_tok = int(pb.tokens.numel()) + 3 * pb.n_pairs

@@ -100,6 +100,8 @@ int lddl_tokenize(lddl_ctx* ctx, void* stream, const uint8_t* d_text, int64_t n_
  *   between sentences is attached to the left one, which the BERT tokenizer ignores), and a
  *   whitespace-only sentence stands for the reference's dropped empty string (0 pieces, dropped
  *   by the pair builder exactly like pretrain.py:92-97). The output feeds lddl_tokenize.
+ *   Both outputs NULL cancels the pending segmentation (releases its scratch; the host calls it
+ *   when something fails between count and fill).
  * ------------------------------------------------------------------------------------------- */
 int lddl_punkt_set_params(lddl_ctx* ctx, const uint8_t* table, int64_t table_bytes,
                           const uint8_t* records, int64_t records_bytes);
@@ -207,6 +209,8 @@ int lddl_scan_i64(void* stream, const int64_t* d_in, int64_t n, int64_t* d_out);
  *   token_type_ids, attention_mask, and either special_tokens_mask (dynamic masking) or labels
  *   (static: d_lab_bytes/d_lab_off = masked_lm_labels strings, d_pos/d_pos_off = decoded
  *   masked_lm_positions; unmasked slots = ignore_index). Unused outputs may be NULL.
+ *   Token and label writes at positions >= seq_len are dropped (the host refuses such a batch
+ *   with IndexError before launching, as the reference's tensor indexing does).
  * ------------------------------------------------------------------------------------------- */
 int lddl_collate_encode(lddl_ctx* ctx, void* stream, const uint8_t* d_bytes, const int64_t* d_a_off,
                         const int64_t* d_b_off, const int32_t* d_na, const int32_t* d_nb,
@@ -219,7 +223,10 @@ int lddl_collate_encode(lddl_ctx* ctx, void* stream, const uint8_t* d_bytes, con
 /* ---------------------------------------------------------------------------------------------
  * Dynamic masking (lddl/torch/bert.py:152-196 `_mask_tokens`) in place on d_input_ids
  * [batch, seq_len] int64; writes d_labels. Special slots come from d_special_tokens_mask, or,
- * if NULL, from the lengths (positions 0, na+1 and >= na+nb+2, as _to_encoded_inputs sets them).
+ * if NULL, from the lengths (positions 0, na+1 and >= na+nb+2, as _to_encoded_inputs sets them),
+ * or, if the lengths are NULL too, from the ids: a slot is special iff its id is one of
+ * [PAD] [UNK] [CLS] [SEP] [MASK] (`special_tokens_mask=None`, i.e.
+ * tokenizer.get_special_tokens_mask(ids, already_has_special_tokens=True), bert.py:167-172).
  * Native mode: Philox4x32-10 keyed by (seed, counter) — call with a fresh counter per batch.
  * Replay mode (all four d_r_* non-NULL): apply captured torch draws (masked_indices,
  * indices_replaced, indices_random as uint8, random_words int64) bit for bit.

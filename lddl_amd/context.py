@@ -76,18 +76,65 @@ class Context:
     def __len__(self):
         return self.vocab_size
 
+    # ---- the tokenizer duck-type the reference's hot path uses -----------------
+    # pretrain.py:79-80, 384; lddl/torch/bert.py:111, 123, 169-171, 185-186, 191
+    mask_token = '[MASK]'
+    cls_token = '[CLS]'
+    sep_token = '[SEP]'
+    pad_token = '[PAD]'
+    unk_token = '[UNK]'
+
+    @property
+    def all_special_tokens(self):
+        return [t for t in ('[UNK]', '[SEP]', '[PAD]', '[CLS]', '[MASK]') if self.special_ids[t] >= 0]
+
+    @property
+    def all_special_ids(self):
+        return [self.special_ids[t] for t in self.all_special_tokens]
+
     def convert_tokens_to_ids(self, tokens):
+        """A token -> its id, a list of tokens -> list of ids ([UNK] for unknown tokens)."""
         unk = self.special_ids['[UNK]']
+        if isinstance(tokens, str):
+            return self.vocab.get(tokens, unk)
         return [self.vocab.get(t, unk) for t in tokens]
 
-    # ------------------------------------------------------------------------------------------
-    def tokenize(self, text, sent_off, max_pieces=512):
-        """WordPiece-tokenize device-resident sentences.
+    def convert_ids_to_tokens(self, ids):
+        if isinstance(ids, int):
+            return self.tokens[ids]
+        return [self.tokens[int(i)] for i in ids]
 
-        text: uint8 cuda tensor; sent_off: int64 cuda tensor [n_sent+1].
+    def get_special_tokens_mask(self, token_ids_0, token_ids_1=None,
+                                already_has_special_tokens=False):
+        """BertTokenizerFast.get_special_tokens_mask: with already_has_special_tokens, 1 for
+        every id in all_special_ids; else the [CLS] A [SEP] (B [SEP]) layout."""
+        if already_has_special_tokens:
+            if token_ids_1 is not None:
+                raise ValueError('You should not supply a second sequence if the provided '
+                                 'sequence of ids is already formatted with special tokens '
+                                 'for the model.')
+            sp = set(self.all_special_ids)
+            return [1 if int(t) in sp else 0 for t in token_ids_0]
+        out = [1] + [0] * len(token_ids_0) + [1]
+        if token_ids_1 is not None:
+            out += [0] * len(token_ids_1) + [1]
+        return out
+
+    # ------------------------------------------------------------------------------------------
+    def tokenize(self, text, sent_off=None, max_pieces=512, max_length=None, truncation=False):
+        """Two forms.
+
+        tokenize(str, max_length=None, truncation=False) -> list of WordPiece strings: the
+        reference's per-sentence call `tokenizer.tokenize(s, max_length=512, truncation=True)`
+        (pretrain.py:79-80), as a host convenience over the same GPU kernel.
+
+        tokenize(text, sent_off, max_pieces=512): WordPiece-tokenize device-resident sentences
+        (the product path). text: uint8 cuda tensor; sent_off: int64 cuda tensor [n_sent+1].
         Returns (ids int32[n_bytes], sent_len int32[n_sent]): sentence s's pieces are
         ids[sent_off[s] : sent_off[s] + (sent_len[s] & LEN_MASK)].
         """
+        if isinstance(text, str):
+            return self._tokenize_str(text, max_length if truncation and max_length else None)
         assert text.dtype == torch.uint8 and text.is_cuda and sent_off.dtype == torch.int64
         n_sent = sent_off.numel() - 1
         ids = torch.empty(max(text.numel(), 1), dtype=torch.int32, device=self.device)
@@ -95,6 +142,14 @@ class Context:
         check(lib.lddl_tokenize(self._h, _stream(), _ptr(text), text.numel(), _ptr(sent_off),
                                 n_sent, max_pieces, _ptr(ids), _ptr(sent_len)))
         return ids, sent_len
+
+    def _tokenize_str(self, s, max_length=None):
+        b = np.array(bytearray(s.encode('utf-8')), np.uint8)
+        if len(b) == 0:
+            return []
+        cap = min(len(b), 1 << 24) if max_length is None else int(max_length)
+        ids, off = self.tokenize_host(b, np.asarray([0, len(b)], np.int64), cap)
+        return [self.tokens[i] for i in ids[off[0]:off[1]]]
 
     def tokenize_host(self, text, sent_off, max_pieces=512):
         """Convenience: numpy in, ragged numpy (ids, offsets) out."""

@@ -51,7 +51,8 @@ __device__ inline bool is_ws(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13)
 // Split bytes[b0,b1) on whitespace and look every token up; token t -> out[t] (t < max_tok).
 // Whole wave cooperates: 64-byte windows, word starts found by ballot. Returns #tokens.
 __device__ int32_t split_lookup(const Tables& T, const uint8_t* bytes, int64_t b0, int64_t b1,
-                                int32_t* out, int32_t max_tok, const uint16_t* scatter) {
+                                int32_t* out, int32_t max_tok, const uint16_t* scatter,
+                                int32_t limit) {
   const int lane = lane_id();
   int32_t ntok = 0;
   uint8_t prev = ' ';
@@ -68,7 +69,10 @@ __device__ int32_t split_lookup(const Tables& T, const uint8_t* bytes, int64_t b
       while (e < b1 && !is_ws(bytes[e])) ++e;
       int32_t id = token_lookup(T, bytes + i, (int)(e - i));
       if (id < 0) id = T.special_id[kUnk];
-      if (t < max_tok) out[scatter ? scatter[t] : t] = id;
+      if (t < max_tok) {
+        const int32_t dst = scatter ? (int32_t)scatter[t] : t;
+        if (dst < limit) out[dst] = id;  // a masked position >= L is refused on the host
+      }
     }
     ntok += __popcll(m);
     prev = (uint8_t)__shfl((int)c, 63, 64);
@@ -121,12 +125,12 @@ __global__ void __launch_bounds__(64 * kEncWaves) encode_kernel(EncodeArgs E) {
   }
   __syncthreads();
   if (active) {
-    split_lookup(E.T, E.bytes, E.a_off[b], E.a_off[b + 1], sid + 1, na, nullptr);
-    split_lookup(E.T, E.bytes, E.b_off[b], E.b_off[b + 1], sid + na + 2, nb, nullptr);
+    split_lookup(E.T, E.bytes, E.a_off[b], E.a_off[b + 1], sid + 1, na, nullptr, E.L);
+    split_lookup(E.T, E.bytes, E.b_off[b], E.b_off[b + 1], sid + na + 2, nb, nullptr, E.L);
     if (E.labels && E.lab_bytes) {  // labels[b, positions] = ids of masked_lm_labels (bert.py:120-125)
       const int64_t p0 = E.pos_off[b];
       split_lookup(E.T, E.lab_bytes, E.lab_off[b], E.lab_off[b + 1], slab,
-                   (int32_t)(E.pos_off[b + 1] - p0), E.pos + p0);
+                   (int32_t)(E.pos_off[b + 1] - p0), E.pos + p0, E.L);
     }
   }
   __syncthreads();
@@ -145,12 +149,14 @@ __global__ void __launch_bounds__(64 * kEncWaves) encode_kernel(EncodeArgs E) {
 struct MaskArgs {
   int64_t* ids;        // [B, L] in/out
   int64_t* labels;     // [B, L] out
-  const int64_t* special;  // [B, L] special_tokens_mask (nullable -> derived from na/nb)
+  const int64_t* special;  // [B, L] special_tokens_mask (nullable -> derived from na/nb, or
+                           // without lengths from the ids: get_special_tokens_mask)
   const int32_t* na;
   const int32_t* nb;
   int64_t B, L;
   float p;
   int64_t ignore_index, mask_id, vocab_len;
+  int32_t special_ids[kNumSpecial];  // [PAD] [UNK] [CLS] [SEP] [MASK] (-1 if absent)
   uint64_t seed, counter;
   // replay (all or none)
   const uint8_t* r_masked;
@@ -163,13 +169,16 @@ __global__ void __launch_bounds__(256) mask_kernel(MaskArgs M) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= M.B * M.L) return;
   const int64_t b = i / M.L, x = i - b * M.L;
+  const int64_t id = M.ids[i];
   bool special;
   if (M.special) special = M.special[i] != 0;
-  else {
+  else if (M.na) {
     const int32_t na = M.na[b], end = na + M.nb[b] + 3;
     special = x == 0 || x == na + 1 || x >= end - 1;
+  } else {  // tokenizer.get_special_tokens_mask(ids, already_has_special_tokens=True)
+    special = false;
+    for (int k = 0; k < kNumSpecial; ++k) special |= M.special_ids[k] >= 0 && id == M.special_ids[k];
   }
-  const int64_t id = M.ids[i];
   bool masked, replaced, rnd;
   int64_t word;
   if (M.r_masked) {
@@ -227,13 +236,14 @@ extern "C" int lddl_mask_dynamic(lddl_ctx* c, void* stream, int64_t* d_input_ids
                                  const uint8_t* d_r_replaced, const uint8_t* d_r_random,
                                  const int64_t* d_r_words) {
   if (!c) LDDL_FAIL(-1, "null ctx");
-  if (!d_special_tokens_mask && (!d_na || !d_nb)) LDDL_FAIL(-1, "need special mask or lengths");
+  if (!d_special_tokens_mask && (!d_na != !d_nb)) LDDL_FAIL(-1, "need both lengths or neither");
   if (c->tab.special_id[kMask] < 0) LDDL_FAIL(-1, "vocab has no [MASK]");
   const int64_t n = batch * seq_len;
   if (n <= 0) return 0;
   MaskArgs M{d_input_ids, d_labels, d_special_tokens_mask, d_na, d_nb, batch, seq_len,
-             mlm_probability, ignore_index, c->tab.special_id[kMask], vocab_len, seed, counter,
+             mlm_probability, ignore_index, c->tab.special_id[kMask], vocab_len, {}, seed, counter,
              d_r_masked, d_r_replaced, d_r_random, d_r_words};
+  for (int k = 0; k < kNumSpecial; ++k) M.special_ids[k] = c->tab.special_id[k];
   hipLaunchKernelGGL(mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      as_stream(stream), M);
   LDDL_HIP(hipGetLastError());

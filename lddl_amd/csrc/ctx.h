@@ -97,6 +97,7 @@ struct lddl_ctx {
   int64_t* d_render_off = nullptr;  // token i = d_render[off[i] .. off[i+1])
   uint32_t* d_bloom = nullptr;
   int32_t vocab_size = 0;
+  size_t lds_per_block = 0;         // hipDeviceAttributeMaxSharedMemoryPerBlock of `device`
   std::vector<std::string> tokens;  // host copy of the vocab lines
   lddl::DevArena arena;             // per-call temporaries (pair plans)
   void* punkt = nullptr;            // lddl_punkt_state (segment.hip), created by lddl_punkt_set_params

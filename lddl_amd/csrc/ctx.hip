@@ -48,6 +48,11 @@ extern "C" int lddl_ctx_create(int device, const uint8_t* norm_table, int64_t ta
   }
   auto* c = new lddl_ctx();
   c->device = device;
+  {
+    int lds = 0;
+    if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess)
+      c->lds_per_block = (size_t)lds;
+  }
 
   // vocab.txt: one token per line, id = line number (BertTokenizerFast / WordPiece.from_file)
   std::string cur;

@@ -1727,7 +1727,10 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     LDDL_HIP(hipStreamSynchronize(st));
     int64_t cap = 1;
     for (int64_t v : h_np) cap = std::max(cap, v);
-    const size_t kLdsBudget = 150 * 1024;
+    // dynamic-LDS budget of the swap kernel: what the device grants a block (160 KiB on
+    // gfx950), minus headroom for the kernel's static LDS
+    const size_t kLdsBudget = std::min<size_t>(150 * 1024, c->lds_per_block > 10 * 1024
+                                                               ? c->lds_per_block - 10 * 1024 : 0);
     if (cap <= 65536 && 2 * (size_t)(cap + kShufStage) <= kLdsBudget)
       hipLaunchKernelGGL(apply_shuffle_kernel<uint16_t>, dim3((unsigned)n_part), dim3(64),
                          2 * (size_t)(cap + kShufStage), st, P->kd_off, P->kp_off, prm->dup,

@@ -865,6 +865,15 @@ extern "C" int lddl_segment_fill(lddl_ctx* c, void* stream, int64_t* d_sent_off,
   lddl_punkt_state* ps = punkt_of(c);
   if (!ps || ps->n_doc < 0) LDDL_FAIL(-1, "no pending segmentation (lddl_segment_count)");
   hipStream_t st = as_stream(stream);
+  if (!d_sent_off && !d_doc_sent_off) {  // cancel: release the pending segmentation's scratch
+    for (DevArena::Block* b : ps->blocks()) {
+      c->arena.give(*b, st);
+      *b = DevArena::Block{};
+    }
+    ps->n_doc = -1;
+    return 0;
+  }
+  if (!d_sent_off || !d_doc_sent_off) LDDL_FAIL(-1, "lddl_segment_fill: null output");
   const int64_t n_doc = ps->n_doc;
   int rc = 0;
   if (n_doc > 0) {

@@ -2,28 +2,40 @@
 (lddl/dask/bert/pretrain.py:563-884): same flags, same output layout, GPU data plane.
 
 Pipeline (reference call stack in SURVEY.md §3.1):
-  read `*.txt` sources into blocks (readers.py)            -> lddl_amd.dask.readers (host)
-  random shuffle of documents over partitions (100-111)    -> seeded permutation (host; the
-                                                              reference's is unseeded)
+  read `*.txt` sources into blocks (readers.py)            -> lddl_amd.dask.readers (host; each
+                                                              rank reads only its own blocks)
+  random shuffle of documents over partitions (100-111)    -> seeded shuffle of the documents of
+                                                              each GPU batch of partitions (host;
+                                                              the reference's is global and
+                                                              unseeded)
   split_id_text (readers.py:131-136)                       -> host, per line
-  sent_tokenize + strip + drop empty (86-88)               -> lddl_segment_* (HIP Punkt; host
-                                                              segment.py with --sentence-splitter host)
+  sent_tokenize + strip + drop empty (86-88)               -> lddl_segment_* (HIP Punkt; nltk on
+                                                              the host with --sentence-splitter host)
   tokenizer.tokenize(s, max_length=512, truncation=True)   -> lddl_tokenize (HIP)
   _to_partition_pairs / create_pairs_from_document /
     create_masked_lm_predictions (386-402, 241-365, 182-238) -> lddl_pairs_plan / emit (HIP)
   _to_dataframe_binned (binning.py:63-93)                  -> lddl_bin_partitions (HIP)
   instance dict + serialize_np_array (345-358)             -> lddl_render_* (HIP)
-  to_parquet / write_partition_binned                      -> pyarrow writer (host)
+  to_parquet / write_partition_binned + _metadata          -> pyarrow writer (host)
 
 Random state: the reference draws from each Dask worker's unseeded global `random` (H1). Here
 partition p is processed as if `random.seed(partition_seed(--seed, p))` had been called before
 its `_to_partition_pairs`, which the test-suite replays bit for bit on the CPU.
 
-Multi-GPU (`--schedule mpi`, launched with torchrun): rank r owns partitions p with
-p % world_size == r (partitions are independent); there is no data-path collective.
+Multi-GPU (`--schedule mpi`, launched with torchrun, one process per GPU): rank r owns the
+partitions p with p % world_size == r (partitions are independent) and reads only
+those blocks.
+
+`--num-shards S` (lddl_amd; the reference runs `balance_dask_output` as a second job over the
+files): the pair tables stay in HBM, are binned per rank and balanced across ranks in one pass
+(lddl_amd/balance.py: RCCL all-gather of the per-bin counts, all-to-all-v of the rows that
+change rank), and the output is the balancer's layout directly: `shard-<k>.parquet_<b>` (or
+`shard-<k>.parquet` unbinned) with N or N+1 samples per bin, plus `.num_samples.json`
+(lddl/dask/load_balance.py:90-92, 372-378) — what get_bert_pretrain_data_loader consumes.
 """
 import argparse
 import functools
+import json
 import os
 import random
 import sys
@@ -53,33 +65,57 @@ def _resolve_vocab(vocab_file):
         'a vocab.txt path (e.g. {}/vocab_synth_uncased_30522.txt)'.format(vocab_file, ASSETS))
 
 
-def get_partitions(args, rank=0, world=1):
-    """Partitions (lists of raw document lines) owned by `rank`, after sampling and the shuffle."""
+def plan_partitions(args):
+    """Every partition of the corpus as an unread readers.Block, in the reference's partition
+    order (wikipedia, books, common crawl; db.concat, pretrain.py:412-438)."""
     blocksize = args.block_size
     if args.num_blocks is not None:
         if blocksize is not None:
             raise ValueError('Only one of num_blocks or blocksize needs to be set!')
         blocksize = readers.estimate_block_size((args.wikipedia, args.books, args.common_crawl),
                                                 args.num_blocks)
-    parts = []
+    blocks = []
     if args.wikipedia is not None:
-        parts += readers.read_wikipedia(args.wikipedia, args.wikipedia_lang, blocksize,
-                                        args.sample_ratio, args.seed)
+        blocks += readers.plan_blocks(readers.wikipedia_dir(args.wikipedia, args.wikipedia_lang),
+                                      blocksize, args.sample_ratio, args.seed)
     if args.books is not None:
-        parts += readers.read_books(args.books, blocksize, args.sample_ratio, args.seed)
+        blocks += readers.plan_blocks(args.books, blocksize, args.sample_ratio, args.seed)
     if args.common_crawl is not None:
-        parts += readers.read_common_crawl(args.common_crawl, blocksize, args.sample_ratio,
-                                           args.seed)
-    mine = [p for p in range(len(parts)) if p % world == rank]
-    # shuffle documents over this rank's partitions, keeping each partition's document count
-    docs = [d for p in mine for d in parts[p]]
-    random.Random(partition_seed(args.seed, -1 - rank)).shuffle(docs)
-    out, k = [], 0
+        blocks += readers.plan_blocks(args.common_crawl, blocksize, args.sample_ratio, args.seed)
+    return blocks
+
+
+def iter_batches(args, rank=0, world=1, blocks=None):
+    """This rank's partitions in GPU batches of <= --gpu-batch-bytes of input, read lazily:
+    yields [(p, lines)] per batch, the documents shuffled over the batch's partitions (each keeps
+    its document count) by Random(partition_seed(seed, -1 - first partition of the batch))."""
+    blocks = plan_partitions(args) if blocks is None else blocks
+    mine = [p for p in range(len(blocks)) if p % world == rank]
+    cur, size = [], 0
+    groups = []
     for p in mine:
-        n = len(parts[p])
-        out.append((p, docs[k:k + n]))
-        k += n
-    return out
+        b = blocks[p].nbytes
+        if cur and size + b > args.gpu_batch_bytes:
+            groups.append(cur)
+            cur, size = [], 0
+        cur.append(p)
+        size += b
+    if cur:
+        groups.append(cur)
+    for g in groups:
+        parts = [(p, readers.read_block(blocks[p])) for p in g]
+        docs = [d for _, lines in parts for d in lines]
+        random.Random(partition_seed(args.seed, -1 - g[0])).shuffle(docs)
+        out, k = [], 0
+        for p, lines in parts:
+            out.append((p, docs[k:k + len(lines)]))
+            k += len(lines)
+        yield out
+
+
+def get_partitions(args, rank=0, world=1):
+    """Partitions (lists of raw document lines) owned by `rank`, after sampling and the shuffle."""
+    return [pl for batch in iter_batches(args, rank, world) for pl in batch]
 
 
 def _segment_docs(lines):
@@ -92,7 +128,7 @@ def _segment_docs(lines):
 
 def build_corpus(partitions, workers=1):
     """Flatten partitions into the device corpus layout: text bytes, sentence byte offsets,
-    document sentence offsets, partition document offsets."""
+    document sentence offsets, partition document offsets (host segmentation)."""
     flat = [lines for _, lines in partitions]
     if workers > 1 and sum(len(x) for x in flat) > 2000:
         from multiprocessing import get_context
@@ -148,34 +184,49 @@ def punkt_params(args):
         return PunktParams()
 
 
-def process_batch(ctx, args, partitions, corpus, outdir):
-    """Run the GPU hot path over a group of partitions and write their files."""
+def make_batch_pairs(ctx, args, partitions, corpus, timer=None):
+    """The GPU hot path over one batch of partitions -> PairBatch (pairs in partition order)."""
     import torch
     from ...pairs import make_pairs
-    from ... import output
     dev = ctx.device
+    tm = timer or (lambda name: None)
     if corpus[0] == 'documents':  # GPU Punkt: sentences of every document of the batch
         from ... import punkt
         _, text, doc_off, part_doc_off = corpus
         d_text = torch.from_numpy(text).to(dev) if len(text) else torch.zeros(
             1, dtype=torch.uint8, device=dev)[:0]
-        d_so, d_dso = punkt.segment(ctx, d_text, torch.from_numpy(doc_off).to(dev))
+        d_doc = torch.from_numpy(doc_off).to(dev)
+        tm('h2d')
+        d_so, d_dso = punkt.segment(ctx, d_text, d_doc)
+        tm('segment')
     else:
         _, text, sent_off, doc_sent_off, part_doc_off = corpus
         d_text = torch.from_numpy(text).to(dev) if len(text) else torch.zeros(
             1, dtype=torch.uint8, device=dev)[:0]
         d_so = torch.from_numpy(sent_off).to(dev)
         d_dso = torch.from_numpy(doc_sent_off).to(dev)
+        tm('h2d')
     ids, sent_len = ctx.tokenize(d_text, d_so, max_pieces=512)
+    tm('tokenize')
     seeds = np.asarray([partition_seed(args.seed, p) for p, _ in partitions], np.int64)
     pb = make_pairs(ctx, d_so, ids, sent_len, d_dso,
                     torch.from_numpy(part_doc_off).to(dev), torch.from_numpy(seeds).to(dev),
                     seq=args.target_seq_length, dup=args.duplicate_factor, masking=args.masking,
                     short_seq_prob=args.short_seq_prob, masked_lm_ratio=args.masked_lm_ratio,
                     rng=getattr(args, 'rng', 'replay'), native_seed=args.seed)
+    tm('pairs')
+    return pb
+
+
+def process_batch(ctx, args, partitions, corpus, outdir, timer=None):
+    """Run the GPU hot path over a group of partitions and write their files."""
+    from ... import output
+    tm = timer or (lambda name: None)
+    pb = make_batch_pairs(ctx, args, partitions, corpus, timer)
     part_rows = pb.part_off.cpu().numpy()
     index = [p for p, _ in partitions]
     if args.bin_size is not None:
+        import torch
         nbins = args.target_seq_length // args.bin_size
         nt = ((pb.tok_off[1:] - pb.tok_off[:-1]) + 3).to(torch.int32)
         perm, bin_id, counts = output.bin_partitions(ctx, nt, pb.part_off, args.bin_size, nbins)
@@ -184,9 +235,14 @@ def process_batch(ctx, args, partitions, corpus, outdir):
     else:
         nbins, counts = None, None
         rd = output.render(ctx, pb)
+    tm('render')
     if args.output_format == 'parquet':
-        return output.write_parquet(outdir, rd, part_rows, index, args.masking, nbins, counts)
-    return write_txt(outdir, rd, part_rows, index, args.masking, nbins, counts)
+        paths = output.write_parquet(outdir, rd, part_rows, index, args.masking, nbins, counts)
+    else:
+        paths = write_txt(outdir, rd, part_rows, index, args.masking, nbins, counts,
+                          getattr(args, 'n_partitions', len(part_rows) - 1))
+    tm('write')
+    return paths
 
 
 def _txt_line(row, masking):
@@ -202,9 +258,20 @@ def _txt_line(row, masking):
         row['is_random_next'], row['A'], row['B'], row['num_tokens'])
 
 
-def write_txt(outdir, rd, part_rows, index, masking, nbins, counts):
-    """Debug output (`--output-format txt`): dask's to_textfiles names partition i `<i>.txt`;
-    the binned writer (binning.py:439-509) adds `_<bin>`."""
+def _pad_name(n):
+    """fsspec build_name_function(n - 1) (dask to_textfiles' default names): zero-padded to the
+    width of the largest partition index."""
+    import math
+    w = int(math.ceil(math.log10(max(n - 1, 0) + 1e-8)))
+    return lambda i: str(i).zfill(w)
+
+
+def write_txt(outdir, rd, part_rows, index, masking, nbins, counts, n_part):
+    """Debug output (`--output-format txt`, pretrain.py:501-531): dask's to_textfiles writes
+    partition i to `<i>.txt` (i zero-padded to the width of n_part - 1); the binned writer
+    (binning.py:439-509) names (i, b) `<i>_<b>.txt` and creates every bin's file. Lines are
+    joined by '\n' without a trailing newline (last_endline=False)."""
+    name = _pad_name(n_part)
     paths = []
     for p in range(len(part_rows) - 1):
         r0, r1 = int(part_rows[p]), int(part_rows[p + 1])
@@ -215,26 +282,69 @@ def write_txt(outdir, rd, part_rows, index, masking, nbins, counts):
                 spans.append((b, b0, b0 + int(counts[p, b])))
                 b0 += int(counts[p, b])
         for b, a, z in spans:
-            fn = os.path.join(outdir, '{}.txt'.format(index[p]) if b is None else
-                              '{}.txt_{}'.format(index[p], b))
+            fn = os.path.join(outdir, '{}.txt'.format(name(index[p])) if b is None else
+                              '{}_{}.txt'.format(index[p], b))
             with open(fn, 'w') as f:
-                for r in range(a, z):
-                    f.write(_txt_line(rd.row(r), masking) + '\n')
+                f.write('\n'.join(_txt_line(rd.row(r), masking) for r in range(a, z)))
             paths.append(fn)
     return paths
 
 
-def _batches(partitions, max_bytes):
-    cur, size = [], 0
-    for p, lines in partitions:
-        b = sum(len(x) for x in lines)
-        if cur and size + b > max_bytes:
-            yield cur
-            cur, size = [], 0
-        cur.append((p, lines))
-        size += b
-    if cur:
-        yield cur
+def write_balanced(ctx, args, bb, outdir, binned):
+    """This rank's balanced shards: `shard-<k>.parquet_<b>` per bin (binned) or
+    `shard-<k>.parquet`, the load balancer's names (load_balance.py:90-92)."""
+    import torch
+    from ... import output
+    dev = ctx.device
+    nbins = len(bb.bin_off) - 1
+    paths = []
+    for m, s in enumerate(bb.shards):
+        idx, bins = bb.shard_rows(m)
+        rows = torch.from_numpy(idx).to(dev)
+        if bb.rows is not None:
+            rows = bb.rows.index_select(0, rows)
+        rd = output.render(ctx, bb.table, rows, torch.from_numpy(bins).to(dev) if binned else None)
+        r0 = 0
+        for b in range(nbins):
+            r1 = r0 + int(bb.shard_counts[m, b])
+            fn = os.path.join(outdir, 'shard-{}.parquet{}'.format(s, '_{}'.format(b) if binned
+                                                                 else ''))
+            output.write_table(rd, r0, r1, args.masking, binned, fn)
+            paths.append(fn)
+            r0 = r1
+    return paths
+
+
+def num_samples_of_shards(bb, binned):
+    """`.num_samples.json` content of the balanced layout (load_balance.py:372-378)."""
+    out = {}
+    S, B = bb.all_shard_counts.shape
+    for b in range(B):
+        for s in range(S):
+            out['shard-{}.parquet{}'.format(s, '_{}'.format(b) if binned else '')] = int(
+                bb.all_shard_counts[s, b])
+    return out
+
+
+class _StageTimer:
+    """Cumulative wall time per stage (device-synchronised), printed at the end of main."""
+
+    def __init__(self, enabled):
+        self.enabled, self.t, self.acc = enabled, None, {}
+
+    def __call__(self, name):
+        if not self.enabled:
+            return
+        import torch
+        torch.cuda.synchronize()
+        now = time.perf_counter()
+        if self.t is not None:
+            self.acc[name] = self.acc.get(name, 0.0) + now - self.t
+        self.t = now
+
+    def mark(self):
+        if self.enabled:
+            self.t = time.perf_counter()
 
 
 def main(args):
@@ -246,36 +356,84 @@ def main(args):
                              'sequence length.')
     if args.output_format not in ('parquet', 'txt'):
         raise ValueError('Format {} not supported!'.format(args.output_format))
+    if args.num_shards is not None and args.output_format != 'parquet':
+        raise ValueError('--num-shards writes balanced parquet shards only')
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     vocab = _resolve_vocab(args.vocab_file)
     tic = time.perf_counter()
     outdir = expand_outdir_and_mkdir(args.sink)
-    partitions = get_partitions(args, rank, world)
-    if args.sentence_splitter == 'gpu':
-        batches = [(b, build_doc_corpus(b)) for b in _batches(partitions, args.gpu_batch_bytes)]
-    else:  # host segmentation first: its process pool forks before this process touches the GPU
-        batches = [(b, ('sentences',) + build_corpus(b, args.local_n_workers))
-                   for b in _batches(partitions, args.gpu_batch_bytes)]
+    blocks = plan_partitions(args)
+    args.n_partitions = len(blocks)
+    batches = iter_batches(args, rank, world, blocks)
+    if args.sentence_splitter == 'host':
+        # host segmentation first: its process pool forks before this process touches the GPU
+        batches = [(b, ('sentences',) + build_corpus(b, args.local_n_workers)) for b in batches]
+    else:
+        batches = ((b, build_doc_corpus(b)) for b in batches)
     import torch
+    import torch.distributed as dist
     if world > 1:
         torch.cuda.set_device(local)
+        if not dist.is_initialized():
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     from ...context import Context
     ctx = Context(vocab, do_lower_case=True)  # BertTokenizerFast default, SURVEY H5
     if args.sentence_splitter == 'gpu':
         from ... import punkt
         punkt.set_params(ctx, punkt_params(args))
+    timer = _StageTimer(args.profile_stages)
+    timer.mark()
     n_files = 0
+    kept = []
     for batch, corpus in batches:
-        n_files += len(process_batch(ctx, args, batch, corpus, outdir))
+        timer('read')
+        if args.num_shards is None:
+            n_files += len(process_batch(ctx, args, batch, corpus, outdir, timer))
+        else:
+            kept.append(make_batch_pairs(ctx, args, batch, corpus, timer))
+        timer.mark()
+    if args.num_shards is not None:
+        from ...balance import balance
+        from ...pairs import cat_pair_batches, PairBatch
+        timer.mark()
+        if kept:
+            pb = cat_pair_batches(kept)
+        else:  # a rank without partitions still takes part in the collectives
+            e64 = torch.zeros(1, dtype=torch.int64, device=ctx.device)
+            pb = PairBatch(torch.zeros(0, dtype=torch.int32, device=ctx.device), e64,
+                           torch.zeros(0, dtype=torch.int32, device=ctx.device),
+                           torch.zeros(0, dtype=torch.uint8, device=ctx.device))
+            if args.masking:
+                pb.pos = torch.zeros(0, dtype=torch.int16, device=ctx.device)
+                pb.labels = torch.zeros(0, dtype=torch.int32, device=ctx.device)
+                pb.pos_off = e64.clone()
+        del kept
+        binned = args.bin_size is not None
+        bin_size = args.bin_size if binned else args.target_seq_length
+        nbins = args.target_seq_length // bin_size
+        bb = balance(ctx, pb, bin_size, nbins, num_shards=args.num_shards)
+        timer('balance')
+        n_files += len(write_balanced(ctx, args, bb, outdir, binned))
+        timer('render+write')
+        if rank == 0:
+            with open(os.path.join(outdir, '.num_samples.json'), 'w') as f:
+                json.dump(num_samples_of_shards(bb, binned), f)
     if world > 1:
-        import torch.distributed as dist
-        if not dist.is_initialized():
-            dist.init_process_group('gloo')
         dist.barrier()
+    if rank == 0 and args.num_shards is None and args.output_format == 'parquet':
+        from ... import output
+        output.write_dataset_metadata(outdir, len(blocks),
+                                      None if args.bin_size is None else
+                                      args.target_seq_length // args.bin_size)
     if rank == 0:
         print('Running the dask pipeline took {} s'.format(time.perf_counter() - tic))
+        if args.profile_stages:
+            print('stage seconds (rank 0): ' + json.dumps(
+                {k: round(v, 3) for k, v in timer.acc.items()}))
+    if world > 1:
+        dist.barrier()
     return n_files
 
 
@@ -325,10 +483,11 @@ def attach_args(parser=None):
                     'masking in the data loader)')
     parser.add_argument('--masked-lm-ratio', type=float, default=0.15, help='Default: 0.15')
     parser.add_argument('--gpu-batch-bytes', type=int, default=1 << 30,
-                        help='lddl_amd: input text bytes per GPU batch of partitions')
+                        help='lddl_amd: input text bytes per GPU batch of partitions (documents '
+                             'are shuffled within a batch)')
     parser.add_argument('--sentence-splitter', choices=['gpu', 'host'], default='gpu',
                         help='gpu: Punkt on the GPU (exact nltk PunktSentenceTokenizer); host: '
-                             'lddl_amd.dask.bert.segment (nltk if importable, else rules)')
+                             "nltk's sent_tokenize in host processes (requires nltk)")
     parser.add_argument('--punkt-params', type=str, default=None,
                         help='JSON PunktParameters (abbrev_types, collocations, sent_starters, '
                              'ortho_context); default: nltk English model if loadable, else '
@@ -338,6 +497,13 @@ def attach_args(parser=None):
                              "(random.seed(partition seed)), bit-exact with the reference; "
                              "'native' draws the same distributions from Philox counter streams "
                              "keyed by --seed (documents and pairs in parallel)")
+    parser.add_argument('--num-shards', type=int, default=None,
+                        help='lddl_amd: balance in HBM across all ranks (RCCL) and write the '
+                             "load balancer's layout (shard-<k>.parquet[_<b>] with N or N+1 "
+                             'samples per bin + .num_samples.json) instead of part.* files')
+    attach_bool_arg(parser, 'profile-stages', default=False,
+                    help_str='lddl_amd: print device-synchronised seconds per stage (read, h2d, '
+                    'segment, tokenize, pairs, render, write, balance)')
     return parser
 
 

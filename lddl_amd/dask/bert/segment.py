@@ -1,41 +1,16 @@
-"""Sentence segmentation at the host boundary (the reference's `nltk.tokenize.sent_tokenize`,
-lddl/dask/bert/pretrain.py:86, 583).
+"""Host sentence segmentation (`--sentence-splitter host`): the reference's own
+`nltk.tokenize.sent_tokenize` (lddl/dask/bert/pretrain.py:86, 583), for debugging and A/B runs
+against the GPU Punkt (lddl_amd/punkt.py + csrc/segment.hip, the default).
 
-The reference needs NLTK's pre-trained English Punkt model, which is downloaded at run time
-(`nltk.download('punkt')`); this environment has no network and no model. Order of preference:
-  1. `nltk.tokenize.sent_tokenize` when nltk and its English Punkt model load;
-  2. nltk's untrained `PunktSentenceTokenizer()` when nltk imports but the model is absent;
-  3. the built-in rule splitter below (an approximation of untrained Punkt: break after
-     [.?!] plus closing quotes/brackets when whitespace follows, except after an ellipsis or a
-     single-letter initial followed by a capitalised word).
-A GPU Punkt is SURVEY.md §8(f1) ("next"); this module is the host fallback until then.
+The reference needs nltk and downloads its English Punkt model at run time
+(`nltk.download('punkt')`). Here, with nltk importable:
+  1. `nltk.tokenize.sent_tokenize` when the English Punkt model loads locally;
+  2. nltk's untrained `PunktSentenceTokenizer()` otherwise (what offline nltk degrades to).
+Without nltk this splitter refuses to run: an approximation would silently produce other
+sentences than the reference. Use the GPU splitter, which restates nltk's Punkt exactly.
 """
-import re
-
 _splitter = None
 KIND = None
-
-_BREAK = re.compile(r'''(?<=[.?!])(?:["')\]}']*)(?=\s+\S)''')
-
-
-def _rule_split(text):
-    out, start = [], 0
-    for m in _BREAK.finditer(text):
-        end = m.end()
-        head = text[start:end].rstrip()
-        # token that carries the terminator
-        tok = head.split()[-1] if head.split() else ''
-        core = tok.rstrip('"\')]}\'')
-        if core.endswith('...'):
-            continue
-        nxt = text[end:].lstrip()[:1]
-        word = core[:-1]
-        if len(word) == 1 and word.isalpha() and core.endswith('.') and nxt.isupper():
-            continue  # an initial ("J. Smith")
-        out.append(text[start:end])
-        start = end
-    out.append(text[start:])
-    return out
 
 
 def _init():
@@ -44,14 +19,17 @@ def _init():
         return
     try:
         import nltk
-        try:
-            nltk.data.find('tokenizers/punkt')
-            _splitter, KIND = nltk.tokenize.sent_tokenize, 'nltk-punkt-english'
-        except LookupError:
-            from nltk.tokenize.punkt import PunktSentenceTokenizer
-            _splitter, KIND = PunktSentenceTokenizer().tokenize, 'nltk-punkt-untrained'
-    except ImportError:
-        _splitter, KIND = _rule_split, 'rules'
+    except ImportError as e:
+        raise RuntimeError(
+            "--sentence-splitter host needs nltk (the reference's sent_tokenize), which is not "
+            "importable here; use the default --sentence-splitter gpu (exact nltk Punkt on the "
+            "GPU)") from e
+    try:
+        nltk.data.find('tokenizers/punkt')
+        _splitter, KIND = nltk.tokenize.sent_tokenize, 'nltk-punkt-english'
+    except LookupError:
+        from nltk.tokenize.punkt import PunktSentenceTokenizer
+        _splitter, KIND = PunktSentenceTokenizer().tokenize, 'nltk-punkt-untrained'
 
 
 def sent_tokenize(text):

@@ -9,9 +9,14 @@
 * `random_sample(sample_ratio, seed)` keeps a line iff random() < ratio, with the per-partition
   MT states of dask 2021.10's `random_state_data_python` (624 words of randint(0, 2**32) each
   drawn from Random(seed), in partition order).
+
+Blocks are planned from file sizes and a short scan for the newline after each cut
+(`plan_blocks`), so a process reads and decodes only the blocks it owns (`read_block`): under
+torchrun every rank holds its own share of the corpus, not all of it.
 """
 import os
 import random
+from dataclasses import dataclass
 
 
 def find_files_under(path, extensions=('.txt',)):
@@ -50,6 +55,76 @@ def _block_starts(data, blocksize):
     return starts
 
 
+def _next_line_start(f, off, size, chunk=1 << 16):
+    """First byte after the first newline at or after offset off - 1 (dask read_block)."""
+    pos = off - 1
+    while pos < size:
+        f.seek(pos)
+        buf = f.read(chunk)
+        j = buf.find(b'\n')
+        if j >= 0:
+            return pos + j + 1
+        pos += len(buf)
+        if not buf:
+            break
+    return size
+
+
+def _file_block_starts(fn, blocksize):
+    """_block_starts of the file's bytes, reading only around the cuts."""
+    size = os.path.getsize(fn)
+    if not blocksize or size == 0:
+        return [0, size]
+    starts = [0]
+    with open(fn, 'rb') as f:
+        for off in range(blocksize, size, blocksize):
+            starts.append(_next_line_start(f, off, size))
+    starts.append(size)
+    return starts
+
+
+@dataclass
+class Block:
+    """One dask partition before it is read: bytes [start, end) of `path` (empty if end <= start),
+    with the MT state of its random_sample (None: no sampling)."""
+    path: str
+    start: int
+    end: int
+    state: tuple = None
+    ratio: float = 1.0
+
+    @property
+    def nbytes(self):
+        return max(self.end - self.start, 0)
+
+
+def plan_blocks(path, blocksize=None, sample_ratio=1.0, sample_seed=12345):
+    """Blocks of one source in partition order (no data read beyond the cut scans)."""
+    blocks = []
+    for fn in find_files_under(path):
+        st = _file_block_starts(fn, blocksize)
+        for a, b in zip(st[:-1], st[1:]):
+            blocks.append(Block(fn, a, b if (b > a or len(st) <= 2) else a))
+    if sample_ratio < 1.0:
+        for b, s in zip(blocks, random_state_data_python(len(blocks), sample_seed)):
+            b.state, b.ratio = s, sample_ratio
+    return blocks
+
+
+def read_block(blk):
+    """The partition's lines: stripped, non-empty, sampled (readers.py:60-71)."""
+    if blk.nbytes == 0:
+        return []
+    with open(blk.path, 'rb') as f:
+        f.seek(blk.start)
+        lines = _filter(f.read(blk.end - blk.start).split(b'\n'))
+    if blk.state is None:
+        return lines
+    r = random.Random()
+    r.setstate(blk.state)
+    return [x for x in lines if r.random() < blk.ratio]
+
+
 def read_blocks(files, blocksize=None):
     """List of blocks; each block is a list of raw lines (bytes, without the delimiter)."""
     blocks = []
@@ -82,20 +157,15 @@ def _filter(block):
 
 def read_bag_of_text(path, blocksize=None, sample_ratio=1.0, sample_seed=12345):
     """readers.py:60-71: partitions of stripped, non-empty lines, optionally sampled."""
-    blocks = [_filter(b) for b in read_blocks(find_files_under(path), blocksize)]
-    if sample_ratio < 1.0:
-        states = random_state_data_python(len(blocks), sample_seed)
-        out = []
-        for b, st in zip(blocks, states):
-            r = random.Random()
-            r.setstate(st)
-            out.append([x for x in b if r.random() < sample_ratio])
-        blocks = out
-    return blocks
+    return [read_block(b) for b in plan_blocks(path, blocksize, sample_ratio, sample_seed)]
+
+
+def wikipedia_dir(path, lang='en'):
+    return os.path.join(path, lang)
 
 
 def read_wikipedia(path, lang='en', blocksize=None, sample_ratio=1.0, sample_seed=12345):
-    return read_bag_of_text(os.path.join(path, lang), blocksize, sample_ratio, sample_seed)
+    return read_bag_of_text(wikipedia_dir(path, lang), blocksize, sample_ratio, sample_seed)
 
 
 def read_books(path, blocksize=None, sample_ratio=1.0, sample_seed=12345):

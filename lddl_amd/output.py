@@ -179,6 +179,38 @@ def table(rd, r0, r1, masking, binned):
     return pa.Table.from_arrays(cols, schema=schema(masking, binned))
 
 
+def write_table(rd, r0, r1, masking, binned, path, compression=DEFAULT_COMPRESSION):
+    """Rows [r0, r1) of a Rendered as one parquet file."""
+    pq.write_table(table(rd, r0, r1, masking, binned), path, compression=compression)
+    return path
+
+
+def write_dataset_metadata(outdir, n_part, nbins=None):
+    """dask's `_common_metadata` (schema) and `_metadata` (row groups of every partition, in
+    partition order, file path `part.<i>.parquet`) next to the part files — ArrowDatasetEngine
+    .write_metadata (dask 2021.10, dataframe/io/parquet/arrow.py:712-735) as driven by
+    `to_parquet` (pretrain.py:473-478) and `to_parquet_binned` (binning.py:325-339). Binned, each
+    partition contributes its LAST bin file's row groups under the unsuffixed name, which is
+    what write_partition_binned hands back (binning.py:378-421: `_meta` is overwritten per bin
+    and `set_file_path(filename)`)."""
+    meta = None
+    schema = None
+    for p in range(n_part):
+        name = 'part.{}.parquet'.format(p)
+        fn = os.path.join(outdir, name if nbins is None else '{}_{}'.format(name, nbins - 1))
+        md = pq.read_metadata(fn)
+        md.set_file_path(name)
+        if meta is None:
+            meta, schema = md, pq.read_schema(fn)
+        else:
+            meta.append_row_groups(md)
+    if meta is None:
+        return None
+    pq.write_metadata(schema, os.path.join(outdir, '_common_metadata'))
+    meta.write_metadata_file(os.path.join(outdir, '_metadata'))
+    return os.path.join(outdir, '_metadata')
+
+
 def write_parquet(outdir, rd, part_rows, part_index, masking, nbins=None, bin_counts=None,
                   compression=DEFAULT_COMPRESSION):
     """Write the reference's files for a group of partitions.

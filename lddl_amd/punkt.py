@@ -100,9 +100,15 @@ def segment(ctx, text, doc_off):
     n_sent = ctypes.c_int64()
     check(lib.lddl_segment_count(ctx._h, _stream(), _ptr(text), text.numel(), _ptr(doc_off), n_doc,
                                  ctypes.byref(n_sent)))
-    sent_off = torch.empty(n_sent.value + 1, dtype=torch.int64, device=ctx.device)
-    doc_sent_off = torch.empty(n_doc + 1, dtype=torch.int64, device=ctx.device)
-    check(lib.lddl_segment_fill(ctx._h, _stream(), _ptr(sent_off), _ptr(doc_sent_off)))
+    filled = False
+    try:
+        sent_off = torch.empty(n_sent.value + 1, dtype=torch.int64, device=ctx.device)
+        doc_sent_off = torch.empty(n_doc + 1, dtype=torch.int64, device=ctx.device)
+        check(lib.lddl_segment_fill(ctx._h, _stream(), _ptr(sent_off), _ptr(doc_sent_off)))
+        filled = True
+    finally:
+        if not filled:  # e.g. an allocation failed: cancel, so the context stays usable
+            lib.lddl_segment_fill(ctx._h, _stream(), None, None)
     return sent_off, doc_sent_off
 
 

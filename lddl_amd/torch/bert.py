@@ -16,6 +16,7 @@ import ctypes
 import io
 import logging
 import os
+import re
 
 import numpy as np
 import torch
@@ -55,9 +56,21 @@ def _npy_u16(b):
     return np.load(io.BytesIO(b)).astype(np.uint16)
 
 
+_ODD_ASCII_WS = re.compile('[\x1c-\x1f]')
+
+
+def _canon(s):
+    """The string as the GPU splitter sees it: the reference splits with Python's str.split()
+    (Unicode whitespace, bert.py:80-81); the kernel splits on ASCII space / \\t-\\r. Strings
+    holding any other whitespace are re-joined with single spaces first (same tokens)."""
+    if s.isascii() and not _ODD_ASCII_WS.search(s):
+        return s
+    return ' '.join(s.split())
+
+
 def _pack(batch, static):
-    As = [s[0].encode('utf-8') for s in batch]
-    Bs = [s[1].encode('utf-8') for s in batch]
+    As = [_canon(s[0]).encode('utf-8') for s in batch]
+    Bs = [_canon(s[1]).encode('utf-8') for s in batch]
     na = np.fromiter((len(s[0].split()) for s in batch), np.int32, len(batch))
     nb = np.fromiter((len(s[1].split()) for s in batch), np.int32, len(batch))
     la = np.fromiter(map(len, As), np.int64, len(batch))
@@ -68,7 +81,7 @@ def _pack(batch, static):
     parts = As + Bs
     extra = None
     if static:
-        labs = [s[4].encode('utf-8') for s in batch]
+        labs = [_canon(s[4]).encode('utf-8') for s in batch]
         lab_off = np.zeros(len(batch) + 1, np.int64)
         lab_off[1:] = np.cumsum([len(x) for x in labs])
         lab_off += b_off[-1]
@@ -97,6 +110,8 @@ def _mask_tokens(inputs, special_tokens_mask=None, tokenizer=None, mlm_probabili
     """lddl/torch/bert.py:152-196 on the GPU; masks `inputs` in place and returns
     (inputs, labels).
 
+    special_tokens_mask=None marks the slots whose id is a special token, as the reference's
+    tokenizer.get_special_tokens_mask(ids, already_has_special_tokens=True) (bert.py:167-172).
     Native mode draws from Philox keyed by (seed, counter): pass a new counter per batch.
     replay = dict(masked=, replaced=, random=, words=) applies captured torch draws exactly.
     """
@@ -105,9 +120,8 @@ def _mask_tokens(inputs, special_tokens_mask=None, tokenizer=None, mlm_probabili
     B, L = inputs.shape
     labels = torch.empty_like(inputs)
     stm = special_tokens_mask
-    if stm is None:
-        raise ValueError('special_tokens_mask is required (the GPU path has no per-id lookup)')
-    stm = stm.to(device=inputs.device, dtype=torch.long).contiguous()
+    if stm is not None:
+        stm = stm.to(device=inputs.device, dtype=torch.long).contiguous()
     r = [None] * 4
     if replay is not None:
         r = [replay['masked'].to(inputs.device, torch.uint8).contiguous(),
@@ -149,6 +163,9 @@ def encode_packed(pk, ctx, sequence_length_alignment=8, ignore_index=-1):
     stm = labels = d_lab_off = d_pos = d_pos_off = None
     if pk.static:
         lab_off, pos, pos_off = pk.extra
+        if len(pos) and int(pos.max()) >= L:  # the reference's labels[i][positions] raises
+            raise IndexError('masked_lm_positions holds {} >= sequence length {}'.format(
+                int(pos.max()), L))
         d_lab_off, d_pos_off = _dev(lab_off, dev), _dev(pos_off, dev)
         d_pos = _dev(pos.view(np.int16), dev) if len(pos) else torch.zeros(1, dtype=torch.int16,
                                                                            device=dev)
@@ -172,15 +189,16 @@ class GPUCollateLoader:
     """Iterates a torch DataLoader of PackedBatch and finishes the collate on the GPU."""
 
     def __init__(self, loader, ctx, mlm_probability, ignore_index, sequence_length_alignment,
-                 extra_collate, seed):
+                 extra_collate, seed, start_epoch=0):
         self._loader = loader
         self._ctx = ctx
         self._mlm = mlm_probability
         self._ignore = ignore_index
         self._align = sequence_length_alignment
         self._extra = extra_collate
-        self._seed = seed
-        self._counter = 0
+        self._seed = seed            # Philox key: distinct per (base_seed, rank, bin)
+        self._epoch = start_epoch    # counter = epoch << 32 | batch: no stream repeats across
+        self._counter = start_epoch << 32  # epochs, and a resumed run continues, not replays
 
     @property
     def dataset(self):
@@ -193,6 +211,8 @@ class GPUCollateLoader:
         return getattr(self._loader, k)
 
     def __iter__(self):
+        self._counter = self._epoch << 32
+        self._epoch += 1
         for pk in self._loader:
             with torch.no_grad():
                 enc = encode_packed(pk, self._ctx, self._align, self._ignore)
@@ -204,6 +224,12 @@ class GPUCollateLoader:
                         counter=self._counter)
                     self._counter += 1
             yield self._extra(enc)
+
+
+def mask_seed(base_seed, rank, bin_id=-1):
+    """64-bit Philox key of one (rank, bin) loader's dynamic masking: independent streams per
+    rank and per bin (the reference draws all of them from each worker's torch RNG)."""
+    return ((int(base_seed) * 1000003 + int(rank)) * 65537 + int(bin_id) + 1) & ((1 << 64) - 1)
 
 
 class BertPretrainBinned(Binned):
@@ -259,17 +285,17 @@ def get_bert_pretrain_data_loader(path, local_rank=0, shuffle_buffer_size=16384,
         data_loader_kwargs['collate_fn'] = _pack_batch
     data_loader_kwargs['persistent_workers'] = True
 
-    def make(paths):
+    def make(paths, bin_id=-1):
         dl = data_loader_class(BertPretrainDataset(paths, **dataset_kwargs), **data_loader_kwargs)
         if return_raw_samples:
             return dl
         return GPUCollateLoader(dl, ctx, mlm_probability, ignore_index,
                                 sequence_length_alignment, extra_collate,
-                                base_seed * 1000003 + get_rank())
+                                mask_seed(base_seed, get_rank(), bin_id), start_epoch)
 
     paths = get_all_parquets_under(path)
     bin_ids = get_all_bin_ids(paths)
     if bin_ids:
-        return BertPretrainBinned([make(get_file_paths_for_bin_id(paths, b)) for b in bin_ids],
+        return BertPretrainBinned([make(get_file_paths_for_bin_id(paths, b), b) for b in bin_ids],
                                   base_seed=base_seed, start_epoch=start_epoch, logger=logger)
     return make(paths)

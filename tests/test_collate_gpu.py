@@ -82,30 +82,110 @@ def test_mask_replay_bit_exact(g, ctx_c, seed):
 
 
 def test_mask_native_rates(ctx_c):
-    """15% / 80-10-10 within 0.1% (absolute) under the native counter RNG."""
+    """north_star: 15% / 80-10-10 each within 0.1% (absolute) under the native counter RNG.
+    >= 2e7 masked slots, so 1e-3 is > 10 sigma for every rate. Input ids are out-of-vocab
+    sentinels (>= len(tokenizer)), so a random replacement (drawn from [0, len)) can never equal
+    the original: keep / random / [MASK] are told apart exactly (a random draw of the [MASK] id
+    itself, probability 0.1 / V = 3.4e-6, is the only confusion left)."""
     from lddl_amd.torch.bert import _mask_tokens
-    B, L = 256, 512
-    ids = torch.randint(5, len(ctx_c), (B, L), device='cuda')
+    V = len(ctx_c)
+    mid = ctx_c.special_ids['[MASK]']
+    B, L = 8192, 2048
+    g = torch.Generator(device='cuda').manual_seed(3)
+    ids = torch.randint(V + 10, V + 5000, (B, L), device='cuda', generator=g)
     stm = torch.zeros(B, L, dtype=torch.long, device='cuda')
     stm[:, 0] = 1
-    stm[:, 300:] = 1
+    stm[:, 1800:] = 1
     n_ok = int((stm == 0).sum())
-    tot_masked = tot_repl = tot_rand = tot_keep = 0
-    for counter in range(40):
-        x = ids.clone()
-        out, lab = _mask_tokens(x, stm, ctx_c, 0.15, -1, seed=99, counter=counter)
+    tot = dict(masked=0, repl=0, rand=0, keep=0)
+    calls = 0
+    while tot['masked'] < 2e7:
+        out, lab = _mask_tokens(ids.clone(), stm, ctx_c, 0.15, -1, seed=99, counter=calls)
         m = lab != -1
         assert not bool((m & (stm == 1)).any())
-        tot_masked += int(m.sum())
-        tot_repl += int((m & (out == ctx_c.special_ids['[MASK]'])).sum())
-        same = m & (out == ids)
-        tot_keep += int(same.sum())
-        tot_rand += int((m & (out != ids) & (out != ctx_c.special_ids['[MASK]'])).sum())
-    n = 40 * n_ok
-    assert abs(tot_masked / n - 0.15) < 0.001
-    assert abs(tot_repl / tot_masked - 0.8) < 0.001 * 10  # 80% of the masked
-    # random words equal to the original (1/V) are counted as keeps; both ~10%
-    assert abs((tot_rand + tot_keep) / tot_masked - 0.2) < 0.01
+        assert bool((lab[m] == ids[m]).all())
+        tot['masked'] += int(m.sum())
+        tot['repl'] += int((m & (out == mid)).sum())
+        tot['keep'] += int((m & (out == ids)).sum())
+        tot['rand'] += int((m & (out < V) & (out != mid)).sum())
+        assert bool(((out == ids) | m).all())  # unmasked slots untouched
+        calls += 1
+    n = calls * n_ok
+    assert tot['repl'] + tot['keep'] + tot['rand'] == tot['masked']
+    assert abs(tot['masked'] / n - 0.15) < 1e-3
+    assert abs(tot['repl'] / tot['masked'] - 0.8) < 1e-3
+    assert abs(tot['rand'] / tot['masked'] - 0.1) < 1e-3
+    assert abs(tot['keep'] / tot['masked'] - 0.1) < 1e-3
+
+
+def test_mask_special_tokens_mask_none(ctx_c):
+    """special_tokens_mask=None: special slots are the ids of all_special_ids (the reference's
+    get_special_tokens_mask(ids, already_has_special_tokens=True), bert.py:167-172)."""
+    from lddl_amd.torch.bert import _mask_tokens
+    V = len(ctx_c)
+    sp = ctx_c.all_special_ids
+    ids = torch.randint(0, V, (64, 256), device='cuda')
+    ids[:, ::7] = sp[0]
+    ids[:, 3::11] = sp[3]
+    ids[:, 0] = ctx_c.special_ids['[CLS]']
+    exp = torch.tensor([ctx_c.get_special_tokens_mask(r, already_has_special_tokens=True)
+                        for r in ids.cpu().tolist()], device='cuda')
+    a = _mask_tokens(ids.clone(), None, ctx_c, seed=7, counter=1)
+    b = _mask_tokens(ids.clone(), exp, ctx_c, seed=7, counter=1)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert not bool(((a[1] != -1) & (exp == 1)).any())
+
+
+def test_tokenizer_duck_type(ctx_u):
+    """tokenize(s, max_length, truncation), mask_token, convert_tokens_to_ids(str),
+    get_special_tokens_mask against the oracle tokenizer."""
+    from oracle import oracle as O
+    tok = O.Tokenizer(VOCAB_UNCASED, lowercase=True)
+    s = 'Hello, World! Tokenization of naïve café-style text [MASK] works.'
+    b = np.frombuffer(s.encode(), np.uint8)
+    ids, off = tok.tokenize(b, np.asarray([0, len(b)], np.int64))
+    exp = [ctx_u.tokens[i] for i in ids[off[0]:off[1]]]
+    assert ctx_u.tokenize(s) == exp
+    assert ctx_u.tokenize(s, max_length=5, truncation=True) == exp[:5]
+    w = next(t for t in ctx_u.tokens[1000:] if t.isalpha() and t.islower() and len(t) > 2)
+    long_s = ' '.join([w] * 700)
+    assert len(ctx_u.tokenize(long_s, max_length=512, truncation=True)) == 512
+    assert len(ctx_u.tokenize(long_s)) == 700
+    assert ctx_u.tokenize('') == []
+    assert ctx_u.convert_tokens_to_ids(ctx_u.mask_token) == ctx_u.special_ids['[MASK]']
+    assert ctx_u.convert_tokens_to_ids(['[CLS]', 'zzzznotaword']) == [
+        ctx_u.special_ids['[CLS]'], ctx_u.special_ids['[UNK]']]
+    assert ctx_u.get_special_tokens_mask([5, 6], [7]) == [1, 0, 0, 1, 0, 1]
+    cls = ctx_u.special_ids['[CLS]']
+    assert ctx_u.get_special_tokens_mask([cls, 999, 5], already_has_special_tokens=True) == [
+        1, 0, 0]
+
+
+def test_encode_rejects_position_beyond_length(g, ctx_u):
+    from lddl_amd.torch.bert import _to_encoded_inputs
+    batch = batch_static(g, ctx_u)[:2]
+    bad = list(batch[0])
+    from io import BytesIO
+    bio = BytesIO()
+    np.save(bio, np.asarray([1, 600], np.uint16))
+    bad[3] = bio.getvalue()
+    bad[4] = 'a b'
+    with pytest.raises(IndexError):
+        _to_encoded_inputs([tuple(bad), batch[1]], ctx_u)
+
+
+def test_encode_unicode_whitespace_split(ctx_u):
+    """Python's str.split() whitespace (\x1c-\x1f, U+00A0, U+3000 ...) separates tokens exactly
+    as in the reference's _to_encoded_inputs."""
+    from lddl_amd.torch.bert import _to_encoded_inputs
+    a = 'the\x1cquick\u00a0brown fox'
+    b = 'jumps\u3000over  the\tlazy'
+    enc = _to_encoded_inputs([(a, b, False)], ctx_u)
+    want = ([ctx_u.special_ids['[CLS]']] + ctx_u.convert_tokens_to_ids(a.split()) +
+            [ctx_u.special_ids['[SEP]']] + ctx_u.convert_tokens_to_ids(b.split()) +
+            [ctx_u.special_ids['[SEP]']])
+    got = enc['input_ids'][0].cpu().tolist()
+    assert got[:len(want)] == want and all(x == 0 for x in got[len(want):])
 
 
 def test_mask_native_deterministic(ctx_c):

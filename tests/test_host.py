@@ -72,11 +72,54 @@ def test_random_sample_is_dask_semantics(tmp_path):
     assert a[0] == ['doc{} text'.format(i) for i in range(200) if r.random() < 0.5]
 
 
-def test_rule_sentence_splitter():
+def test_host_splitter_refuses_without_nltk(monkeypatch):
+    """--sentence-splitter host runs nltk's sent_tokenize or nothing (no approximation)."""
+    import sys
     from lddl_amd.dask.bert import segment as S
-    out = S._rule_split('One here. Two is J. Smith! Three... still three? Four.')
-    assert [s.strip() for s in out] == ['One here.', 'Two is J. Smith!',
-                                         'Three... still three?', 'Four.']
+    monkeypatch.setattr(S, '_splitter', None)
+    monkeypatch.setitem(sys.modules, 'nltk', None)
+    with pytest.raises(RuntimeError, match='needs nltk'):
+        S.sent_tokenize('One. Two.')
+
+
+def test_file_block_starts_match_in_memory_blocks(tmp_path):
+    rng = np.random.default_rng(4)
+    lines = [b'x' * int(n) for n in rng.integers(0, 300, 400)]
+    data = b'\n'.join(lines) + b'\n'
+    f = tmp_path / 'a.txt'
+    f.write_bytes(data)
+    for bs in (1, 7, 100, 4096, 70_000, 10 ** 7):
+        assert R._file_block_starts(str(f), bs) == R._block_starts(data, bs)
+    # plan + read == the in-memory blocks, filtered
+    for bs in (None, 50, 1000):
+        got = [R.read_block(b) for b in R.plan_blocks(str(tmp_path), bs)]
+        exp = [R._filter(b) for b in R.read_blocks([str(f)], bs)]
+        assert got == exp
+
+
+def test_ranks_read_only_their_blocks(tmp_path, monkeypatch):
+    from lddl_amd.dask.bert import pretrain as P
+    src = tmp_path / 'src' / 'en'
+    src.mkdir(parents=True)
+    (src / 'w.txt').write_text(''.join('wiki-{} text {}\n'.format(i, i) for i in range(400)))
+    args = P.attach_args().parse_args(['--sink', str(tmp_path / 'o'), '--wikipedia',
+                                       str(tmp_path / 'src'), '--num-blocks', '8',
+                                       '--sample-ratio', '1.0', '--gpu-batch-bytes', '3000'])
+    seen = []
+    orig = R.read_block
+    monkeypatch.setattr(R, 'read_block', lambda b: seen.append(b.start) or orig(b))
+    parts = {}
+    for rank in range(3):
+        seen.clear()
+        mine = P.get_partitions(args, rank, 3)
+        blocks = P.plan_partitions(args)
+        assert sorted(seen) == sorted(blocks[p].start for p in range(len(blocks)) if p % 3 == rank)
+        for p, lines in mine:
+            assert p % 3 == rank
+            parts[p] = lines
+    # every document exactly once over all ranks (shuffled inside each rank's batches)
+    docs = sorted(d for lines in parts.values() for d in lines)
+    assert docs == sorted('wiki-{} text {}'.format(i, i) for i in range(400))
 
 
 def test_pretrain_flags_match_reference_surface():

@@ -214,3 +214,103 @@ def test_pretrain_cli_native_rng(tmp_path):
                 assert np.all(np.diff(pos.astype(int)) > 0)
                 n += 1
     assert n > 50
+
+
+def _cli(tmp_path, sink, extra, seq=128, dup=2, masking=True):
+    from lddl_amd.dask.bert import pretrain as P
+    src = tmp_path / 'source'
+    if not src.exists():
+        _write_source(str(src))
+    argv = ['--schedule', 'local', '--wikipedia', str(src), '--sink', str(sink),
+            '--target-seq-length', str(seq), '--num-blocks', '4', '--seed', '7',
+            '--vocab-file', VOCAB_UNCASED, '--local-n-workers', '1', '--duplicate-factor',
+            str(dup)] + (['--masking'] if masking else []) + extra
+    args = P.attach_args().parse_args(argv)
+    P.main(args)
+    return P.attach_args().parse_args(argv)
+
+
+@pytest.mark.parametrize('binned', [False, True])
+def test_pretrain_cli_dask_metadata(tmp_path, binned):
+    """_common_metadata + _metadata as dask's ArrowDatasetEngine.write_metadata leaves them
+    (binning.py:325-339, pretrain.py:473-478): row groups of every partition in order, file
+    paths part.<i>.parquet (binned: the last bin file's row groups)."""
+    from lddl_amd.dask.bert import pretrain as P
+    sink = tmp_path / 'out'
+    args = _cli(tmp_path, sink, ['--bin-size', '32'] if binned else [])
+    n_part = len(P.plan_partitions(args))
+    md = pq.read_metadata(sink / '_metadata')
+    names = [md.row_group(i).column(0).file_path for i in range(md.num_row_groups)]
+    assert names == ['part.{}.parquet'.format(p) for p in range(n_part)]
+    suffix = '_3' if binned else ''
+    assert md.num_rows == sum(pq.read_metadata(sink / 'part.{}.parquet{}'.format(p, suffix)).num_rows
+                              for p in range(n_part))
+    assert pq.read_schema(sink / '_common_metadata').equals(
+        pq.read_schema(sink / 'part.0.parquet{}'.format(suffix)))
+
+
+@pytest.mark.parametrize('binned', [False, True])
+def test_pretrain_cli_txt_output(tmp_path, binned):
+    """--output-format txt (pretrain.py:501-531, binning.py:439-509): the parquet rows of the
+    same run as the reference's text lines, dask's file names, no trailing newline."""
+    from lddl_amd.dask.bert import pretrain as P
+    extra = ['--bin-size', '32'] if binned else []
+    args = _cli(tmp_path, tmp_path / 'pq', extra)
+    _cli(tmp_path, tmp_path / 'txt', extra + ['--output-format', 'txt'])
+    for p in range(len(P.plan_partitions(args))):
+        if binned:
+            for b in range(4):
+                rows = pq.read_table(tmp_path / 'pq' / 'part.{}.parquet_{}'.format(p, b)).to_pylist()
+                got = (tmp_path / 'txt' / '{}_{}.txt'.format(p, b)).read_text()
+                assert got == '\n'.join(P._txt_line(r, True) for r in rows)
+        else:
+            rows = pq.read_table(tmp_path / 'pq' / 'part.{}.parquet'.format(p)).to_pylist()
+            got = (tmp_path / 'txt' / '{}.txt'.format(p)).read_text()
+            assert got == '\n'.join(P._txt_line(r, True) for r in rows)
+            r = rows[0]  # (numpy's array str may wrap a long positions list onto new lines)
+            assert got.startswith('is_random_next: {} - [CLS] {} [SEP] {} [SEP] - '
+                                  'masked_lm_positions: ['.format(r['is_random_next'], r['A'],
+                                                                  r['B']))
+            assert '] - {} - {}'.format(r['masked_lm_labels'], r['num_tokens']) in got
+
+
+@pytest.mark.parametrize('binned,masking', [(True, True), (False, False)])
+def test_pretrain_cli_num_shards_balanced(tmp_path, binned, masking):
+    """--num-shards: the balancer's layout straight from HBM (shard-<k>.parquet[_<b>], N or N+1
+    samples per bin, .num_samples.json) holding exactly the rows of the part.* output of the
+    same run; then get_bert_pretrain_data_loader consumes it."""
+    import logging
+    from collections import Counter
+    from lddl_amd.torch import get_bert_pretrain_data_loader
+    extra = ['--bin-size', '32'] if binned else []
+    from lddl_amd.dask.bert import pretrain as P
+    args = _cli(tmp_path, tmp_path / 'parts', extra, masking=masking)
+    _cli(tmp_path, tmp_path / 'shards', extra + ['--num-shards', '4'], masking=masking)
+    nb = 4 if binned else 1
+    ns = json.loads((tmp_path / 'shards' / '.num_samples.json').read_text())
+    want_rows, got_rows = Counter(), Counter()
+    for p in range(len(P.plan_partitions(args))):
+        for b in range(nb):
+            fn = 'part.{}.parquet{}'.format(p, '_{}'.format(b) if binned else '')
+            for r in pq.read_table(tmp_path / 'parts' / fn).to_pylist():
+                want_rows[tuple(sorted(r.items()))] += 1
+    for b in range(nb):
+        counts = []
+        for s in range(4):
+            fn = 'shard-{}.parquet{}'.format(s, '_{}'.format(b) if binned else '')
+            t = pq.read_table(tmp_path / 'shards' / fn)
+            assert ns[fn] == t.num_rows
+            counts.append(t.num_rows)
+            for r in t.to_pylist():
+                if binned:
+                    assert r['bin_id'] == b
+                got_rows[tuple(sorted(r.items()))] += 1
+        assert max(counts) - min(counts) <= 1
+    assert got_rows == want_rows
+    assert len(ns) == 4 * nb
+    dl = get_bert_pretrain_data_loader(
+        str(tmp_path / 'shards'), vocab_file=VOCAB_UNCASED,
+        data_loader_kwargs={'batch_size': 16, 'num_workers': 2}, log_level=logging.WARNING)
+    n = sum(batch['input_ids'].size(0) for batch in dl)
+    # the loader evens out files to the smallest count per bin (lost-samples rule)
+    assert sum(ns.values()) - 4 * nb <= n <= sum(ns.values())
