@@ -11,6 +11,14 @@
 //                         masked, ignore_index elsewhere. Native mode draws from a counter-based
 //                         Philox4x32-10 keyed by (seed, counter, slot); replay mode applies
 //                         captured torch masks bit for bit.
+//   lddl_collate_count    the whitespace token counts len(A.split()), len(B.split()) of every
+//                         sample and max(na + nb + 3), which sizes the batch (bert.py:80-96).
+//   lddl_collate_encode_masked   _to_encoded_inputs + _mask_tokens in ONE pass (the loader's
+//                         dynamic-masking collate, bert.py:348-365): the row is built in LDS and
+//                         masked on its way out, so input_ids / token_type_ids / attention_mask /
+//                         labels are each written once (36 B per slot incl. the string read)
+//                         and no special_tokens_mask is materialised; bit-identical to
+//                         lddl_collate_encode followed by lddl_mask_dynamic (same Philox stream).
 #include "common.h"
 #include "ctx.h"
 #include "device.h"
@@ -80,6 +88,27 @@ __device__ int32_t split_lookup(const Tables& T, const uint8_t* bytes, int64_t b
   return ntok;
 }
 
+// One slot's native-RNG masking decision (bert.py:176-192): Philox4x32-10 keyed by seed, counter
+// (batch) and the flat slot index. Returns the output id; *label = id if masked else ignore.
+struct MaskDraw {
+  float p;
+  int64_t ignore_index, mask_id, vocab_len;
+  uint64_t seed, counter;
+};
+__device__ inline int64_t mask_slot(const MaskDraw& D, int64_t flat, bool special, int64_t id,
+                                    int64_t* label) {
+  const uint4 r = Philox::gen(make_uint4((uint32_t)flat, (uint32_t)(flat >> 32), (uint32_t)D.counter,
+                                         (uint32_t)(D.counter >> 32)),
+                              make_uint2((uint32_t)D.seed, (uint32_t)(D.seed >> 32)));
+  const bool masked = !special && u01(r.x) < D.p;
+  const bool replaced = masked && u01(r.y) < 0.8f;
+  const bool rnd = masked && !replaced && u01(r.z) < 0.5f;
+  *label = masked ? id : D.ignore_index;
+  if (replaced) return D.mask_id;
+  if (rnd) return (int64_t)(((uint64_t)r.w * (uint64_t)D.vocab_len) >> 32);
+  return id;
+}
+
 struct EncodeArgs {
   Tables T;
   const uint8_t* bytes;
@@ -99,6 +128,8 @@ struct EncodeArgs {
   const int64_t* pos_off;
   int64_t* labels;
   int64_t ignore_index;
+  int32_t fused_mask;  // 1: dynamic masking applied on the way out (labels written from it)
+  MaskDraw draw;
 };
 
 constexpr int kEncWaves = 4;
@@ -137,12 +168,51 @@ __global__ void __launch_bounds__(64 * kEncWaves) encode_kernel(EncodeArgs E) {
   if (!active) return;
   const int64_t row = (int64_t)b * E.L;
   for (int32_t x = lane; x < E.L; x += 64) {
-    E.input_ids[row + x] = sid[x];
+    const bool special = x == 0 || x == na + 1 || x >= end - 1;
+    if (E.fused_mask) {
+      int64_t lab;
+      E.input_ids[row + x] = mask_slot(E.draw, row + x, special, sid[x], &lab);
+      E.labels[row + x] = lab;
+    } else {
+      E.input_ids[row + x] = sid[x];
+      if (E.labels) E.labels[row + x] = slab[x] < 0 ? E.ignore_index : (int64_t)slab[x];
+    }
     E.token_type_ids[row + x] = (x >= na + 2 && x < end) ? 1 : 0;
     E.attention_mask[row + x] = x < end ? 1 : 0;
-    if (E.special_tokens_mask)
-      E.special_tokens_mask[row + x] = (x == 0 || x == na + 1 || x >= end - 1) ? 1 : 0;
-    if (E.labels) E.labels[row + x] = slab[x] < 0 ? E.ignore_index : (int64_t)slab[x];
+    if (E.special_tokens_mask) E.special_tokens_mask[row + x] = special ? 1 : 0;
+  }
+}
+
+// Whitespace token counts of A and B per sample (one wave per sample, ballots over 64-byte
+// windows) and the batch's max(na + nb + 3) (atomicMax on an int32).
+__device__ int32_t count_words(const uint8_t* bytes, int64_t b0, int64_t b1) {
+  const int lane = lane_id();
+  int32_t n = 0;
+  uint8_t prev = ' ';
+  for (int64_t base = b0; base < b1; base += 64) {
+    const int64_t i = base + lane;
+    const uint8_t c = i < b1 ? bytes[i] : ' ';
+    const int up = __shfl_up((int)c, 1, 64);
+    const uint8_t pc = lane == 0 ? prev : (uint8_t)up;
+    n += __popcll(__ballot(!is_ws(c) && is_ws(pc)));
+    prev = (uint8_t)__shfl((int)c, 63, 64);
+  }
+  return n;
+}
+
+__global__ void __launch_bounds__(256) count_kernel(const uint8_t* __restrict__ bytes,
+                                                    const int64_t* __restrict__ a_off,
+                                                    const int64_t* __restrict__ b_off, int32_t B,
+                                                    int32_t* __restrict__ na, int32_t* __restrict__ nb,
+                                                    int32_t* __restrict__ max_len) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int32_t x = count_words(bytes, a_off[b], a_off[b + 1]);
+  const int32_t y = count_words(bytes, b_off[b], b_off[b + 1]);
+  if (lane_id() == 0) {
+    na[b] = x;
+    nb[b] = y;
+    atomicMax(max_len, x + y + 3);
   }
 }
 
@@ -165,39 +235,38 @@ struct MaskArgs {
   const int64_t* r_words;
 };
 
+// special_tokens_mask of slot i = (b, x): the given tensor, else the layout from the lengths,
+// else membership of the id in the special ids
+__device__ inline bool mask_special(const MaskArgs& M, int64_t i, int64_t b, int64_t x, int64_t id) {
+  if (M.special) return M.special[i] != 0;
+  if (M.na) {
+    const int32_t na = M.na[b], end = na + M.nb[b] + 3;
+    return x == 0 || x == na + 1 || x >= end - 1;
+  }
+  bool sp = false;  // tokenizer.get_special_tokens_mask(ids, already_has_special_tokens=True)
+  for (int k = 0; k < kNumSpecial; ++k) sp |= M.special_ids[k] >= 0 && id == M.special_ids[k];
+  return sp;
+}
+
 __global__ void __launch_bounds__(256) mask_kernel(MaskArgs M) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= M.B * M.L) return;
   const int64_t b = i / M.L, x = i - b * M.L;
   const int64_t id = M.ids[i];
-  bool special;
-  if (M.special) special = M.special[i] != 0;
-  else if (M.na) {
-    const int32_t na = M.na[b], end = na + M.nb[b] + 3;
-    special = x == 0 || x == na + 1 || x >= end - 1;
-  } else {  // tokenizer.get_special_tokens_mask(ids, already_has_special_tokens=True)
-    special = false;
-    for (int k = 0; k < kNumSpecial; ++k) special |= M.special_ids[k] >= 0 && id == M.special_ids[k];
+  const bool special = mask_special(M, i, b, x, id);
+  if (!M.r_masked) {  // native: the shared Philox decision (also used by the fused collate)
+    int64_t lab;
+    const int64_t out = mask_slot(MaskDraw{M.p, M.ignore_index, M.mask_id, M.vocab_len, M.seed,
+                                           M.counter}, i, special, id, &lab);
+    M.labels[i] = lab;
+    if (out != id) M.ids[i] = out;
+    return;
   }
-  bool masked, replaced, rnd;
-  int64_t word;
-  if (M.r_masked) {
-    masked = M.r_masked[i];
-    replaced = M.r_replaced[i];
-    rnd = M.r_random[i];
-    word = M.r_words[i];
-  } else {
-    const uint4 r = Philox::gen(make_uint4((uint32_t)i, (uint32_t)(i >> 32), (uint32_t)M.counter,
-                                           (uint32_t)(M.counter >> 32)),
-                                make_uint2((uint32_t)M.seed, (uint32_t)(M.seed >> 32)));
-    masked = !special && u01(r.x) < M.p;
-    replaced = masked && u01(r.y) < 0.8f;
-    rnd = masked && !replaced && u01(r.z) < 0.5f;
-    word = (int64_t)(((uint64_t)r.w * (uint64_t)M.vocab_len) >> 32);
-  }
+  // replay of captured torch draws: masked_indices already excludes special slots
+  const bool masked = M.r_masked[i], replaced = M.r_replaced[i], rnd = M.r_random[i];
   M.labels[i] = masked ? id : M.ignore_index;
   if (replaced) M.ids[i] = M.mask_id;
-  else if (rnd) M.ids[i] = word;
+  else if (rnd) M.ids[i] = M.r_words[i];
 }
 
 }  // namespace
@@ -219,7 +288,7 @@ extern "C" int lddl_collate_encode(lddl_ctx* c, void* stream, const uint8_t* d_b
     LDDL_FAIL(-1, "vocab needs [CLS] and [SEP]");
   EncodeArgs E{c->tab, d_bytes, d_a_off, d_b_off, d_na, d_nb, batch, seq_len, d_input_ids,
                d_token_type_ids, d_attention_mask, d_special_tokens_mask, d_lab_bytes, d_lab_off,
-               d_pos, d_pos_off, d_labels, ignore_index};
+               d_pos, d_pos_off, d_labels, ignore_index, 0, {}};
   const size_t lds = sizeof(int32_t) * 2 * (size_t)seq_len * kEncWaves;
   if (lds > 160 * 1024) LDDL_FAIL(-1, "sequence length %d too long for the collate kernel", seq_len);
   hipLaunchKernelGGL(encode_kernel, dim3((unsigned)((batch + kEncWaves - 1) / kEncWaves)),
@@ -246,6 +315,46 @@ extern "C" int lddl_mask_dynamic(lddl_ctx* c, void* stream, int64_t* d_input_ids
   for (int k = 0; k < kNumSpecial; ++k) M.special_ids[k] = c->tab.special_id[k];
   hipLaunchKernelGGL(mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      as_stream(stream), M);
+  LDDL_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int lddl_collate_count(void* stream, const uint8_t* d_bytes, const int64_t* d_a_off,
+                                  const int64_t* d_b_off, int32_t batch, int32_t* d_na,
+                                  int32_t* d_nb, int32_t* d_max_len) {
+  if (batch < 0 || !d_max_len) LDDL_FAIL(-1, "bad arguments");
+  hipStream_t st = as_stream(stream);
+  LDDL_HIP(hipMemsetAsync(d_max_len, 0, sizeof(int32_t), st));
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(count_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, d_bytes,
+                     d_a_off, d_b_off, batch, d_na, d_nb, d_max_len);
+  LDDL_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int lddl_collate_encode_masked(lddl_ctx* c, void* stream, const uint8_t* d_bytes,
+                                          const int64_t* d_a_off, const int64_t* d_b_off,
+                                          const int32_t* d_na, const int32_t* d_nb, int32_t batch,
+                                          int32_t seq_len, int64_t* d_input_ids,
+                                          int64_t* d_token_type_ids, int64_t* d_attention_mask,
+                                          int64_t* d_labels, float mlm_probability,
+                                          int64_t ignore_index, int64_t vocab_len, uint64_t seed,
+                                          uint64_t counter) {
+  if (!c) LDDL_FAIL(-1, "null ctx");
+  if (batch <= 0 || seq_len <= 0) return 0;
+  if (c->tab.special_id[kCls] < 0 || c->tab.special_id[kSep] < 0 || c->tab.special_id[kMask] < 0)
+    LDDL_FAIL(-1, "vocab needs [CLS], [SEP] and [MASK]");
+  if (!d_input_ids || !d_token_type_ids || !d_attention_mask || !d_labels)
+    LDDL_FAIL(-1, "null output");
+  EncodeArgs E{c->tab, d_bytes, d_a_off, d_b_off, d_na, d_nb, batch, seq_len, d_input_ids,
+               d_token_type_ids, d_attention_mask, nullptr, nullptr, nullptr, nullptr, nullptr,
+               d_labels, ignore_index, 1,
+               MaskDraw{mlm_probability, ignore_index, c->tab.special_id[kMask], vocab_len, seed,
+                        counter}};
+  const size_t lds = sizeof(int32_t) * 2 * (size_t)seq_len * kEncWaves;
+  if (lds > 160 * 1024) LDDL_FAIL(-1, "sequence length %d too long for the collate kernel", seq_len);
+  hipLaunchKernelGGL(encode_kernel, dim3((unsigned)((batch + kEncWaves - 1) / kEncWaves)),
+                     dim3(64 * kEncWaves), lds, as_stream(stream), E);
   LDDL_HIP(hipGetLastError());
   return 0;
 }

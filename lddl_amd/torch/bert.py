@@ -17,6 +17,7 @@ import io
 import logging
 import os
 import re
+import time
 
 import numpy as np
 import torch
@@ -69,10 +70,11 @@ def _canon(s):
 
 
 def _pack(batch, static):
+    """Flat host buffers of a batch: A and B strings back to back (separators canonicalised to
+    ASCII), their offsets and, with static masking, the labels strings and decoded positions.
+    Token counts are taken on the GPU (lddl_collate_count), not with str.split() here."""
     As = [_canon(s[0]).encode('utf-8') for s in batch]
     Bs = [_canon(s[1]).encode('utf-8') for s in batch]
-    na = np.fromiter((len(s[0].split()) for s in batch), np.int32, len(batch))
-    nb = np.fromiter((len(s[1].split()) for s in batch), np.int32, len(batch))
     la = np.fromiter(map(len, As), np.int64, len(batch))
     lb = np.fromiter(map(len, Bs), np.int64, len(batch))
     a_off = np.zeros(len(batch) + 1, np.int64)
@@ -91,7 +93,7 @@ def _pack(batch, static):
         parts += labs
         extra = (lab_off, np.concatenate(pos) if pos else np.zeros(0, np.uint16), pos_off)
     blob = np.frombuffer(bytearray(b''.join(parts)), np.uint8)
-    return blob, a_off, b_off, na, nb, extra
+    return blob, a_off, b_off, extra
 
 
 def _dev(a, device):
@@ -138,9 +140,11 @@ class PackedBatch:
     """A collated batch as flat host buffers (built in a DataLoader worker, picklable)."""
 
     def __init__(self, batch):
+        t0 = time.perf_counter()
         self.static = len(batch[0]) > 3
-        self.blob, self.a_off, self.b_off, self.na, self.nb, self.extra = _pack(batch, self.static)
+        self.blob, self.a_off, self.b_off, self.extra = _pack(batch, self.static)
         self.nsl = np.asarray([s[2] for s in batch], np.int64)
+        self.pack_s = time.perf_counter() - t0  # host time of the pack (in the worker)
 
     def __len__(self):
         return len(self.nsl)
@@ -150,16 +154,40 @@ def _pack_batch(batch):
     return PackedBatch(batch)
 
 
-def encode_packed(pk, ctx, sequence_length_alignment=8, ignore_index=-1):
-    """`_to_encoded_inputs` on an already packed batch (main process, GPU)."""
+def encode_packed(pk, ctx, sequence_length_alignment=8, ignore_index=-1, mask=None, events=None):
+    """`_to_encoded_inputs` on an already packed batch (main process, GPU).
+
+    mask = (mlm_probability, seed, counter) on a dynamic-masking batch runs `_mask_tokens` fused
+    into the same kernel (lddl_collate_encode_masked) and returns `labels` instead of
+    `special_tokens_mask`. events: optional pair of torch.cuda.Event recorded around the
+    encode kernel (timing)."""
     dev = ctx.device
     B = len(pk)
-    seq = int((pk.na + pk.nb).max()) + 3
-    L = ((seq - 1) // sequence_length_alignment + 1) * sequence_length_alignment
     d_blob = _dev(pk.blob, dev) if len(pk.blob) else torch.zeros(1, dtype=torch.uint8, device=dev)
-    d_a, d_b, d_na, d_nb = (_dev(x, dev) for x in (pk.a_off, pk.b_off, pk.na, pk.nb))
+    d_off = _dev(np.concatenate([pk.a_off, pk.b_off]), dev)
+    d_a, d_b = d_off[:B + 1], d_off[B + 1:]
+    cnt = torch.empty(2 * B + 1, dtype=torch.int32, device=dev)
+    d_na, d_nb, d_mx = cnt[:B], cnt[B:2 * B], cnt[2 * B:]
+    check(lib.lddl_collate_count(_stream(), _ptr(d_blob), _ptr(d_a), _ptr(d_b), B, _ptr(d_na),
+                                 _ptr(d_nb), _ptr(d_mx)))
+    seq = int(d_mx.item())  # the batch's shape: max(len(A) + len(B) + 3) (bert.py:91-96)
+    L = ((seq - 1) // sequence_length_alignment + 1) * sequence_length_alignment
     out = {k: torch.empty(B, L, dtype=torch.long, device=dev)
            for k in ('input_ids', 'token_type_ids', 'attention_mask')}
+    if mask is not None and not pk.static:
+        p, seed, counter = mask
+        labels = torch.empty(B, L, dtype=torch.long, device=dev)
+        if events is not None:
+            events[0].record()
+        check(lib.lddl_collate_encode_masked(
+            ctx.handle, _stream(), _ptr(d_blob), _ptr(d_a), _ptr(d_b), _ptr(d_na), _ptr(d_nb), B,
+            L, _ptr(out['input_ids']), _ptr(out['token_type_ids']), _ptr(out['attention_mask']),
+            _ptr(labels), float(p), ignore_index, len(ctx), seed, counter))
+        if events is not None:
+            events[1].record()
+        out['next_sentence_labels'] = _dev(pk.nsl, dev)
+        out['labels'] = labels
+        return out
     stm = labels = d_lab_off = d_pos = d_pos_off = None
     if pk.static:
         lab_off, pos, pos_off = pk.extra
@@ -172,11 +200,15 @@ def encode_packed(pk, ctx, sequence_length_alignment=8, ignore_index=-1):
         labels = torch.empty(B, L, dtype=torch.long, device=dev)
     else:
         stm = torch.empty(B, L, dtype=torch.long, device=dev)
+    if events is not None:
+        events[0].record()
     check(lib.lddl_collate_encode(ctx.handle, _stream(), _ptr(d_blob), _ptr(d_a), _ptr(d_b),
                                   _ptr(d_na), _ptr(d_nb), B, L, _ptr(out['input_ids']),
                                   _ptr(out['token_type_ids']), _ptr(out['attention_mask']),
                                   _ptr(stm), _ptr(d_blob) if pk.static else None, _ptr(d_lab_off),
                                   _ptr(d_pos), _ptr(d_pos_off), _ptr(labels), ignore_index))
+    if events is not None:
+        events[1].record()
     out['next_sentence_labels'] = _dev(pk.nsl, dev)
     if pk.static:
         out['labels'] = labels
@@ -199,6 +231,8 @@ class GPUCollateLoader:
         self._seed = seed            # Philox key: distinct per (base_seed, rank, bin)
         self._epoch = start_epoch    # counter = epoch << 32 | batch: no stream repeats across
         self._counter = start_epoch << 32  # epochs, and a resumed run continues, not replays
+        self.stats = None  # dict(pack_s=[], blob_bytes=[], events=[], slots=[]): record timings
+        self._stream = torch.cuda.Stream(device=ctx.device)
 
     @property
     def dataset(self):
@@ -214,15 +248,26 @@ class GPUCollateLoader:
         self._counter = self._epoch << 32
         self._epoch += 1
         for pk in self._loader:
-            with torch.no_grad():
-                enc = encode_packed(pk, self._ctx, self._align, self._ignore)
-                if 'special_tokens_mask' in enc:  # dynamic masking
-                    stm = enc.pop('special_tokens_mask')
-                    enc['input_ids'], enc['labels'] = _mask_tokens(
-                        enc['input_ids'], special_tokens_mask=stm, tokenizer=self._ctx,
-                        mlm_probability=self._mlm, ignore_index=self._ignore, seed=self._seed,
-                        counter=self._counter)
-                    self._counter += 1
+            ev = None
+            if self.stats is not None:
+                self.stats['pack_s'].append(pk.pack_s)
+                self.stats['blob_bytes'].append(len(pk.blob))
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            consumer = torch.cuda.current_stream()
+            # the collate runs on its own stream: its one host sync (the batch shape) waits for
+            # the count kernel only, not for the training step queued on the consumer's stream
+            with torch.cuda.stream(self._stream), torch.no_grad():
+                # dynamic masking: collate + _mask_tokens in one kernel
+                enc = encode_packed(pk, self._ctx, self._align, self._ignore,
+                                    mask=(self._mlm, self._seed, self._counter), events=ev)
+            consumer.wait_stream(self._stream)
+            for t in enc.values():
+                t.record_stream(consumer)
+            if not pk.static:
+                self._counter += 1
+            if self.stats is not None:
+                self.stats['events'].append(ev)
+                self.stats['slots'].append(enc['input_ids'].numel())
             yield self._extra(enc)
 
 

@@ -197,3 +197,22 @@ def test_mask_native_deterministic(ctx_c):
     c = _mask_tokens(ids.clone(), stm, ctx_c, seed=5, counter=4)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     assert not torch.equal(a[1], c[1])
+
+
+@pytest.mark.parametrize('align', [8, 1])
+def test_fused_collate_mask_equals_two_pass(g, ctx_c, align):
+    """lddl_collate_encode_masked == lddl_collate_encode + lddl_mask_dynamic (same Philox
+    stream), i.e. the loader's one-kernel collate is the reference's _to_encoded_inputs followed
+    by _mask_tokens."""
+    from lddl_amd.torch.bert import PackedBatch, encode_packed, _mask_tokens
+    pk = PackedBatch(batch_dyn(g, ctx_c))
+    two = encode_packed(pk, ctx_c, align)
+    ids, lab = _mask_tokens(two['input_ids'], two.pop('special_tokens_mask'), ctx_c, 0.15, -1,
+                            seed=1234567, counter=(3 << 32) + 5)
+    one = encode_packed(pk, ctx_c, align, mask=(0.15, 1234567, (3 << 32) + 5))
+    assert set(one) == {'input_ids', 'token_type_ids', 'attention_mask', 'labels',
+                        'next_sentence_labels'}
+    assert torch.equal(one['input_ids'], ids) and torch.equal(one['labels'], lab)
+    for k in ('token_type_ids', 'attention_mask', 'next_sentence_labels'):
+        assert torch.equal(one[k], two[k])
+    assert int((lab != -1).sum()) > 0
