@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "common.h"
 #include "ctx.h"
@@ -306,7 +307,7 @@ __device__ inline uint32_t bloom_candidates32(const uint32_t* bloom, const B32& 
 // The longest candidate is probed first (most words are one piece); when it misses, the Bloom
 // filter (LDS) rules out the shorter lengths that cannot be pieces.
 __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v, int nb,
-                           uint64_t ends, Pcs& pc) {
+                           uint64_t ends, Pcs& pc, bool first_probe_missed = false) {
   int n = 0, start = 0;
   while (start < nb) {
     const B32 a = shr_bytes(v, start);
@@ -314,7 +315,17 @@ __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v,
     const uint64_t e = ends >> start;  // bit L: a piece of length L may end here
     int len = nb - start < T.max_piece_bytes ? nb - start : T.max_piece_bytes;
     while (len > 0 && !((e >> len) & 1ull)) --len;
-    int32_t id = len > 0 ? probe32(T, a, len, cont) : -1;
+    // (the caller may already know that the whole word is not one piece)
+    int32_t id = len > 0 && !(first_probe_missed && start == 0 && len == nb) ? probe32(T, a, len, cont)
+                                                                              : -1;
+#ifdef LDDL_TOK_ONE_PROBE  // A/B experiment only: one full-length probe per unit
+    pc.put(0, id < 0 ? T.special_id[kUnk] : id);
+    return 1;
+#endif
+#ifdef LDDL_TOK_NO_BLOOM  // A/B experiment only: descending probes without the Bloom filter
+    while (id < 0 && --len > 0)
+      if ((e >> len) & 1ull) id = probe32(T, a, len, cont);
+#endif
     if (id < 0 && len > 1) {
       uint32_t cand = bloom_candidates32(bloom, a, len - 1, cont) & (uint32_t)(e >> 1);
       while (cand) {
@@ -527,6 +538,73 @@ __device__ int unit_pieces(const Tables& T, const uint32_t* bloom, const uint32_
   return wordpiece32(T, bloom, v, nb, ends, pc);
 }
 
+// The normalised word of a word / isolated-char unit in registers (<= 32 bytes) and the byte
+// positions where a piece may end. status: 0 ok, 1 empty (every char dropped: 0 pieces), -1 the
+// unit needs the lane kernel (> kNorm normalised bytes). ASCII units are loaded straight from the
+// text (SWAR lowercase); others are normalised through the lane's LDS row `w` first.
+struct UnitWord {
+  B32 v;
+  int nb;
+  uint64_t ends;
+  int status;
+};
+
+__device__ UnitWord unit_word(const Tables& T, const uint32_t* s_ascii, const uint8_t* __restrict__ text,
+                              int64_t n_bytes, int64_t start, int len, bool unit_slow, uint8_t* w) {
+  UnitWord u;
+  u.status = 0;
+  if (!unit_slow && len <= 32 && T.ascii_mode != 0) {
+    B32 v = load32(text, n_bytes, start);
+    if (T.ascii_mode == 1) v = B32{swar_lower(v.w0), swar_lower(v.w1), swar_lower(v.w2), swar_lower(v.w3)};
+    u.v = v;
+    u.nb = len;
+    u.ends = ~0ull;
+    return u;
+  }
+  int nb = 0;
+  int64_t j = start;
+  const int64_t je = start + len;
+  while (j < je) {
+    const uint32_t b0 = text[j];
+    uint32_t cp, e;
+    if (b0 < 0x80) {
+      cp = b0;
+      e = s_ascii[b0];
+      ++j;
+    } else {
+      cp = utf8_next(text, je, j);
+      e = tab_entry(T, cp);
+    }
+    if ((e >> 30) == kDrop) continue;
+    uint8_t ob[12];
+    int olen;
+    if (e & kIdent) olen = put_utf8(ob, cp);
+    else if (e & kMulti) {
+      const uint8_t* p = T.pool + (e & 0xFFFFFFu);
+      olen = p[0];
+      for (int q = 0; q < olen; ++q) ob[q] = p[2 + q];
+    } else olen = put_utf8(ob, e & 0x1FFFFFu);
+    if (nb + olen > kNorm) {
+      u.status = -1;
+      return u;
+    }
+    for (int q = 0; q < olen; ++q) w[nb + q] = ob[q];
+    nb += olen;
+  }
+  u.nb = nb;
+  if (nb == 0) {
+    u.status = 1;
+    return u;
+  }
+  uint64_t ends = 1ull << nb;
+  for (int e = 1; e < nb; ++e)
+    if ((w[e] & 0xC0) != 0x80) ends |= 1ull << e;
+  u.ends = ends;
+  const uint64_t* w8 = reinterpret_cast<const uint64_t*>(w);
+  u.v = B32{w8[0], w8[1], w8[2], w8[3]};
+  return u;
+}
+
 __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
     Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
     int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
@@ -576,25 +654,48 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Batched wave tokenizer: classification per 64-byte window feeds an LDS queue of units that
-// spans sentences; WordPiece runs when 64 units are queued, so every lane has a word. Pieces are
-// placed by a segmented scan over the queue (units of one sentence are contiguous and ordered)
-// on top of each in-flight sentence's running count (a ring of kRing sentences).
+// Batched wave tokenizer. Classification per 64-byte window feeds an LDS queue of units that
+// spans sentences. When kSF units are queued they are resolved in two phases:
+//   A (one lane per unit, 64 at a time): literal specials, and one full-length vocab probe of
+//     every ASCII word / punctuation unit. ~3/4 of the units are a single piece and are done.
+//   B (one lane per unit, 64 at a time): greedy longest-match WordPiece of the remaining "hard"
+//     units only (multi-piece words, non-ASCII). Deferring them across kSF units gives every
+//     lane of a phase-B pass a hard unit, instead of ~16 hard units and 48 idle lanes per 64-unit
+//     flush: the divergent longest-match loop (Bloom pass + descending probes per piece) runs
+//     ~3x less often (round 2: phase B was ~47 % of the kernel, counters in profiles/r02_*).
+// Pieces are then placed in queue order by a segmented scan over each in-flight sentence's
+// running count (a ring of kRing sentences); a phase-B chunk's pieces are placed before the next
+// chunk reuses the per-lane piece columns.
 // ---------------------------------------------------------------------------------------------
-constexpr int kQ = 128;     // queued units (a window adds <= 64; flush at >= 64)
-constexpr int kRing = 64;   // sentences in flight per wave
-constexpr int kBW = 16;     // waves per workgroup (one workgroup per CU shares the Bloom filter)
+#ifndef LDDL_TOK_SF
+#define LDDL_TOK_SF 192
+#endif
+#ifndef LDDL_TOK_BW
+#define LDDL_TOK_BW 16
+#endif
+constexpr int kSF = LDDL_TOK_SF;   // units resolved per pass (kSF / 64 phase-A rounds)
+constexpr int kQ = kSF + 64;       // queue capacity (a window adds <= 64 units)
+constexpr int kRing = 64;          // sentences in flight per wave
+constexpr int kBW = LDDL_TOK_BW;   // waves per workgroup (one workgroup per CU shares the Bloom filter)
+using HIdx = std::conditional_t<(kSF > 256), uint16_t, uint8_t>;
+constexpr int32_t kHardBit = INT32_MIN;  // q_res: pieces are in column (res & 63) of pcs
 
 struct alignas(16) BatchLds {
   uint8_t us[64], ue[64], uk[64];
   int32_t q_rel[kQ];        // unit start relative to its sentence's first byte
   uint8_t q_len[kQ], q_kind[kQ], q_slot[kQ], q_slow[kQ];
+  int32_t q_res[kSF];       // phase A/B result: the single piece id, or kHardBit | column
+  uint8_t q_npc[kSF];       // pieces of the unit
+  HIdx h_idx[kSF];          // queue positions of the hard units, in order
   int64_t r_b0[kRing];
-  int32_t r_sent[kRing], r_count[kRing], r_flags[kRing], r_pending[kRing], r_state[kRing];
-  int32_t pcs[kPcs * 64];  // lane l's pieces at pcs[64 q + l]
-  alignas(16) uint8_t nrm[64 * kNorm];  // lane l's normalised word (generic path)
+  int32_t r_sent[kRing], r_count[kRing], r_flags[kRing], r_pending[kRing];
+  // lane l's pieces at pcs[64 q + l]; the same bytes hold lane l's normalised word (32 B at
+  // byte 32 l) while phase B loads it into registers, before any piece is written
+  alignas(16) int32_t pcs[kPcs * 64];
 };
+static_assert(kPcs * 64 * 4 >= 64 * kNorm, "normalised-word rows must fit the piece columns");
 
+// r_flags: kLenHasClsSep | sentence state
 enum : int32_t { kClosed = 1, kFallback = 2 };
 
 #ifndef LDDL_TOK_MIN_WAVES
@@ -625,48 +726,116 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
   int64_t ppos = -1;
   int64_t nb0 = -1, nb1 = -1;
 
-  auto flush = [&]() {
-    const int m = qn < 64 ? qn : 64;
-#ifdef LDDL_TOK_COUNT_FLUSH  // diagnostics: flushes and units per flush, in fb_n[1..2]
-    if (lane == 0) {
-      atomicAdd(fb_n + 1, 1u);
-      atomicAdd(fb_n + 2, (uint32_t)m);
-    }
-#endif
-    int npc = 0;
-    bool cs_flag = false;
-    int slot = -1;
-    Pcs pc{W.pcs + lane};
-    if (lane < m) {
-      slot = W.q_slot[lane];
-      npc = unit_pieces(T, s_bloom, s_ascii, text, n_bytes, W.r_b0[slot] + W.q_rel[lane], W.q_len[lane],
-                        W.q_kind[lane], W.q_slow[lane] != 0, pc, W.nrm + lane * kNorm, cs_flag);
-      if (npc < 0) {
-        atomicOr(&W.r_state[slot], kFallback);
-        npc = 0;
+  // place queue units [u0, u1) (all resolved) in order: segmented scan per sentence
+  auto place = [&](int u0, int u1) {
+    for (int r0 = u0; r0 < u1; r0 += 64) {
+      const int u = r0 + lane;
+      const bool act = u < u1;
+      const int npc = act ? W.q_npc[u] : 0;
+      const int slot = act ? W.q_slot[u] : -1;
+      const int incl = wave_incl_scan(npc);
+      const int excl = incl - npc;
+      const int prev_slot = __shfl(slot, lane > 0 ? lane - 1 : 0, 64);
+      const uint64_t F = ballot(act && (lane == 0 || slot != prev_slot));
+      const int s0 = 63 - __clzll(F & (lane == 63 ? ~0ull : ((2ull << lane) - 1)));
+      const int seg_excl = excl - __shfl(excl, s0, 64);
+      const int next_slot = __shfl(slot, lane < 63 ? lane + 1 : 63, 64);
+      const bool seg_last = act && (lane == 63 || u + 1 >= u1 || next_slot != slot);
+      if (act) {
+        const int o = W.r_count[slot] + seg_excl;
+        const int64_t bb = W.r_b0[slot];
+        const int32_t res = W.q_res[u];
+        if (res & kHardBit) {
+          const int col = res & 63;
+          for (int q = 0; q < npc; ++q)
+            if (o + q < max_pieces) ids[bb + o + q] = W.pcs[64 * q + col];
+        } else if (npc && o < max_pieces) {
+          ids[bb + o] = res;
+          const int kind = W.q_kind[u];
+          if (kind - 2 == kCls || kind - 2 == kSep) atomicOr(&W.r_flags[slot], kLenHasClsSep);
+        }
       }
+      wave_sync();
+      if (seg_last) {
+        W.r_count[slot] += seg_excl + npc;
+        W.r_pending[slot] -= lane - s0 + 1;
+      }
+      wave_sync();
     }
-    const int incl = wave_incl_scan(npc);
-    const int excl = incl - npc;
-    const int prev_slot = __shfl(slot, lane > 0 ? lane - 1 : 0, 64);
-    const uint64_t F = ballot(lane < m && (lane == 0 || slot != prev_slot));
-    const int s0 = 63 - __clzll(F & (lane == 63 ? ~0ull : ((2ull << lane) - 1)));
-    const int seg_excl = excl - __shfl(excl, s0, 64);
-    const int next_slot = __shfl(slot, lane < 63 ? lane + 1 : 63, 64);
-    const bool seg_last = lane < m && (lane == m - 1 || next_slot != slot);
-    if (lane < m) {
-      const int o = W.r_count[slot] + seg_excl;
-      const int64_t bb = W.r_b0[slot];
-      for (int q = 0; q < npc; ++q)
-        if (o + q < max_pieces) ids[bb + o + q] = pc.get(q);
-      if (cs_flag && o < max_pieces) atomicOr(&W.r_flags[slot], kLenHasClsSep);
+  };
+
+  auto flush = [&]() {
+    const int m = qn < kSF ? qn : kSF;
+    // phase A: specials and single-piece words
+    int nh = 0;
+    for (int r0 = 0; r0 < m; r0 += 64) {
+      const int u = r0 + lane;
+      bool hard = false;
+      if (u < m) {
+        const int kind = W.q_kind[u], len = W.q_len[u];
+        int32_t res = 0;
+        int npc = 1;
+        if (kind >= 2) {
+          res = T.special_id[kind - 2];
+        } else if (!W.q_slow[u] && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32) {
+          B32 v = load32(text, n_bytes, W.r_b0[W.q_slot[u]] + W.q_rel[u]);
+          if (T.ascii_mode == 1) v = B32{swar_lower(v.w0), swar_lower(v.w1), swar_lower(v.w2), swar_lower(v.w3)};
+          res = probe32(T, v, len, 0);
+          hard = res < 0;
+        } else {
+          hard = true;
+        }
+#ifdef LDDL_TOK_NO_WP  // A/B experiment only: classification + placement without WordPiece
+        hard = false;
+        res = len;
+#endif
+        if (!hard) {
+          W.q_res[u] = res;
+          W.q_npc[u] = (uint8_t)npc;
+        }
+      }
+      const uint64_t H = ballot(hard);
+      if (hard) W.h_idx[nh + (int)popc_below(H)] = (HIdx)u;
+      nh += __popcll(H);
     }
     wave_sync();
-    if (seg_last) {
-      W.r_count[slot] += seg_excl + npc;
-      W.r_pending[slot] -= lane - s0 + 1;
+    // phase B in chunks of 64 hard units, each chunk placed with the units before the next one
+    int placed = 0;
+    for (int h0 = 0; h0 < nh; h0 += 64) {
+      const int hn = nh - h0 < 64 ? nh - h0 : 64;
+      int u = -1;
+      UnitWord uw;
+      uw.status = 1;
+      bool known_miss = false;
+      if (lane < hn) {
+        u = W.h_idx[h0 + lane];
+        const int len = W.q_len[u];
+        const bool slow = W.q_slow[u] != 0;
+        known_miss = !slow && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32;
+        uw = unit_word(T, s_ascii, text, n_bytes, W.r_b0[W.q_slot[u]] + W.q_rel[u], len, slow,
+                       reinterpret_cast<uint8_t*>(W.pcs) + 32 * lane);
+      }
+      wave_sync();  // every normalised word is in registers: the rows become piece columns
+      int npc = 0;
+      if (lane < hn) {
+        Pcs pc{W.pcs + lane};
+        if (uw.status == 0) npc = wordpiece32(T, s_bloom, uw.v, uw.nb, uw.ends, pc, known_miss);
+        else if (uw.status < 0) npc = -1;
+        if (npc < 0) {  // the sentence goes to the lane kernel
+          atomicOr(&W.r_flags[W.q_slot[u]], kFallback);
+          npc = 0;
+        }
+        W.q_res[u] = kHardBit | lane;
+        W.q_npc[u] = (uint8_t)npc;
+      }
+      wave_sync();
+      const int lim = h0 + 64 < nh ? (int)W.h_idx[h0 + 64] : m;
+      place(placed, lim);
+      placed = lim;
     }
-    // drop the processed units from the queue (sources [64, qn) never overlap targets [0, qn-64))
+    place(placed, m);
+    // drop the processed units from the queue (sources [m, qn) never overlap targets [0, qn-m)
+    // when qn - m <= 64 <= m; otherwise m == kSF and qn - m <= 63 < kSF)
     const int rest = qn - m;
     int32_t rel = 0;
     uint8_t ql = 0, qk = 0, qs = 0, qw = 0;
@@ -692,12 +861,13 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
   auto retire = [&]() {
     while (head < tail) {
       const int sl = (int)(head % kRing);
-      const int st = W.r_state[sl];
+      const int st = W.r_flags[sl];
       if (!(st & kClosed) || W.r_pending[sl] > 0) break;
       if (lane == 0) {
         const int32_t sid = W.r_sent[sl];
         if (st & kFallback) fb_list[atomicAdd(fb_n, 1u)] = sid;
-        else sent_len[sid] = (W.r_count[sl] < max_pieces ? W.r_count[sl] : max_pieces) | W.r_flags[sl];
+        else
+          sent_len[sid] = (W.r_count[sl] < max_pieces ? W.r_count[sl] : max_pieces) | (st & kLenHasClsSep);
       }
       ++head;
     }
@@ -732,7 +902,6 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
         W.r_count[cur_slot] = 0;
         W.r_flags[cur_slot] = 0;
         W.r_pending[cur_slot] = 0;
-        W.r_state[cur_slot] = 0;
       }
       wave_sync();
       pos = b0;
@@ -752,7 +921,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
       }
 #endif
       if (R.fallback) {
-        if (lane == 0) W.r_state[cur_slot] |= kFallback;
+        if (lane == 0) W.r_flags[cur_slot] |= kFallback;
         pos = b1;
       } else {
         const int n = R.n_units;
@@ -773,11 +942,11 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
       }
     }
     if (pos >= b1) {
-      if (lane == 0) W.r_state[cur_slot] |= kClosed;
+      if (lane == 0) W.r_flags[cur_slot] |= kClosed;
       wave_sync();
       cur = false;
     }
-    if (qn >= 64) {
+    if (qn >= kSF) {
       flush();
       // the open sentence already has max_pieces pieces: the rest of it cannot be kept
       if (cur && W.r_count[cur_slot] >= max_pieces) pos = b1;
