@@ -374,6 +374,9 @@ def main():
                     help='C5 loader bins (64 -> 8 bins, the reference example local_example.sh)')
     ap.add_argument('--c5-workers', type=int, default=2,
                     help='DataLoader workers per bin (= shards per bin of the C5 dataset)')
+    ap.add_argument('--chunks', type=int, default=1,
+                    help='c2: split the step into partition-aligned chunks, tokenizing chunk k+1 '
+                         'on a side stream under chunk k\'s pair planner')
     ap.add_argument('--seed', type=int, default=1234)
     ap.add_argument('--gen-threads', type=int, default=16)
     ap.add_argument('--cpu-sample-bytes', type=int, default=48 << 20)
@@ -423,6 +426,8 @@ def main():
 
     def step(ev=None, rng=args.rng, b=None):
         b = base if b is None else b
+        if args.chunks > 1 and args.workload == 'c2':
+            return step_chunked(ev, rng, b)
         if ev is not None:
             ev[0].record()
         ids, sent_len = ctx.tokenize(b['text'], b['sent_off'])
@@ -444,6 +449,27 @@ def main():
               'kept_sent': pb.n_kept_sentences, 'kept_doc': pb.n_kept_documents}
         del pb  # nothing of a step outlives it (HBM is reused by the next step)
         return n_tok, st, sent_len
+
+    def step_chunked(ev, rng, b):
+        """The same step with tokenization of chunk k+1 pipelined under the pairs of chunk k
+        (lddl_amd.pairs.tokenize_and_pair_chunked); tokenize_ms then spans only chunk 0."""
+        from lddl_amd.pairs import tokenize_and_pair_chunked
+        if ev is not None:
+            ev[0].record()
+            ev[1].record()
+        pbs = tokenize_and_pair_chunked(ctx, b['text'], b['sent_off'], doc_off, b['part_off'],
+                                        b['part_seed'], n_chunks=args.chunks, seq=args.seq, dup=5,
+                                        masking=True, short_seq_prob=0.1, masked_lm_ratio=0.15,
+                                        rng=rng)
+        if ev is not None:
+            ev[2].record()
+        n_tok = sum(int(p.tokens.numel()) + 3 * p.n_pairs for p in pbs)
+        st = {'pairs': sum(p.n_pairs for p in pbs), 'masked': sum(p.n_masked for p in pbs),
+              'plan_ms': sum(p.plan_ms for p in pbs), 'tokens': n_tok,
+              'kept_sent': sum(p.n_kept_sentences for p in pbs),
+              'kept_doc': sum(p.n_kept_documents for p in pbs)}
+        del pbs
+        return n_tok, st, None
 
     def timed(rng, b=None, pcie=None):
         """W untimed steps, then exactly K steps between barrier + synchronize; max over ranks.
@@ -540,6 +566,13 @@ def main():
     plan_ms = float(np.mean([s['plan_ms'] for s in stats]))
     st = stats[-1]
     n_pairs = st['pairs']
+    if sent_len is None:  # chunked step: the tokenizer's own launch, timed once more (untimed step)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _, sent_len = ctx.tokenize(text, sent_off)
+        e1.record()
+        torch.cuda.synchronize()
+        tok_ms = e0.elapsed_time(e1)
     pieces = int((sent_len & ((1 << 30) - 1)).sum())
     bal_ms = None
     if args.workload == 'c4':  # one more, untimed step with the balance phases timed

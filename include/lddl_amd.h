@@ -80,6 +80,15 @@ int lddl_tokenize(lddl_ctx* ctx, void* stream, const uint8_t* d_text, int64_t n_
                   int32_t* d_sent_len);
 
 /* ---------------------------------------------------------------------------------------------
+ * UTF-8 validation (the strict decode dask.bag.read_text applies to every input block, readers.py
+ * :60-71; the reference raises UnicodeDecodeError on malformed input): *d_first_bad (device int64)
+ * = offset of the first byte that does not begin or continue a well-formed sequence (Python's
+ * decoder rules: no overlongs, surrogates or > U+10FFFF), or 0x7F7F7F7F7F7F7F7F if all of
+ * d_text[0 .. n_bytes) is valid. Asynchronous on `stream`.
+ * ------------------------------------------------------------------------------------------- */
+int lddl_utf8_check(void* stream, const uint8_t* d_text, int64_t n_bytes, int64_t* d_first_bad);
+
+/* ---------------------------------------------------------------------------------------------
  * Punkt sentence segmentation (device in, device out).
  * Replaces `nltk.tokenize.sent_tokenize(text)` + `strip()` + dropping empty sentences
  * (lddl/dask/bert/pretrain.py:86-88) for every document of a batch: nltk 3.6.5's

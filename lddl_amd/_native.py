@@ -6,6 +6,12 @@ There is no fallback: if the library is missing the import fails loudly. Build i
 import ctypes
 import os
 
+# torch first: its HIP runtime (torch/lib/libamdhip64.so, soname libamdhip64.so.7) must be the
+# process's one runtime. Loaded the other way round, liblddl_amd.so would bring in
+# /opt/rocm/lib/libamdhip64.so.7 and torch (which asks for "libamdhip64.so") a second copy, and
+# the two HIP runtimes do not share devices ("no ROCm-capable device is detected").
+import torch  # noqa: F401,E402
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('LDDL_AMD_LIB') or os.path.join(_HERE, '_lib', 'liblddl_amd.so')
 
@@ -49,6 +55,7 @@ SIGNATURES = {
     'lddl_collate_encode': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_i64]),
+    'lddl_utf8_check': (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),
     'lddl_collate_count': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
     'lddl_collate_encode_masked': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32,
                                                   c_i32, c_vp, c_vp, c_vp, c_vp, ctypes.c_float,

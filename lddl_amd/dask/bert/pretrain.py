@@ -85,10 +85,11 @@ def plan_partitions(args):
     return blocks
 
 
-def iter_batches(args, rank=0, world=1, blocks=None):
+def iter_batches(args, rank=0, world=1, blocks=None, as_bytes=False):
     """This rank's partitions in GPU batches of <= --gpu-batch-bytes of input, read lazily:
     yields [(p, lines)] per batch, the documents shuffled over the batch's partitions (each keeps
-    its document count) by Random(partition_seed(seed, -1 - first partition of the batch))."""
+    its document count) by Random(partition_seed(seed, -1 - first partition of the batch)).
+    as_bytes: lines as UTF-8 bytes (the GPU segmenter's input) instead of str."""
     blocks = plan_partitions(args) if blocks is None else blocks
     mine = [p for p in range(len(blocks)) if p % world == rank]
     cur, size = [], 0
@@ -103,7 +104,7 @@ def iter_batches(args, rank=0, world=1, blocks=None):
     if cur:
         groups.append(cur)
     for g in groups:
-        parts = [(p, readers.read_block(blocks[p])) for p in g]
+        parts = [(p, readers.read_block(blocks[p], as_bytes=as_bytes)) for p in g]
         docs = [d for _, lines in parts for d in lines]
         random.Random(partition_seed(args.seed, -1 - g[0])).shuffle(docs)
         out, k = [], 0
@@ -121,6 +122,8 @@ def get_partitions(args, rank=0, world=1):
 def _segment_docs(lines):
     out = []
     for raw in lines:
+        if isinstance(raw, bytes):
+            raw = raw.decode('utf-8')
         _, sents = segment.document_sentences(raw)
         out.append([s.encode('utf-8') for s in sents])
     return out
@@ -161,11 +164,13 @@ def build_doc_corpus(partitions):
     chunks, part_nd = [], []
     for _, lines in partitions:
         part_nd.append(len(lines))
-        for raw in lines:
-            chunks.append(readers.split_id_text(raw)[1].encode('utf-8'))
+        if lines and isinstance(lines[0], bytes):
+            chunks += [readers.split_id_text_bytes(raw)[1] for raw in lines]
+        else:
+            chunks += [readers.split_id_text(raw)[1].encode('utf-8') for raw in lines]
     text = np.frombuffer(b''.join(chunks), np.uint8) if chunks else np.zeros(0, np.uint8)
     doc_off = np.zeros(len(chunks) + 1, np.int64)
-    np.cumsum([len(c) for c in chunks], out=doc_off[1:])
+    np.cumsum(np.fromiter(map(len, chunks), np.int64, len(chunks)), out=doc_off[1:])
     part_doc_off = np.zeros(len(part_nd) + 1, np.int64)
     np.cumsum(part_nd, out=part_doc_off[1:])
     return 'documents', text, doc_off, part_doc_off
@@ -197,6 +202,11 @@ def make_batch_pairs(ctx, args, partitions, corpus, timer=None):
             1, dtype=torch.uint8, device=dev)[:0]
         d_doc = torch.from_numpy(doc_off).to(dev)
         tm('h2d')
+        bad = punkt.utf8_first_invalid(d_text)
+        if bad >= 0:  # dask.bag.read_text decodes strictly: the reference raises here too
+            raise UnicodeDecodeError('utf-8', bytes(text[max(bad - 8, 0):bad + 8]), 0, 1,
+                                     'invalid UTF-8 in the input documents (byte {} of the '
+                                     'batch text)'.format(bad))
         d_so, d_dso = punkt.segment(ctx, d_text, d_doc)
         tm('segment')
     else:
@@ -218,8 +228,9 @@ def make_batch_pairs(ctx, args, partitions, corpus, timer=None):
     return pb
 
 
-def process_batch(ctx, args, partitions, corpus, outdir, timer=None):
-    """Run the GPU hot path over a group of partitions and write their files."""
+def process_batch(ctx, args, partitions, corpus, outdir, timer=None, executor=None, futures=None):
+    """Run the GPU hot path over a group of partitions and write their files (concurrently on
+    `executor` when given: the futures go to `futures`)."""
     from ... import output
     tm = timer or (lambda name: None)
     pb = make_batch_pairs(ctx, args, partitions, corpus, timer)
@@ -237,7 +248,8 @@ def process_batch(ctx, args, partitions, corpus, outdir, timer=None):
         rd = output.render(ctx, pb)
     tm('render')
     if args.output_format == 'parquet':
-        paths = output.write_parquet(outdir, rd, part_rows, index, args.masking, nbins, counts)
+        paths = output.write_parquet(outdir, rd, part_rows, index, args.masking, nbins, counts,
+                                     executor=executor, futures=futures)
     else:
         paths = write_txt(outdir, rd, part_rows, index, args.masking, nbins, counts,
                           getattr(args, 'n_partitions', len(part_rows) - 1))
@@ -290,7 +302,7 @@ def write_txt(outdir, rd, part_rows, index, masking, nbins, counts, n_part):
     return paths
 
 
-def write_balanced(ctx, args, bb, outdir, binned):
+def write_balanced(ctx, args, bb, outdir, binned, executor=None, futures=None):
     """This rank's balanced shards: `shard-<k>.parquet_<b>` per bin (binned) or
     `shard-<k>.parquet`, the load balancer's names (load_balance.py:90-92)."""
     import torch
@@ -309,7 +321,11 @@ def write_balanced(ctx, args, bb, outdir, binned):
             r1 = r0 + int(bb.shard_counts[m, b])
             fn = os.path.join(outdir, 'shard-{}.parquet{}'.format(s, '_{}'.format(b) if binned
                                                                  else ''))
-            output.write_table(rd, r0, r1, args.masking, binned, fn)
+            if executor is None:
+                output.write_table(rd, r0, r1, args.masking, binned, fn)
+            else:
+                futures.append(executor.submit(output.write_table, rd, r0, r1, args.masking,
+                                               binned, fn))
             paths.append(fn)
             r0 = r1
     return paths
@@ -324,6 +340,32 @@ def num_samples_of_shards(bb, binned):
             out['shard-{}.parquet{}'.format(s, '_{}'.format(b) if binned else '')] = int(
                 bb.all_shard_counts[s, b])
     return out
+
+
+def _prefetch(gen, depth=1):
+    """Iterate `gen` in a background thread, `depth` items ahead (the host read / decode of batch
+    k+1 overlaps the GPU work and the file writes of batch k). Exceptions are re-raised here."""
+    import queue
+    import threading
+    q = queue.Queue(maxsize=depth)
+    done = object()
+
+    def run():
+        try:
+            for item in gen:
+                q.put(item)
+        except BaseException as e:  # noqa: B902 - handed to the consumer
+            q.put(e)
+            return
+        q.put(done)
+    threading.Thread(target=run, daemon=True).start()
+    while True:
+        item = q.get()
+        if item is done:
+            return
+        if isinstance(item, BaseException):
+            raise item
+        yield item
 
 
 class _StageTimer:
@@ -366,7 +408,7 @@ def main(args):
     outdir = expand_outdir_and_mkdir(args.sink)
     blocks = plan_partitions(args)
     args.n_partitions = len(blocks)
-    batches = iter_batches(args, rank, world, blocks)
+    batches = iter_batches(args, rank, world, blocks, as_bytes=args.sentence_splitter == 'gpu')
     if args.sentence_splitter == 'host':
         # host segmentation first: its process pool forks before this process touches the GPU
         batches = [(b, ('sentences',) + build_corpus(b, args.local_n_workers)) for b in batches]
@@ -384,16 +426,29 @@ def main(args):
         from ... import punkt
         punkt.set_params(ctx, punkt_params(args))
     timer = _StageTimer(args.profile_stages)
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(max_workers=max(1, args.write_threads))
+    if args.sentence_splitter == 'gpu':
+        batches = _prefetch(batches)
     timer.mark()
     n_files = 0
     kept = []
+    pending = []  # writes of the previous batch (at most two batches of rendered rows in memory)
     for batch, corpus in batches:
         timer('read')
         if args.num_shards is None:
-            n_files += len(process_batch(ctx, args, batch, corpus, outdir, timer))
+            futs = []
+            n_files += len(process_batch(ctx, args, batch, corpus, outdir, timer, pool, futs))
+            for f in pending:
+                f.result()
+            pending = futs
+            timer('write_wait')
         else:
             kept.append(make_batch_pairs(ctx, args, batch, corpus, timer))
         timer.mark()
+    for f in pending:
+        f.result()
+    timer('write_wait')
     if args.num_shards is not None:
         from ...balance import balance
         from ...pairs import cat_pair_batches, PairBatch
@@ -415,11 +470,15 @@ def main(args):
         nbins = args.target_seq_length // bin_size
         bb = balance(ctx, pb, bin_size, nbins, num_shards=args.num_shards)
         timer('balance')
-        n_files += len(write_balanced(ctx, args, bb, outdir, binned))
+        futs = []
+        n_files += len(write_balanced(ctx, args, bb, outdir, binned, pool, futs))
+        for f in futs:
+            f.result()
         timer('render+write')
         if rank == 0:
             with open(os.path.join(outdir, '.num_samples.json'), 'w') as f:
                 json.dump(num_samples_of_shards(bb, binned), f)
+    pool.shutdown()
     if world > 1:
         dist.barrier()
     if rank == 0 and args.num_shards is None and args.output_format == 'parquet':
@@ -501,6 +560,9 @@ def attach_args(parser=None):
                         help='lddl_amd: balance in HBM across all ranks (RCCL) and write the '
                              "load balancer's layout (shard-<k>.parquet[_<b>] with N or N+1 "
                              'samples per bin + .num_samples.json) instead of part.* files')
+    parser.add_argument('--write-threads', type=int, default=min(os.cpu_count() or 1, 16),
+                        help='lddl_amd: parquet files written concurrently (threads). Default: '
+                             'min(cpus, 16)')
     attach_bool_arg(parser, 'profile-stages', default=False,
                     help_str='lddl_amd: print device-synchronised seconds per stage (read, h2d, '
                     'segment, tokenize, pairs, render, write, balance)')

@@ -16,6 +16,7 @@ torchrun every rank holds its own share of the corpus, not all of it.
 """
 import os
 import random
+import re
 from dataclasses import dataclass
 
 
@@ -111,13 +112,29 @@ def plan_blocks(path, blocksize=None, sample_ratio=1.0, sample_seed=12345):
     return blocks
 
 
-def read_block(blk):
-    """The partition's lines: stripped, non-empty, sampled (readers.py:60-71)."""
+def _strip_bytes(raw):
+    """str(raw).strip() as UTF-8 bytes. bytes.strip() removes ASCII whitespace only; a line whose
+    remaining first or last byte could be other whitespace (\\x1c-\\x1f, non-ASCII: U+0085,
+    U+00A0, U+2000.., U+3000 ...) takes the exact str path."""
+    s = raw.strip()
+    if s and (s[0] >= 0x80 or s[-1] >= 0x80 or 0x1c <= s[0] <= 0x1f or 0x1c <= s[-1] <= 0x1f):
+        return raw.decode('utf-8').strip().encode('utf-8')
+    return s
+
+
+def read_block(blk, as_bytes=False):
+    """The partition's lines: stripped, non-empty, sampled (readers.py:60-71). as_bytes: the
+    lines as bytes, for the GPU path, which validates them as UTF-8 on the device
+    (lddl_utf8_check) instead of decoding the corpus into Python strings."""
     if blk.nbytes == 0:
         return []
     with open(blk.path, 'rb') as f:
         f.seek(blk.start)
-        lines = _filter(f.read(blk.end - blk.start).split(b'\n'))
+        data = f.read(blk.end - blk.start)
+    if as_bytes:
+        lines = [x for x in map(_strip_bytes, data.split(b'\n')) if x]
+    else:
+        lines = _filter(data.split(b'\n'))
     if blk.state is None:
         return lines
     r = random.Random()
@@ -180,9 +197,24 @@ def read_open_webtext(path, blocksize=None, sample_ratio=1.0, sample_seed=12345)
     return read_bag_of_text(path, blocksize, sample_ratio, sample_seed)
 
 
+_WS = re.compile(r'\s')  # str patterns: \s is exactly str.isspace()
+_WS_ASCII_B = re.compile(rb'[\t-\r\x1c-\x20]')
+
+
 def split_id_text(raw_text):
     """readers.py:131-136: id = chars up to the first whitespace char; text = the rest after it."""
-    i = 0
-    while i < len(raw_text) and not raw_text[i].isspace():
-        i += 1
-    return raw_text[:i], raw_text[i + 1:]
+    m = _WS.search(raw_text)
+    if m is None:
+        return raw_text, ''
+    return raw_text[:m.start()], raw_text[m.start() + 1:]
+
+
+def split_id_text_bytes(raw):
+    """split_id_text on a UTF-8 line, as bytes. Fast path: the first ASCII whitespace byte, when
+    no non-ASCII byte comes before it (a non-ASCII char could itself be whitespace)."""
+    m = _WS_ASCII_B.search(raw)
+    i = len(raw) if m is None else m.start()
+    if max(raw[:i], default=0) < 0x80:
+        return raw[:i], raw[i + 1:]
+    a, b = split_id_text(raw.decode('utf-8'))
+    return a.encode('utf-8'), b.encode('utf-8')

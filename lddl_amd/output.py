@@ -130,8 +130,10 @@ def render(ctx, pb, rows=None, bin_id=None):
     num_tokens = sel((pb.tok_off[1:] - pb.tok_off[:-1]) + 3)
     is_rn = sel(pb.is_random_next)
 
-    def host(t, k):
-        return t[:k].cpu().numpy()
+    def host(t, k):  # pinned staging (torch's caching host allocator): full-rate D2H
+        h = torch.empty(max(k, 1), dtype=t.dtype, pin_memory=True)[:k]
+        h.copy_(t[:k])
+        return h.numpy()
 
     out = Rendered(a_off.cpu().numpy(), host(bufs[0], tot[0]), b_off.cpu().numpy(),
                    host(bufs[1], tot[1]), is_rn.cpu().numpy().astype(bool),
@@ -212,26 +214,33 @@ def write_dataset_metadata(outdir, n_part, nbins=None):
 
 
 def write_parquet(outdir, rd, part_rows, part_index, masking, nbins=None, bin_counts=None,
-                  compression=DEFAULT_COMPRESSION):
+                  compression=DEFAULT_COMPRESSION, executor=None, futures=None):
     """Write the reference's files for a group of partitions.
 
     part_rows: int64 [n_part + 1] row ranges of the partitions inside `rd`; part_index: global
     partition number of each (file name part.<i>.parquet); when binned, bin_counts[p, b] are the
-    rows of (p, b), laid out bin after bin inside the partition's range."""
+    rows of (p, b), laid out bin after bin inside the partition's range. With an `executor`
+    (threads: pyarrow encodes and writes without the GIL) the files are written concurrently and
+    the futures appended to `futures`; the caller waits for them."""
     paths = []
+
+    def put(r0, r1, binned, fn):
+        if executor is None:
+            write_table(rd, r0, r1, masking, binned, fn, compression)
+        else:
+            futures.append(executor.submit(write_table, rd, r0, r1, masking, binned, fn,
+                                           compression))
+        paths.append(fn)
     for p in range(len(part_rows) - 1):
         r0, r1 = int(part_rows[p]), int(part_rows[p + 1])
         name = os.path.join(outdir, 'part.{}.parquet'.format(part_index[p]))
         if nbins is None:
-            pq.write_table(table(rd, r0, r1, masking, False), name, compression=compression)
-            paths.append(name)
+            put(r0, r1, False, name)
             continue
         b0 = r0
         for b in range(nbins):
             b1 = b0 + int(bin_counts[p, b])
-            fn = '{}_{}'.format(name, b)
-            pq.write_table(table(rd, b0, b1, masking, True), fn, compression=compression)
-            paths.append(fn)
+            put(b0, b1, True, '{}_{}'.format(name, b))
             b0 = b1
         assert b0 == r1
     return paths

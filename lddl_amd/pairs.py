@@ -115,3 +115,55 @@ def make_pairs(ctx, sent_off, ids, sent_len, doc_sent_off, part_doc_off, part_se
         lib.lddl_pairs_destroy(h, st)
     return PairBatch(tokens, tok_off, len_a, is_rn, pos, labels, pos_off, int(counts[3]),
                      int(counts[4]), part_off, float(ms.value), n_mask)
+
+
+_SIDE = {}
+
+
+def _side_stream(dev):
+    """One persistent side stream per device: the caching allocator keeps per-stream pools, so
+    a fresh stream per call would never reuse the previous call's blocks."""
+    key = torch.device(dev).index
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
+
+
+def tokenize_and_pair_chunked(ctx, text, sent_off, doc_sent_off, part_doc_off, part_seed,
+                              n_chunks=2, max_pieces=512, tok_stream=None, **pair_kw):
+    """tokenize + make_pairs over `n_chunks` partition-aligned chunks, pipelined on two streams:
+    every chunk's tokenizer is queued on a side stream, each chunk's pair planner on the current
+    stream waits only for its own chunk's tokens, so chunk k+1 is tokenized while chunk k is
+    planned and gathered. Partitions are independent (per-partition seeds), so the result is
+    bit-identical to one call over all partitions. Returns the chunks' PairBatch list in
+    partition order."""
+    n_part = part_doc_off.numel() - 1
+    cuts = [round(k * n_part / n_chunks) for k in range(n_chunks + 1)]
+    pc = torch.tensor(cuts, dtype=torch.int64, device=part_doc_off.device)
+    d_cut = part_doc_off.index_select(0, pc)
+    s_cut = doc_sent_off.index_select(0, d_cut)
+    b_cut = sent_off.index_select(0, s_cut)
+    d_cut, s_cut, b_cut = d_cut.tolist(), s_cut.tolist(), b_cut.tolist()
+    main = torch.cuda.current_stream()
+    side = tok_stream or _side_stream(text.device)
+    side.wait_stream(main)
+    toks = []
+    with torch.cuda.stream(side):
+        for k in range(n_chunks):
+            t = text[b_cut[k]:b_cut[k + 1]]
+            so = sent_off[s_cut[k]:s_cut[k + 1] + 1] - b_cut[k]
+            ids, sl = ctx.tokenize(t, so, max_pieces)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            toks.append((so, ids, sl, ev))
+    out = []
+    for k, (so, ids, sl, ev) in enumerate(toks):
+        main.wait_event(ev)
+        for x in (so, ids, sl):
+            x.record_stream(main)
+        pb = make_pairs(ctx, so, ids, sl, doc_sent_off[d_cut[k]:d_cut[k + 1] + 1] - s_cut[k],
+                        part_doc_off[cuts[k]:cuts[k + 1] + 1] - d_cut[k],
+                        part_seed[cuts[k]:cuts[k + 1]], **pair_kw)
+        del ids
+        out.append(pb)
+    return out

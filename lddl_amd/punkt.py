@@ -112,6 +112,15 @@ def segment(ctx, text, doc_off):
     return sent_off, doc_sent_off
 
 
+def utf8_first_invalid(text):
+    """Offset of the first malformed UTF-8 byte of a uint8 cuda tensor, or -1 (lddl_utf8_check)."""
+    from .context import _ptr, _stream
+    out = torch.empty(1, dtype=torch.int64, device=text.device)
+    check(lib.lddl_utf8_check(_stream(), _ptr(text), text.numel(), _ptr(out)))
+    v = int(out.item())
+    return -1 if v >= text.numel() else v
+
+
 def stripped_sentences(text, sent_off, doc_sent_off):
     """Host helper (tests, debugging): the sentences as the reference sees them, per document:
     decoded, strip()ped, empty ones dropped (pretrain.py:86-88)."""

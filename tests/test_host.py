@@ -107,7 +107,7 @@ def test_ranks_read_only_their_blocks(tmp_path, monkeypatch):
                                        '--sample-ratio', '1.0', '--gpu-batch-bytes', '3000'])
     seen = []
     orig = R.read_block
-    monkeypatch.setattr(R, 'read_block', lambda b: seen.append(b.start) or orig(b))
+    monkeypatch.setattr(R, 'read_block', lambda b, **kw: seen.append(b.start) or orig(b, **kw))
     parts = {}
     for rank in range(3):
         seen.clear()

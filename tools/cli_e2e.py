@@ -1,0 +1,68 @@
+"""End-to-end `preprocess_bert_pretrain` timing (SURVEY 8f2 / BASELINE C1): synthetic
+`<id> <text>` documents written as the reference's source layout, then the CLI with
+--profile-stages (device-synchronised seconds per stage: read = host file read + decode + line
+split + doc corpus build, h2d, segment (GPU Punkt), tokenize, pairs, render, write (pyarrow)).
+
+    python tools/cli_e2e.py --bytes 100e6 [--seq 128] [--bin-size N] [--num-blocks 128]
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--bytes', type=float, default=100e6)
+    ap.add_argument('--seq', type=int, default=128)
+    ap.add_argument('--bin-size', type=int, default=None)
+    ap.add_argument('--num-blocks', type=int, default=128)
+    ap.add_argument('--masking', action='store_true', default=True)
+    ap.add_argument('--files', type=int, default=16)
+    ap.add_argument('--num-shards', type=int, default=None)
+    a = ap.parse_args()
+    from lddl_amd import synth
+    from lddl_amd.dask.bert import pretrain as P
+    root = tempfile.mkdtemp(prefix='lddl_e2e_', dir=os.environ.get('TMPDIR', '/tmp'))
+    try:
+        t0 = time.perf_counter()
+        text, doc_off = synth.generate_doc_text(seed=1234, n_bytes=int(a.bytes), nonascii_frac=0.01,
+                                                threads=16)
+        src = os.path.join(root, 'source', 'en')
+        os.makedirs(src)
+        n_doc = len(doc_off) - 1
+        per = (n_doc + a.files - 1) // a.files
+        for f in range(a.files):
+            with open(os.path.join(src, 'wiki_{}.txt'.format(f)), 'wb') as fh:
+                for d in range(f * per, min(n_doc, (f + 1) * per)):
+                    fh.write(b'wiki-%d ' % d + text[doc_off[d]:doc_off[d + 1]].tobytes() + b'\n')
+        gen_s = time.perf_counter() - t0
+        src_bytes = sum(os.path.getsize(os.path.join(src, x)) for x in os.listdir(src))
+        argv = ['--schedule', 'local', '--wikipedia', os.path.join(root, 'source'), '--sink',
+                os.path.join(root, 'out'), '--target-seq-length', str(a.seq), '--num-blocks',
+                str(a.num_blocks), '--vocab-file',
+                os.path.join(REPO, 'lddl_amd', 'assets', 'vocab_synth_uncased_30522.txt'),
+                '--profile-stages'] + (['--masking'] if a.masking else []) + (
+                    ['--bin-size', str(a.bin_size)] if a.bin_size else []) + (
+                    ['--num-shards', str(a.num_shards)] if a.num_shards else [])
+        import torch  # noqa: F401  (first import outside the clock)
+        t1 = time.perf_counter()
+        P.main(P.attach_args().parse_args(argv))
+        wall = time.perf_counter() - t1
+        out = os.path.join(root, 'out')
+        out_bytes = sum(os.path.getsize(os.path.join(out, x)) for x in os.listdir(out))
+        print(json.dumps({'source_bytes': src_bytes, 'documents': n_doc, 'cli_wall_s': wall,
+                          'source_MB_per_s': src_bytes / wall / 1e6, 'output_bytes': out_bytes,
+                          'generate_s': gen_s, 'argv': argv[argv.index('--target-seq-length'):]}))
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
+if __name__ == '__main__':
+    main()
