@@ -419,7 +419,8 @@ struct PlanArgs {
   int32_t* nmask;      // per slot
   int32_t* mtok;       // mask pool: slot s's decisions at moff[s] .. + nmask[s] (shuffled order)
   int64_t* moff;       // per slot
-  uint16_t* jpool;     // draw pool: j_i of random.shuffle(cand_indexes) at joff[s] + i
+  void* jpool;         // draw pool: j_i of random.shuffle(cand_indexes) at joff[s] + i
+  int32_t jbytes;      // 1 (target_seq_length <= 256: every j_i < 256) or 2 bytes per draw
   int64_t* joff;       // per slot
   int32_t* ncand;      // per slot: candidates (len(A) + len(B) minus literal [CLS]/[SEP])
   unsigned long long* pool_used;  // [0] masks, [1] overflow flag, [2] draws
@@ -620,14 +621,21 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
           }
           const int64_t mb = pool_cur, jb = jpool_cur;
           pool_cur += (num + 7) & ~7;  // 16-byte aligned regions (fy_resolve_kernel's uint4 I/O)
-          jpool_cur += (nc + 7) & ~7;
+          jpool_cur += (nc + 15) & ~15;  // 16-byte aligned for 1-byte draws too
           const bool fits = pool_end <= A.pool_cap && jpool_end <= A.jpool_cap;
           if (!fits && leader) *A.overflow = 1;
           // random.shuffle(cand_indexes): draws j_i (i = nc-1 .. 1) to the pool
-          uint16_t* jd = A.jpool + jb;
-          rng.fy_draws(nc, [&](int64_t i, uint32_t j) {
-            if (fits) jd[i] = (uint16_t)j;
-          });
+          if (A.jbytes == 1) {
+            uint8_t* jd = static_cast<uint8_t*>(A.jpool) + jb;
+            rng.fy_draws(nc, [&](int64_t i, uint32_t j) {
+              if (fits) jd[i] = (uint8_t)j;
+            });
+          } else {
+            uint16_t* jd = static_cast<uint16_t*>(A.jpool) + jb;
+            rng.fy_draws(nc, [&](int64_t i, uint32_t j) {
+              if (fits) jd[i] = (uint16_t)j;
+            });
+          }
           STAMP_ADD(2, st_t);
           // decisions of the masked candidates in shuffled order (pretrain.py:208-221)
           for (int32_t c0 = 0; c0 < num; c0 += 64) {
@@ -1178,7 +1186,7 @@ struct ResolveArgs {
   const int32_t* ncand;
   const int64_t* moff;
   const int64_t* joff;
-  const uint16_t* jpool;
+  const void* jpool;   // 1- or 2-byte draws (the kernel's D)
   uint16_t* mpos;
   const int64_t* kscan;
   const int32_t* dense;
@@ -1214,10 +1222,13 @@ struct LaneCol<uint8_t> {
   }
 };
 
-// NG > 0: all of a pair's draws (nc <= 8 NG) are loaded up front, NG uint4 in flight per lane
-template <typename T, int NG>
+// D: draw type (uint8_t for target_seq_length <= 256, else uint16_t); a uint4 holds 16 / sizeof(D)
+// draws. NG > 0: all of a pair's draws (nc <= NG * 16 / sizeof(D)) are loaded up front, NG uint4
+// in flight per lane.
+template <typename T, typename D, int NG>
 __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_xb[];
+  constexpr int kPerVec = 16 / (int)sizeof(D);  // draws per uint4
   const int lane = threadIdx.x;
   LaneCol<T> x{reinterpret_cast<T*>(s_xb), lane};
   const int64_t q = (int64_t)blockIdx.x * 64 + lane;
@@ -1226,22 +1237,23 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   const int32_t num = R.nmask[slot];
   if (num <= 0) return;
   const int32_t nc = R.ncand[slot];
-  const int64_t jb = R.joff[slot], mb = R.moff[slot];  // both multiples of 8 (planner)
+  const int64_t jb = R.joff[slot], mb = R.moff[slot];  // multiples of 16 / 8 (planner)
   const PairDesc d = R.desc[slot];
   const int32_t na = d.na, nb = d.nb_rn & 0x7FFFFFFF;
   const bool fast = nc == na + nb;
   x.iota(nc);
-  const uint4* jp = reinterpret_cast<const uint4*>(R.jpool + jb);
+  const uint4* jp = reinterpret_cast<const uint4*>(static_cast<const D*>(R.jpool) + jb);
   uint4* mp = reinterpret_cast<uint4*>(R.mpos + mb);
   uint4 acc = make_uint4(0u, 0u, 0u, 0u);  // slots [8h, 8h+8) collected from the top down
-  // step i of group h: swap, or (i < num) finalise slot i
-  auto group = [&](int h, const uint4& jv) {
-    const uint32_t jw[4] = {jv.x, jv.y, jv.z, jv.w};
+  // steps [8h, 8h+8): swap, or (i < num) finalise slot i; w = the two (1-byte draws) or four
+  // (2-byte draws) dwords holding their draws
+  auto group = [&](int h, const uint32_t* w) {
 #pragma unroll
     for (int u = 7; u >= 0; --u) {
       const int i = 8 * h + u;
       if (i >= nc) continue;
-      const int j = (int)((jw[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
+      const int j = sizeof(D) == 1 ? (int)((w[u >> 2] >> (8 * (u & 3))) & 0xFFu)
+                                   : (int)((w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
       const uint32_t xi = x.get(i);
       if (i >= num) {
         if (i >= 1) x.set(j, xi);
@@ -1256,20 +1268,31 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
     }
     if (8 * h < num) mp[h] = acc;  // slots [8h, 8h+8) complete (the top group zero-padded)
   };
+  // one uint4 of draws = kPerVec / 8 groups of 8 steps, processed top down
+  auto vec = [&](int g, const uint4& v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if (sizeof(D) == 1) {
+      if (16 * g + 8 < nc) group(2 * g + 1, w + 2);
+      group(2 * g, w);
+    } else {
+      group(g, w);
+    }
+  };
+  const int nvec = (nc + kPerVec - 1) / kPerVec;
   if (NG > 0) {
     uint4 jv[NG > 0 ? NG : 1];
 #pragma unroll
     for (int g = 0; g < NG; ++g)
-      if (8 * g < nc) jv[g] = jp[g];
+      if (g < nvec) jv[g] = jp[g];
 #pragma unroll
-    for (int h = NG - 1; h >= 0; --h)
-      if (8 * h < nc) group(h, jv[h]);
+    for (int g = NG - 1; g >= 0; --g)
+      if (g < nvec) vec(g, jv[g]);
   } else {
-    uint4 nxt = jp[(nc - 1) >> 3];
-    for (int h = (nc - 1) >> 3; h >= 0; --h) {
+    uint4 nxt = jp[nvec - 1];
+    for (int g = nvec - 1; g >= 0; --g) {
       const uint4 jv = nxt;
-      if (h > 0) nxt = jp[h - 1];  // next group of draws in flight
-      group(h, jv);
+      if (g > 0) nxt = jp[g - 1];  // next vector of draws in flight
+      vec(g, jv);
     }
   }
   if (!fast) {  // literal [CLS]/[SEP] in the pair: candidate index -> position via the tokens
@@ -1675,7 +1698,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   unsigned long long* pool_ctl;  // [0] masks used, [1] overflow flag, [2] draws used
   TRY(P->alloc(&pool_ctl, 3, st));
   int64_t cap = 0, jcap = 0;
-  uint16_t* jpool = nullptr;
+  void* jpool = nullptr;
+  const int jbytes = prm->seq <= 256 ? 1 : 2;  // every draw j_i < nc <= seq - 3
   if (prm->masking && n_sent) {
     LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 24, st));
     hipLaunchKernelGGL(sum_tokens_kernel, dim3(1024), dim3(256), 0, st, d_sent_len, n_sent,
@@ -1685,7 +1709,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     LDDL_HIP(hipStreamSynchronize(st));
     cap = (int64_t)(2.0 * prm->masked_lm_ratio * prm->dup * (double)kept_tokens) +
           (int64_t)prm->dup * P->n_kept_sent / 2 + kPoolChunk * (n_part + 16);
-    jcap = (int64_t)(1.6 * prm->dup * (double)kept_tokens) + kPoolChunk * (n_part + 16);
+    jcap = (int64_t)(1.6 * prm->dup * (double)kept_tokens) + 8 * slots +
+           kPoolChunk * (n_part + 16);  // + the 16-entry alignment of every pair's draws
     if (const char* e = getenv("LDDL_AMD_MASK_POOL")) cap = atoll(e);  // tests: force a re-plan
   }
   for (int attempt = 0; n_part; ++attempt) {
@@ -1693,10 +1718,11 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     if (prm->masking) {
       LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 24, st));
       TRY(P->alloc(&mtok, cap + 4, st));
-      TRY(P->alloc(&jpool, jcap + 8, st));
+      TRY(P->alloc(reinterpret_cast<uint8_t**>(&jpool), jbytes * (jcap + 16), st));
     }
     A.mtok = mtok;
     A.jpool = jpool;
+    A.jbytes = jbytes;
     A.pool_cap = cap;
     A.jpool_cap = jcap;
     A.pool_used = pool_ctl;
@@ -1777,14 +1803,14 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     ResolveArgs RA{P->src, P->n_pairs, P->desc, P->nmask, ncand, P->moff, joff, jpool,
                    P->mpos, P->kscan, P->dense, cls, sep};
     const dim3 grid((unsigned)((P->n_pairs + 63) / 64));
-    if (prm->seq <= 131)  // nc <= 128: all draws in registers
-      hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, 16>), grid, dim3(64),
+    if (prm->seq <= 131)  // nc <= 128: all draws in registers (8 uint4 of 1-byte draws)
+      hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 8>), grid, dim3(64),
                          (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
-    else if (prm->seq <= 256)  // candidate indices and positions fit a byte
-      hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, 0>), grid, dim3(64),
+    else if (prm->seq <= 256)  // candidate indices, positions and draws fit a byte
+      hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 0>), grid, dim3(64),
                          (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
     else
-      hipLaunchKernelGGL((fy_resolve_kernel<uint16_t, 0>), grid, dim3(64),
+      hipLaunchKernelGGL((fy_resolve_kernel<uint16_t, uint16_t, 0>), grid, dim3(64),
                          (size_t)2 * 64 * (size_t)prm->seq, st, RA);
     LDDL_HIP(hipGetLastError());
   }

@@ -1,8 +1,12 @@
-"""Per-kernel HBM traffic per launch from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
-(bench.py --steps 1 --warmup 0) -> profiles/pmc_traffic.json, read by bench.py for
-`roofline.traffic` when the batch size matches.
+"""Per-kernel counters per launch from separate rocprofv3 --pmc passes over one bench step
+(tools/prof_counters.sh) -> profiles/pmc_<tag>.json, read by bench.py for `roofline.traffic`
+and the VALU-issue roofline when the batch size matches.
 
-    python tools/make_pmc_json.py gpurun_out/<dir> <batch_bytes> <label>
+    python tools/make_pmc_json.py gpurun_out/<dir> <batch_bytes> <label> > profiles/pmc.json
+
+HBM bytes: FETCH_SIZE and WRITE_SIZE (KB) in their own passes (MI355X_MICROARCH.md: FETCH_SIZE
+under-reports wide coalesced streaming reads by 2x on gfx950; these kernels' loads are byte- and
+gather-granular, not that shape, so no correction is applied - stated in the json).
 """
 import glob
 import json
@@ -19,21 +23,24 @@ def short(name):
 
 
 def main(src, batch_bytes, label):
-    f = glob.glob(os.path.join(src, 'pmc_fetch', '**', '*.db'), recursive=True)[0]
-    w = glob.glob(os.path.join(src, 'pmc_write', '**', '*.db'), recursive=True)[0]
-    fr, _ = summarise(f)
-    wr, _ = summarise(w)
-    out = {'batch_bytes': batch_bytes, 'source': (
-        'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes over bench.py --steps 1 '
-        '--warmup 0 ({}); mean per dispatch, KB -> bytes; no gfx950 x2 streaming-read correction '
-        '(these kernels do byte-granular and gather loads, not the 16 B/lane streaming shape the '
-        'correction is calibrated for)').format(label), 'kernels': {}}
-    for k in sorted(set(fr) | set(wr)):
-        fk = fr.get(k, {}).get('FETCH_SIZE', 0.0)
-        wk = wr.get(k, {}).get('WRITE_SIZE', 0.0)
-        out['kernels'][short(k)] = {'fetch_kb': fk, 'write_kb': wk,
-                                    'hbm_bytes_per_launch': (fk + wk) * 1024.0}
-    json.dump(out, sys.stdout, indent=1)
+    kernels = {}
+    for sub in sorted(os.listdir(src)):
+        dbs = glob.glob(os.path.join(src, sub, '**', '*.db'), recursive=True)
+        if not dbs:
+            continue
+        res, _ = summarise(dbs[0])
+        for k, cs in res.items():
+            kernels.setdefault(short(k), {}).update(cs)
+    for k, cs in kernels.items():
+        if 'FETCH_SIZE' in cs or 'WRITE_SIZE' in cs:
+            cs['hbm_bytes_per_launch'] = (cs.get('FETCH_SIZE', 0.0) + cs.get('WRITE_SIZE', 0.0)) * 1024.0
+    out = {'batch_bytes': batch_bytes,
+           'source': ('rocprofv3 --pmc passes (one counter group per run) over bench.py --steps 1 '
+                      '--warmup 0 ({}); mean per dispatch; FETCH_SIZE/WRITE_SIZE KB -> '
+                      'hbm_bytes_per_launch, no gfx950 x2 streaming-read correction (byte / '
+                      'gather-granular loads)').format(label),
+           'kernels': kernels}
+    json.dump(out, sys.stdout, indent=1, sort_keys=True)
     print()
 
 
