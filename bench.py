@@ -313,37 +313,39 @@ def run_c5(args):
             train(next(it))
         dt, real, slots, st, tw, tn = timed(args.steps, True)
         ldt, lreal, lslots, lst, _, _ = timed(args.steps, False)
-        kern_ms = [e[0].elapsed_time(e[1]) for e in st['events']]
+        kern_ms = [e[0].elapsed_time(e[1]) for e in lst['events']]
         # algorithmic bytes of the fused collate kernel per launch: the A/B strings read once +
         # input_ids, token_type_ids, attention_mask, labels written once (4 x 8 B per slot)
-        alg = [bb + 32 * n for bb, n in zip(st['blob_bytes'], st['slots'])]
+        alg = [bb + 32 * n for bb, n in zip(lst['blob_bytes'], lst['slots'])]
         k_ms = float(np.mean(kern_ms))
         ach = float(np.mean(alg)) / (k_ms * 1e-3) / 1e9
         return {
             'metric': 'WordPiece+MLM tokens/sec (1/2/4/8 MI355X) and % of HBM roofline',
-            'value': real / dt, 'unit': 'real token slots/s (attention_mask = 1) through loader '
-                                        '+ collate + dynamic masking + training step',
+            'value': lreal / ldt,
+            'unit': 'real token slots/s (attention_mask = 1) delivered by get_bert_pretrain_data_'
+                    'loader (parquet decode + shuffle buffer + collate + dynamic masking)',
             'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+            'ms_per_step': ldt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'int64', 'data': 'synthetic',
             'config': {'workload': 'C5: get_bert_pretrain_data_loader, batch 256 x seq 512 '
                                    '(sequence_length_alignment 8), dynamic masking 0.15, cased '
                                    '28,996 vocab, {} bins of {} tokens, {} workers per bin; input '
                                    '= preprocess_bert_pretrain --num-shards output of {} MiB of '
-                                   'synthetic documents; each batch feeds a bf16 TinyBert '
-                                   'training step (embeddings + MLP + MLM/NSP heads, SGD)'.format(
+                                   'synthetic documents'.format(
                                        512 // args.c5_bin_size, args.c5_bin_size,
                                        args.c5_workers, args.c5_corpus_bytes >> 20),
                        'global_batch': 256, 'seq_len': 512, 'parallelism': 'dp1 (replicas)'},
-            'padded_slots_per_s': slots / dt,
-            'loader_only': {'value': lreal / ldt, 'ms_per_batch': ldt / args.steps * 1e3,
-                            'padded_slots_per_s': lslots / ldt},
-            'train_step_host_ms': tw / args.steps * 1e3,
-            'loader_wait_ms_per_step': tn / args.steps * 1e3,
-            'note': 'value is bounded by the TinyBert step (GPU), not by the loader: the loader '
-                    'alone delivers loader_only.value; loader_wait_ms_per_step is the host time the '
-                    'training loop spends in next(loader) (collate on its own stream)',
-            'host_pack_ms_per_batch': float(np.mean(st['pack_s'])) * 1e3,
+            'padded_slots_per_s': lslots / ldt,
+            'with_training_step': {
+                'value': real / dt, 'ms_per_step': dt / args.steps * 1e3,
+                'padded_slots_per_s': slots / dt,
+                'loader_wait_ms_per_step': tn / args.steps * 1e3,
+                'train_step_host_ms': tw / args.steps * 1e3,
+                'note': 'each batch feeds a bf16 TinyBert training step (embeddings + LayerNorm + '
+                        'MLP + MLM/NSP heads, SGD): the pipeline runs at the step\'s pace; '
+                        'loader_wait_ms_per_step is the host time the training loop spends in '
+                        'next(loader) (the data stall)'},
+            'host_pack_ms_per_batch': float(np.mean(lst['pack_s'])) * 1e3,
             'collate_kernel_us': k_ms * 1e3,
             'roofline': {'kernel': 'encode_kernel (lddl_collate_encode_masked: collate + '
                                    'dynamic masking fused)', 'bound': 'hbm', 'achieved': ach,
@@ -594,37 +596,51 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
-    # Rooflines of the planner and the tokenizer; `roofline` is the dominant one
-    # (the replay planner at C2/C4, the tokenizer under the native RNG). Planner algorithmic
-    # bytes per launch: sentence lengths read per duplicate pass
-    # (4 B x dup x kept sentences) + document offsets (8 B x dup x kept documents) + per pair a
-    # 32-B descriptor, 4-B partition-shuffle draw, 4-B mask count, 4-B candidate count and two
-    # 8-B pool offsets (60 B) + the recorded cand_indexes shuffle draws (2 B per candidate, i.e.
-    # per A/B token) + 4 B per masked decision — all writes to HBM, the MT19937 state stays in LDS.
+    # Rooflines. Algorithmic bytes are SURVEY §8(d)'s compulsory bytes, never this
+    # design's scratch:
+    #  * tokenizer: text read (1 B/byte) + sentence offsets (8 B) + ids written (4 B/piece) +
+    #    sent_len (4 B/sentence)  (~10.5 B per wordpiece);
+    #  * pair stage: 9 B per output token (4 B id read + 4 B id write + positions/labels of the
+    #    15 % masked + per-pair metadata), over the whole stage's time;
+    #  * planner kernel alone: its compulsory inputs and outputs - sentence lengths (4 B) and
+    #    document offsets (8 B) per duplicate pass, a 16-B A/B window descriptor per pair and 6 B
+    #    (position + decision) per mask.
+    # `roofline` is the kernel with the longer launch; `issue_roofline` sets each kernel's VALU
+    # instruction count (committed PMC pass of the same batch size) against the chip's VALU issue
+    # rate, the bound these kernels actually sit on.
     n_bytes, n_sent = corp.text.size, corp.n_sent
-    pair_tokens = st['tokens'] - 3 * n_pairs  # sum of len(A) + len(B) of this rank's step
-    plan_bytes = (4 * 5 * st['kept_sent'] + 8 * 5 * st['kept_doc'] + 60 * n_pairs +
-                  2 * pair_tokens + 4 * st['masked'])
+    plan_bytes = (4 * 5 * st['kept_sent'] + 8 * 5 * st['kept_doc'] + 16 * n_pairs +
+                  6 * st['masked'])
     plan_gbs = plan_bytes / (plan_ms * 1e-3) / 1e9 if plan_ms > 0 else 0.0
-    # tokenizer: text bytes read + sentence offsets read (8 B each) + ids written (4 B / piece)
-    # + sent_len (4 B / sentence)
     tok_bytes = n_bytes + 8 * (n_sent + 1) + 4 * pieces + 4 * n_sent
     achieved = tok_bytes / (tok_ms * 1e-3) / 1e9
-    # HBM bytes per launch from the committed PMC passes (profiles/pmc_traffic.json, made by
-    # tools/make_pmc_json.py) when they were taken on the same batch size
-    pmc_kernels = {}
-    pmc = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
-    if os.path.exists(pmc):
+    stage_bytes = 9 * st['tokens']
+    stage_gbs = stage_bytes / (pair_ms * 1e-3) / 1e9
+    # per-kernel counters per launch from the committed PMC passes (profiles/pmc_*.json, made by
+    # tools/prof_counters.sh + tools/make_pmc_json.py) when taken on the same batch size
+    pmc_kernels, pmc_src = {}, None
+    import glob
+    for pmc in sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_*.json'))):
         try:
             with open(pmc) as f:
                 rec = json.load(f)
-            if rec.get('batch_bytes') == args.batch_bytes:
-                pmc_kernels = rec.get('kernels', {})
         except (OSError, ValueError):
-            pmc_kernels = {}
+            continue
+        if rec.get('batch_bytes') == args.batch_bytes:
+            pmc_kernels, pmc_src = rec.get('kernels', {}), os.path.basename(pmc)
 
     def traffic(kernel):
         return pmc_kernels.get(kernel, {}).get('hbm_bytes_per_launch')
+    valu_peak = 256 * 4 * 2.4e9 / 4  # wave64 VALU instructions / s: 256 CUs x 4 SIMDs x 2.4 GHz / 4
+
+    def issue(kernel, ms):
+        v = pmc_kernels.get(kernel, {}).get('SQ_INSTS_VALU')
+        if not v or not ms:
+            return None
+        a = v / (ms * 1e-3)
+        return {'kernel': kernel, 'bound': 'valu_issue', 'valu_instructions_per_launch': v,
+                'achieved': a, 'peak': valu_peak, 'unit': 'wave64 VALU instr/s',
+                'frac': a / valu_peak, 'source': pmc_src}
 
     plan_roof = {'kernel': 'plan_replay_kernel' if args.rng == 'replay' else
                  'plan_native_kernel x2 + mask_native_kernel + order_native_kernel (HIP events '
@@ -633,12 +649,17 @@ def main():
                  'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': plan_gbs / HBM_PEAK_GBS,
                  'traffic': traffic('plan_replay_kernel') if args.rng == 'replay' else None,
                  'algorithmic_bytes_per_launch': plan_bytes, 'launch_ms': plan_ms,
-                 'note': ('issue-bound on the CU scalar unit, not HBM (DESIGN.md 4)'
-                          if args.rng == 'replay' else 'DESIGN.md 4')}
+                 'note': 'VALU-issue-bound (issue_roofline), not HBM-bound (DESIGN.md 4)'}
     tok_roof = {'kernel': 'tokenize_batch_kernel', 'bound': 'hbm', 'achieved': achieved,
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                 'traffic': traffic('tokenize_batch_kernel'), 'algorithmic_bytes_per_launch': tok_bytes,
-                'launch_ms': tok_ms}
+                'launch_ms': tok_ms,
+                'note': 'VALU-issue-bound (issue_roofline), not HBM-bound (DESIGN.md 4)'}
+    stage_roof = {'kernel': 'pair stage (compaction, densify, plan, shuffle, resolve, layout, '
+                            'gather)', 'bound': 'hbm', 'achieved': stage_gbs,
+                  'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': stage_gbs / HBM_PEAK_GBS,
+                  'algorithmic_bytes_per_step': stage_bytes, 'stage_ms': pair_ms,
+                  'note': 'SURVEY 8d: 9 B per output token'}
     res = {
         'metric': 'WordPiece+MLM tokens/sec (1/2/4/8 MI355X) and % of HBM roofline',
         'value': out_tokens / dt,
@@ -676,6 +697,9 @@ def main():
         'roofline': None,  # the dominant kernel's, filled below
         'roofline_planner': plan_roof,
         'roofline_tokenizer': tok_roof,
+        'roofline_pairs_stage': stage_roof,
+        'issue_roofline': [x for x in (issue('tokenize_batch_kernel', tok_ms),
+                                       issue('plan_replay_kernel', plan_ms)) if x],
     }
     res['roofline'] = plan_roof if plan_ms >= tok_ms else tok_roof
     if bal_ms is not None:

@@ -229,13 +229,6 @@ int lddl_collate_encode(lddl_ctx* ctx, void* stream, const uint8_t* d_bytes, con
                         const int64_t* d_lab_off, const uint16_t* d_pos, const int64_t* d_pos_off,
                         int64_t* d_labels, int64_t ignore_index);
 
-/* Token counts of a batch (the `len(a.split())`, `len(b.split())` of bert.py:80-96, ASCII
- * whitespace; the host passes strings whose separators are ASCII): d_na[b], d_nb[b] and
- * *d_max_len = max(na + nb + 3) (int32, device). The caller reads d_max_len to size the batch. */
-int lddl_collate_count(void* stream, const uint8_t* d_bytes, const int64_t* d_a_off,
-                       const int64_t* d_b_off, int32_t batch, int32_t* d_na, int32_t* d_nb,
-                       int32_t* d_max_len);
-
 /* The loader's dynamic-masking collate in one pass (lddl/torch/bert.py:348-365 =
  * _to_encoded_inputs + _mask_tokens): as lddl_collate_encode (dynamic), then the native-RNG
  * masking of lddl_mask_dynamic applied to each slot as it is written; outputs input_ids (masked),

@@ -56,7 +56,6 @@ SIGNATURES = {
                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_i64]),
     'lddl_utf8_check': (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),
-    'lddl_collate_count': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
     'lddl_collate_encode_masked': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32,
                                                   c_i32, c_vp, c_vp, c_vp, c_vp, ctypes.c_float,
                                                   c_i64, c_i64, c_u64, c_u64]),

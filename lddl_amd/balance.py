@@ -306,6 +306,10 @@ class RankBalance:
     # regroup -------------------------------------------------------------------------------
     def finish(self, recvs):
         n_local = self.pb.n_pairs
+        if self.n_recv == 0 and sum(self.send_rows_per_dst) == 0:
+            # every row stays (always at world size 1): the output is the local bin order itself
+            return BalancedBins(self.pb, self.perm, self.bin_off, self.shards, self.shard_counts,
+                                int(self.pb.tokens.numel()), 0, self.all_shard_counts)
         src = torch.cat([self.perm, torch.arange(n_local, n_local + self.n_recv, dtype=torch.int64,
                                                   device=self.dev)])
         order = _expand(src, *self._order_src, self.dev)

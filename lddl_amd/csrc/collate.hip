@@ -11,8 +11,6 @@
 //                         masked, ignore_index elsewhere. Native mode draws from a counter-based
 //                         Philox4x32-10 keyed by (seed, counter, slot); replay mode applies
 //                         captured torch masks bit for bit.
-//   lddl_collate_count    the whitespace token counts len(A.split()), len(B.split()) of every
-//                         sample and max(na + nb + 3), which sizes the batch (bert.py:80-96).
 //   lddl_collate_encode_masked   _to_encoded_inputs + _mask_tokens in ONE pass (the loader's
 //                         dynamic-masking collate, bert.py:348-365): the row is built in LDS and
 //                         masked on its way out, so input_ids / token_type_ids / attention_mask /
@@ -183,39 +181,6 @@ __global__ void __launch_bounds__(64 * kEncWaves) encode_kernel(EncodeArgs E) {
   }
 }
 
-// Whitespace token counts of A and B per sample (one wave per sample, ballots over 64-byte
-// windows) and the batch's max(na + nb + 3) (atomicMax on an int32).
-__device__ int32_t count_words(const uint8_t* bytes, int64_t b0, int64_t b1) {
-  const int lane = lane_id();
-  int32_t n = 0;
-  uint8_t prev = ' ';
-  for (int64_t base = b0; base < b1; base += 64) {
-    const int64_t i = base + lane;
-    const uint8_t c = i < b1 ? bytes[i] : ' ';
-    const int up = __shfl_up((int)c, 1, 64);
-    const uint8_t pc = lane == 0 ? prev : (uint8_t)up;
-    n += __popcll(__ballot(!is_ws(c) && is_ws(pc)));
-    prev = (uint8_t)__shfl((int)c, 63, 64);
-  }
-  return n;
-}
-
-__global__ void __launch_bounds__(256) count_kernel(const uint8_t* __restrict__ bytes,
-                                                    const int64_t* __restrict__ a_off,
-                                                    const int64_t* __restrict__ b_off, int32_t B,
-                                                    int32_t* __restrict__ na, int32_t* __restrict__ nb,
-                                                    int32_t* __restrict__ max_len) {
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
-  const int32_t x = count_words(bytes, a_off[b], a_off[b + 1]);
-  const int32_t y = count_words(bytes, b_off[b], b_off[b + 1]);
-  if (lane_id() == 0) {
-    na[b] = x;
-    nb[b] = y;
-    atomicMax(max_len, x + y + 3);
-  }
-}
-
 struct MaskArgs {
   int64_t* ids;        // [B, L] in/out
   int64_t* labels;     // [B, L] out
@@ -315,19 +280,6 @@ extern "C" int lddl_mask_dynamic(lddl_ctx* c, void* stream, int64_t* d_input_ids
   for (int k = 0; k < kNumSpecial; ++k) M.special_ids[k] = c->tab.special_id[k];
   hipLaunchKernelGGL(mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      as_stream(stream), M);
-  LDDL_HIP(hipGetLastError());
-  return 0;
-}
-
-extern "C" int lddl_collate_count(void* stream, const uint8_t* d_bytes, const int64_t* d_a_off,
-                                  const int64_t* d_b_off, int32_t batch, int32_t* d_na,
-                                  int32_t* d_nb, int32_t* d_max_len) {
-  if (batch < 0 || !d_max_len) LDDL_FAIL(-1, "bad arguments");
-  hipStream_t st = as_stream(stream);
-  LDDL_HIP(hipMemsetAsync(d_max_len, 0, sizeof(int32_t), st));
-  if (batch == 0) return 0;
-  hipLaunchKernelGGL(count_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, d_bytes,
-                     d_a_off, d_b_off, batch, d_na, d_nb, d_max_len);
   LDDL_HIP(hipGetLastError());
   return 0;
 }

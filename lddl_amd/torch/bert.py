@@ -71,10 +71,14 @@ def _canon(s):
 
 def _pack(batch, static):
     """Flat host buffers of a batch: A and B strings back to back (separators canonicalised to
-    ASCII), their offsets and, with static masking, the labels strings and decoded positions.
-    Token counts are taken on the GPU (lddl_collate_count), not with str.split() here."""
+    ASCII), their token counts (bytes.split() of the canonical strings = the reference's
+    str.split(), bert.py:80-81) and offsets and, with static masking, the labels strings and
+    decoded positions. Runs in the DataLoader workers, so the main process never has to wait for
+    the batch's shape."""
     As = [_canon(s[0]).encode('utf-8') for s in batch]
     Bs = [_canon(s[1]).encode('utf-8') for s in batch]
+    na = np.fromiter(map(len, map(bytes.split, As)), np.int32, len(batch))
+    nb = np.fromiter(map(len, map(bytes.split, Bs)), np.int32, len(batch))
     la = np.fromiter(map(len, As), np.int64, len(batch))
     lb = np.fromiter(map(len, Bs), np.int64, len(batch))
     a_off = np.zeros(len(batch) + 1, np.int64)
@@ -93,7 +97,7 @@ def _pack(batch, static):
         parts += labs
         extra = (lab_off, np.concatenate(pos) if pos else np.zeros(0, np.uint16), pos_off)
     blob = np.frombuffer(bytearray(b''.join(parts)), np.uint8)
-    return blob, a_off, b_off, extra
+    return blob, a_off, b_off, na, nb, extra
 
 
 def _dev(a, device):
@@ -142,7 +146,7 @@ class PackedBatch:
     def __init__(self, batch):
         t0 = time.perf_counter()
         self.static = len(batch[0]) > 3
-        self.blob, self.a_off, self.b_off, self.extra = _pack(batch, self.static)
+        self.blob, self.a_off, self.b_off, self.na, self.nb, self.extra = _pack(batch, self.static)
         self.nsl = np.asarray([s[2] for s in batch], np.int64)
         self.pack_s = time.perf_counter() - t0  # host time of the pack (in the worker)
 
@@ -163,15 +167,13 @@ def encode_packed(pk, ctx, sequence_length_alignment=8, ignore_index=-1, mask=No
     encode kernel (timing)."""
     dev = ctx.device
     B = len(pk)
+    seq = int((pk.na + pk.nb).max()) + 3  # the batch's shape (bert.py:91-96), known on the host
+    L = ((seq - 1) // sequence_length_alignment + 1) * sequence_length_alignment
     d_blob = _dev(pk.blob, dev) if len(pk.blob) else torch.zeros(1, dtype=torch.uint8, device=dev)
     d_off = _dev(np.concatenate([pk.a_off, pk.b_off]), dev)
     d_a, d_b = d_off[:B + 1], d_off[B + 1:]
-    cnt = torch.empty(2 * B + 1, dtype=torch.int32, device=dev)
-    d_na, d_nb, d_mx = cnt[:B], cnt[B:2 * B], cnt[2 * B:]
-    check(lib.lddl_collate_count(_stream(), _ptr(d_blob), _ptr(d_a), _ptr(d_b), B, _ptr(d_na),
-                                 _ptr(d_nb), _ptr(d_mx)))
-    seq = int(d_mx.item())  # the batch's shape: max(len(A) + len(B) + 3) (bert.py:91-96)
-    L = ((seq - 1) // sequence_length_alignment + 1) * sequence_length_alignment
+    d_cnt = _dev(np.concatenate([pk.na, pk.nb]), dev)
+    d_na, d_nb = d_cnt[:B], d_cnt[B:]
     out = {k: torch.empty(B, L, dtype=torch.long, device=dev)
            for k in ('input_ids', 'token_type_ids', 'attention_mask')}
     if mask is not None and not pk.static:
@@ -232,7 +234,6 @@ class GPUCollateLoader:
         self._epoch = start_epoch    # counter = epoch << 32 | batch: no stream repeats across
         self._counter = start_epoch << 32  # epochs, and a resumed run continues, not replays
         self.stats = None  # dict(pack_s=[], blob_bytes=[], events=[], slots=[]): record timings
-        self._stream = torch.cuda.Stream(device=ctx.device)
 
     @property
     def dataset(self):
@@ -253,16 +254,11 @@ class GPUCollateLoader:
                 self.stats['pack_s'].append(pk.pack_s)
                 self.stats['blob_bytes'].append(len(pk.blob))
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            consumer = torch.cuda.current_stream()
-            # the collate runs on its own stream: its one host sync (the batch shape) waits for
-            # the count kernel only, not for the training step queued on the consumer's stream
-            with torch.cuda.stream(self._stream), torch.no_grad():
-                # dynamic masking: collate + _mask_tokens in one kernel
+            # the batch shape is known on the host (counted in the worker): nothing here waits
+            # for the GPU, the collate kernel is queued behind the consumer's training step
+            with torch.no_grad():  # dynamic masking: collate + _mask_tokens in one kernel
                 enc = encode_packed(pk, self._ctx, self._align, self._ignore,
                                     mask=(self._mlm, self._seed, self._counter), events=ev)
-            consumer.wait_stream(self._stream)
-            for t in enc.values():
-                t.record_stream(consumer)
             if not pk.static:
                 self._counter += 1
             if self.stats is not None:
