@@ -950,8 +950,8 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
       flush();
       // the open sentence already has max_pieces pieces: the rest of it cannot be kept
       if (cur && W.r_count[cur_slot] >= max_pieces) pos = b1;
+      retire();  // sentences complete only when their units are placed, i.e. in a flush
     }
-    retire();
   }
   while (qn > 0) {
     flush();
