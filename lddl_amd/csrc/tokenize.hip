@@ -347,22 +347,25 @@ __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v,
 }
 
 // Classification of one 64-byte window [pos, pos+64) of a sentence ending at b1 (one byte per
-// lane). Fills W.us / W.ue / W.uk with the window's complete units (first byte, last byte, kind:
-// 0 word run, 1 isolated char, 2 + k literal special token k) and returns their count, the start
-// of the next window and the mask of lanes holding a byte the register fast path cannot take.
+// lane). Returns, in registers, the window's complete units as masks (US: first bytes, UE: last
+// bytes; unit k = the k-th bit of each), each start lane's unit kind (0 word run, 1 isolated
+// char, 2 + k literal special token k), the start of the next window and the mask of lanes
+// holding a byte the register fast path cannot take. The caller stores what it needs.
 struct WinResult {
   int n_units;
   int64_t next;
   uint64_t slow;
-  bool fallback;  // a unit of >= 64 bytes: the sentence goes to the lane kernel
+  uint64_t US, UE;  // unit starts (a trailing incomplete unit included) / complete unit ends
+  int ukind;        // this lane's unit kind when its US bit is set
+  bool unit_byte;   // this lane's byte belongs to a unit (not a separator)
+  bool fallback;    // a unit of >= 64 bytes: the sentence goes to the lane kernel
 };
 
 // byte = text[pos + lane] (already loaded by the caller, which may prefetch it), any value when
 // pos + lane >= b1.
-template <typename WL>
 __device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
                                      const uint8_t* __restrict__ text, int64_t pos, int64_t b1,
-                                     uint32_t byte, WL& W) {
+                                     uint32_t byte) {
   const int lane = lane_id();
   const int64_t i = pos + lane;
   const bool in = i < b1;
@@ -410,11 +413,15 @@ __device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
   WinResult R;
   R.slow = ballot(slow);
   R.fallback = false;
+  R.ukind = spk >= 0 ? 2 + spk : cat == kCatIso ? 1 : 0;
+  R.unit_byte = cat != kCatSep;
   const bool tail_known = pos + 64 >= b1;  // position 64 is past the sentence end
   const uint64_t US = S | (ISO & LEAD) | (RUN & ~(RUN << 1));
   uint64_t RE = RUN & ~(RUN >> 1);
   if (!tail_known) RE &= ~(1ull << 63);
   const uint64_t UE = ((S & ~S6) << 4) | (S6 << 5) | (ISO & CPL & ~inside) | RE;
+  R.US = US;
+  R.UE = UE;
   R.n_units = __popcll(UE);
   const int n_starts = __popcll(US);
   if (n_starts > R.n_units) {
@@ -433,14 +440,21 @@ __device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
     const int hc = 63 - __clzll(CPL);
     R.next = pos + (hl > hc ? hl : 64);
   }
-  if ((US >> lane) & 1ull) {
-    const int k = (int)popc_below(US);
-    W.us[k] = (uint8_t)lane;
-    W.uk[k] = (uint8_t)(spk >= 0 ? 2 + spk : cat == kCatIso ? 1 : 0);
-  }
-  if ((UE >> lane) & 1ull) W.ue[popc_below(UE)] = (uint8_t)lane;
-  wave_sync();
   return R;
+}
+
+// The window's units as arrays (W.us / W.ue / W.uk, unit k at index k) for the per-sentence
+// kernel, which gives one unit to each lane.
+template <typename WL>
+__device__ inline void store_units(const WinResult& R, WL& W) {
+  const int lane = lane_id();
+  if ((R.US >> lane) & 1ull) {
+    const int k = (int)popc_below(R.US);
+    W.us[k] = (uint8_t)lane;
+    W.uk[k] = (uint8_t)R.ukind;
+  }
+  if ((R.UE >> lane) & 1ull) W.ue[popc_below(R.UE)] = (uint8_t)lane;
+  wave_sync();
 }
 
 // 32 bytes of text from byte `start` (unaligned); bytes at or past `n_bytes` read as 0 and are
@@ -623,8 +637,9 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
     bool fallback = false;
     while (pos < b1 && emitted < max_pieces) {
       const uint32_t byte = pos + lane < b1 ? text[pos + lane] : 0x20u;
-      const WinResult R = classify_window(T, s_ascii, text, pos, b1, byte, W);
+      const WinResult R = classify_window(T, s_ascii, text, pos, b1, byte);
       if (R.fallback) { fallback = true; break; }
+      store_units(R, W);
       int npc = 0;
       bool cs_flag = false;
       Pcs pc{W.pcs + lane};
@@ -681,7 +696,6 @@ using HIdx = std::conditional_t<(kSF > 256), uint16_t, uint8_t>;
 constexpr int32_t kHardBit = INT32_MIN;  // q_res: pieces are in column (res & 63) of pcs
 
 struct alignas(16) BatchLds {
-  uint8_t us[64], ue[64], uk[64];
   int32_t q_rel[kQ];        // unit start relative to its sentence's first byte
   uint8_t q_len[kQ], q_kind[kQ], q_slot[kQ], q_slow[kQ];
   int32_t q_res[kSF];       // phase A/B result: the single piece id, or kHardBit | column
@@ -910,7 +924,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
     }
     if (pos < b1) {
       const uint32_t byte = ppos == pos ? pbyte : (pos + lane < b1 ? text[pos + lane] : 0x20u);
-      const WinResult R = classify_window(T, s_ascii, text, pos, b1, byte, W);
+      const WinResult R = classify_window(T, s_ascii, text, pos, b1, byte);
 #ifndef LDDL_TOK_NO_PREFETCH
       if (R.next < b1) {
         ppos = R.next;
@@ -924,17 +938,22 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
         if (lane == 0) W.r_flags[cur_slot] |= kFallback;
         pos = b1;
       } else {
+        // enqueue straight from the masks: unit k's start lane writes its start, kind and slot,
+        // its end lane the length (the unit's start is the last start at or below it), and its
+        // slow bytes (all inside units) set its slow flag after the start lane cleared it. A
+        // trailing incomplete unit writes queue entry qn + n, which stays outside the queue.
         const int n = R.n_units;
-        if (lane < n) {
-          const int us = W.us[lane], ue = W.ue[lane];
-          const int ulen = ue - us + 1;
-          W.q_rel[qn + lane] = (int32_t)(pos - b0 + us);
-          W.q_len[qn + lane] = (uint8_t)ulen;
-          W.q_kind[qn + lane] = W.uk[lane];
-          W.q_slot[qn + lane] = (uint8_t)cur_slot;
-          W.q_slow[qn + lane] =
-              ((R.slow >> us) & (ulen >= 64 ? ~0ull : ((1ull << ulen) - 1))) != 0;
+        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+        if ((R.US >> lane) & 1ull) {
+          const int k = qn + (int)popc_below(R.US);
+          W.q_rel[k] = (int32_t)(pos - b0 + lane);
+          W.q_kind[k] = (uint8_t)R.ukind;
+          W.q_slot[k] = (uint8_t)cur_slot;
+          W.q_slow[k] = 0;
         }
+        if ((R.UE >> lane) & 1ull)
+          W.q_len[qn + (int)popc_below(R.UE)] = (uint8_t)(lane - (63 - __clzll(R.US & upto)) + 1);
+        if (((R.slow >> lane) & 1ull) && R.unit_byte) W.q_slow[qn + __popcll(R.US & upto) - 1] = 1;
         if (lane == 0) W.r_pending[cur_slot] += n;
         wave_sync();
         qn += n;
