@@ -1047,12 +1047,19 @@ __global__ void __launch_bounds__(64) apply_shuffle_kernel(const int64_t* kd_off
 // ---------------------------------------------------------------------------------------------
 // layout + gather
 // ---------------------------------------------------------------------------------------------
+// src[q]: the planner slot of output pair q (partition shuffle applied); slots[q]: the q-th
+// slot in planner order (every partition's slots base .. base + np - 1), so the per-slot passes
+// read the slot-indexed arrays front to back instead of in shuffled order.
 __global__ void map_pairs_kernel(const int64_t* kd_off, const int64_t* kp_off, int32_t dup,
-                                 const int64_t* part_pair_base, const int32_t* order, int64_t* src) {
+                                 const int64_t* part_pair_base, const int32_t* order, int64_t* src,
+                                 int64_t* slots) {
   const int p = blockIdx.x;
   const int64_t base = (int64_t)dup * kd_off[kp_off[p]];
   const int64_t q0 = part_pair_base[p], n = part_pair_base[p + 1] - q0;
-  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) src[q0 + k] = base + order[base + k];
+  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
+    src[q0 + k] = base + order[base + k];
+    if (slots) slots[q0 + k] = base + k;
+  }
 }
 
 struct Identity {
@@ -1179,7 +1186,7 @@ struct GatherLds {
 // move x[i] to x[j_i] (slot i is never read again); steps i < num finalise slot i = x[j_i].
 // Column layout x[k * 64 + lane] keeps the 64 lanes' accesses in distinct banks.
 struct ResolveArgs {
-  const int64_t* src;
+  const int64_t* src;  // slots in planner order (each pair once; mpos is addressed by moff)
   int64_t n_pairs;
   const PairDesc* desc;
   const int32_t* nmask;
@@ -1796,11 +1803,13 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   LDDL_HIP(hipMemcpyAsync(&P->n_pairs, part_base + n_part, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
   TRY(P->alloc(&P->src, P->n_pairs, st));
+  int64_t* slots = nullptr;  // planner-order slots for the mask replay
+  if (prm->masking) TRY(P->alloc(&slots, P->n_pairs, st));
   if (n_part)
     hipLaunchKernelGGL(map_pairs_kernel, dim3((unsigned)n_part), dim3(256), 0, st, P->kd_off,
-                       P->kp_off, prm->dup, part_base, P->order, P->src);
+                       P->kp_off, prm->dup, part_base, P->order, P->src, slots);
   if (prm->masking && P->n_pairs) {
-    ResolveArgs RA{P->src, P->n_pairs, P->desc, P->nmask, ncand, P->moff, joff, jpool,
+    ResolveArgs RA{slots, P->n_pairs, P->desc, P->nmask, ncand, P->moff, joff, jpool,
                    P->mpos, P->kscan, P->dense, cls, sep};
     const dim3 grid((unsigned)((P->n_pairs + 63) / 64));
     if (prm->seq <= 131)  // nc <= 128: all draws in registers (8 uint4 of 1-byte draws)
