@@ -1152,10 +1152,10 @@ struct KeptLen {
 struct GatherArgs {
   const int32_t* dense;  // kept tokens, packed
   const GatherRec* rec;  // per output pair (pair_prep_kernel)
-  // masks: positions + replacements at rec.moff (any order; ranks are taken from the map)
+  // masks: positions + replacements at rec.moff (any order; ranks are taken from the bitmap)
   const uint16_t* mpos;
   const int32_t* mtok;
-  int32_t max_pred, masking, seq;
+  int32_t masking;
   int64_t n_pairs;
   const int64_t* tok_off;
   const int64_t* pos_off;
@@ -1166,17 +1166,14 @@ struct GatherArgs {
   int32_t* out_lab;
 };
 
-constexpr int kMaxPredLds = 1024;
-constexpr int kMaxSeqGather = 4096;  // LDS position -> mask map per pair
+constexpr int kMaxSeqGather = 4096;
 constexpr int kGWaves = 4;
 
-// Per-wave LDS of the gather: K maps (position -> 1 + mask index) and K decision tables.
+// LDS of the gather per pair in flight: the masked-position bitmap (W words, bit = position - 1)
+// and the decisions indexed by position.
 struct GatherLds {
-  int32_t map_len, max_pred;
-  __host__ __device__ static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
-  __host__ __device__ size_t maps_bytes(int K) const { return align16((size_t)K * map_len * 2); }
-  __host__ __device__ size_t toks_bytes(int K) const { return align16((size_t)K * max_pred * 4); }
-  __host__ __device__ size_t per_wave(int K) const { return maps_bytes(K) + toks_bytes(K); }
+  int32_t W, seq;
+  __host__ __device__ size_t per_pair() const { return ((size_t)4 * W + (size_t)4 * seq + 15) & ~(size_t)15; }
 };
 
 // Replay masks, off the planner's sequential chain: one LANE per pair replays the recorded swaps
@@ -1314,105 +1311,132 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   }
 }
 
-// Gather: each wave emits K consecutive output pairs (their tokens are contiguous in the output).
-// Per pair: A = dense[kscan[a_ks] + a_front ..+ na), B likewise; output token x < na + nb comes from
-// A (x < na) or B. The masks of each pair go to an LDS map (position -> 1 + mask index); each
-// output lane finds its own decision, and a ballot prefix over the map gives each masked token
-// its rank, i.e. its place in the position-sorted masked_lm_positions / labels (labels take the
-// original token). All K*C token loads of the wave are issued before any is consumed (the
-// kernel is bound by load latency and cache lines).
-template <int K, int C>
-__global__ void __launch_bounds__(64 * kGWaves) gather_kernel(GatherArgs G, GatherLds Lg) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  uint8_t* wbase = g_smem + (size_t)w * Lg.per_wave(K);
-  uint16_t* maps = reinterpret_cast<uint16_t*>(wbase);
-  int32_t* toks = reinterpret_cast<int32_t*>(wbase + Lg.maps_bytes(K));
-  const int map_len = Lg.map_len;
-  const int64_t qb = ((int64_t)blockIdx.x * kGWaves + w) * K;
+// Gather: each half-wave emits K output pairs, 4 consecutive tokens per lane (128 per pass), so
+// a wave has 2K pairs in flight with all their parameters in vector registers. Per pair:
+// A = dense[kscan[a_ks] + a_front ..+ na), B likewise; output token x < na + nb comes from A
+// (x < na, position x + 1) or B (position x + 2); a lane's 4 tokens are one 16-byte load and one
+// 16-byte non-temporal store except where they straddle A/B or the end. The pair's masks (any
+// order in the pool) go to a per-pair LDS bitmap + position-indexed decision table; a masked
+// token's rank (its place in the position-sorted masked_lm_positions / labels) is the count of
+// masked tokens before it in the half-wave, from four ballots.
+typedef int32_t tok4_t __attribute__((ext_vector_type(4), aligned(4)));
 
-  int64_t mbase[K], tof[K], aoff[K], boff[K], po[K];
-  int32_t na[K], nb[K], rn[K], nm[K], rk[K];
-  bool act[K];
+#ifndef LDDL_GMINW
+#define LDDL_GMINW 1
+#endif
+template <int K>
+__global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(GatherArgs G, GatherLds Lg) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, sl = lane & 31;
+  const int64_t wg = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t q0 = (wg * kGWaves + w) * 2 * K;  // pairs q0 + 2k + h
+  const uint64_t hm = h ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
+  const uint64_t before = ((1ull << lane) - 1ull) & hm;  // lanes before this one in its half
+  const int W = Lg.W;
+
+  int64_t tof[K], aoff[K], boff[K], po[K], mb[K];
+  int32_t na[K], nb[K], rk[K], nm[K];
+  uint32_t* bm[K];
+  int32_t* dec[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    act[k] = qb + k < G.n_pairs;
+    const int64_t q = q0 + 2 * k + h;
+    const bool act = q < G.n_pairs;
     GatherRec r{0, 0, 0, 0, 0, 0, 0};
-    if (act[k]) r = G.rec[qb + k];
+    if (act) r = G.rec[q];
     na[k] = r.na;
     nb[k] = r.nb_rn & 0x7FFFFFFF;
-    rn[k] = (int32_t)((uint32_t)r.nb_rn >> 31);
     aoff[k] = r.aoff;
     boff[k] = r.boff;
-    mbase[k] = r.moff;
-    tof[k] = act[k] ? G.tok_off[qb + k] : 0;
+    mb[k] = r.moff;
     nm[k] = G.masking ? r.nm : 0;
-    po[k] = (G.masking && act[k]) ? G.pos_off[qb + k] : 0;
+    tof[k] = act ? G.tok_off[q] : 0;
+    po[k] = (G.masking && act) ? G.pos_off[q] : 0;
     rk[k] = 0;
+    uint8_t* pb = g_smem + (((size_t)w * K + k) * 2 + h) * Lg.per_pair();
+    bm[k] = reinterpret_cast<uint32_t*>(pb);
+    dec[k] = reinterpret_cast<int32_t*>(pb + 4 * (size_t)W);
+    if (sl == 0 && act) {
+      G.len_a[q] = na[k];
+      G.is_rn[q] = (uint8_t)((uint32_t)r.nb_rn >> 31);
+    }
   }
-  for (int32_t cb = 0;; cb += 64 * C) {  // one pass for seq <= 64 * C + 3
-    int32_t tok[K][C];
+  auto load_tokens = [&](int32_t x, tok4_t* v) {
 #pragma unroll
-    for (int k = 0; k < K; ++k)
+    for (int k = 0; k < K; ++k) {
+      const int32_t n = na[k] + nb[k];
+      if (x + 3 < na[k]) {
+        v[k] = *reinterpret_cast<const tok4_t*>(G.dense + aoff[k] + x);
+      } else if (x >= na[k] && x + 3 < n) {
+        v[k] = *reinterpret_cast<const tok4_t*>(G.dense + boff[k] + (x - na[k]));
+      } else {
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const int32_t x = cb + c * 64 + lane;
-        tok[k][c] = x < na[k] ? G.dense[aoff[k] + x]
-                              : (x < na[k] + nb[k] ? G.dense[boff[k] + (x - na[k])] : 0);
-      }
-    if (G.masking && cb == 0) {  // token loads are in flight while the mask maps are built
-      uint32_t* m32 = reinterpret_cast<uint32_t*>(maps);
-      for (int i = lane; i < K * map_len / 2; i += 64) m32[i] = 0u;
-      wave_sync();
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        if (!nm[k]) continue;
-        uint16_t* map = maps + k * map_len;
-        int32_t* tk = toks + k * G.max_pred;
-        const int64_t mb = mbase[k];
-        for (int j = lane; j < nm[k]; j += 64) {
-          map[G.mpos[mb + j]] = (uint16_t)(j + 1);
-          tk[j] = G.mtok[mb + j];
+        for (int e = 0; e < 4; ++e) {
+          const int32_t xe = x + e;
+          v[k][e] = xe < na[k] ? G.dense[aoff[k] + xe] : xe < n ? G.dense[boff[k] + (xe - na[k])] : 0;
         }
       }
-      wave_sync();
     }
+  };
+  tok4_t v[K];
+  load_tokens(4 * sl, v);  // the first pass's tokens are in flight while the mask tables fill
+  if (G.masking) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      for (int i = sl; i < W; i += 32) bm[k][i] = 0u;
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      for (int j = sl; j < nm[k]; j += 32) {
+        const int p = G.mpos[mb[k] + j];
+        atomicOr(&bm[k][(p - 1) >> 5], 1u << ((p - 1) & 31));
+        dec[k][p] = G.mtok[mb[k] + j];
+      }
+    wave_sync();
+  }
+  for (int32_t cb = 0;; cb += 128) {
+    const int32_t x = cb + 4 * sl;
+    if (cb > 0) load_tokens(x, v);
     bool more = false;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      if (!act[k]) continue;
       const int32_t n = na[k] + nb[k];
-      const uint16_t* map = maps + k * map_len;
-      const int32_t* mt = toks + k * G.max_pred;
-      int32_t* out = G.out_tok + tof[k];
+      if (G.masking) {
+        bool mk[4];
+        int rank = rk[k], tot = 0;
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const int32_t x = cb + c * 64 + lane;
-        const bool in = x < n;
-        const int32_t pos = x < na[k] ? x + 1 : x + 2;
-        int32_t v = tok[k][c];
-        if (G.masking) {
-          const int m = in ? (int)map[pos] : 0;
-          const uint64_t bits = ballot(m != 0);
-          if (m) {
-            const int64_t o = po[k] + rk[k] + (int)popc_below(bits);
-            G.out_pos[o] = (uint16_t)pos;
-            G.out_lab[o] = v;
-            if (mt[m - 1] != kKeep) v = mt[m - 1];
-          }
-          rk[k] += __popcll(bits);
+        for (int e = 0; e < 4; ++e) {
+          const int32_t xe = x + e, b = xe < na[k] ? xe : xe + 1;
+          mk[e] = xe < n && ((bm[k][b >> 5] >> (b & 31)) & 1u);
+          const uint64_t M = ballot(mk[e]);
+          rank += __popcll(M & before);
+          tot += __popcll(M & hm);
         }
-        // non-temporal: the output is streamed, never re-read by this step (36.3 -> 33.7 ms
-        // per 6 GiB against plain stores, profiles/r01_v17_gather_nt.txt)
-        if (in) __builtin_nontemporal_store(v, &out[x]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (mk[e]) {
+            const int32_t xe = x + e, pos = xe < na[k] ? xe + 1 : xe + 2;
+            G.out_pos[po[k] + rank] = (uint16_t)pos;
+            G.out_lab[po[k] + rank] = v[k][e];
+            const int32_t d = dec[k][pos];
+            if (d != kKeep) v[k][e] = d;
+            ++rank;
+          }
+        }
+        rk[k] += tot;
       }
-      more |= n > cb + 64 * C;
-      if (cb == 0 && lane == 0) {
-        G.len_a[qb + k] = na[k];
-        G.is_rn[qb + k] = (uint8_t)rn[k];
+      // non-temporal: the output is streamed, never re-read by this step
+      int32_t* out = G.out_tok + tof[k];
+      if (x + 3 < n) {
+        __builtin_nontemporal_store(v[k], reinterpret_cast<tok4_t*>(out + x));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (x + e < n) __builtin_nontemporal_store(v[k][e], out + x + e);
       }
+      more |= n > cb + 128;
     }
-    if (!more) break;
+    if (!ballot(more)) break;
   }
 }
 
@@ -1646,7 +1670,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     max_pred = (int32_t)rint((double)prm->seq * prm->masked_lm_ratio);
     if (max_pred < 1) max_pred = 1;
     if (max_pred > prm->seq) max_pred = prm->seq;
-    if (max_pred > kMaxPredLds) TRY((set_error("masked_lm_ratio * seq too large"), -1));
+
   }
   P->max_pred = max_pred;
   if (prm->rng == LDDL_RNG_NATIVE) {
@@ -1866,9 +1890,7 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
   G.rec = P->rec;
   G.mpos = P->mpos;
   G.mtok = P->mtok;
-  G.max_pred = P->max_pred;
   G.masking = P->masking;
-  G.seq = P->seq;
   G.n_pairs = P->n_pairs;
   G.tok_off = P->tok_off;
   G.pos_off = P->pos_off;
@@ -1877,19 +1899,20 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
   G.is_rn = d_is_rn;
   G.out_pos = d_pos;
   G.out_lab = d_lab;
-  GatherLds Lg{(P->seq + 1) & ~1, P->max_pred};
+  GatherLds Lg{(P->seq + 31) / 32, P->seq};
   auto launch = [&](auto kern, int K) {
-    const int64_t per_wg = (int64_t)K * kGWaves;
-    const size_t lds = P->masking ? (size_t)kGWaves * Lg.per_wave(K) : 0;
-    hipLaunchKernelGGL(kern, dim3((unsigned)((P->n_pairs + per_wg - 1) / per_wg)),
-                       dim3(64 * kGWaves), lds, st, G, Lg);
+    const int64_t per_wg = (int64_t)2 * K * kGWaves;
+    const int64_t nwg = (P->n_pairs + per_wg - 1) / per_wg;
+    const int64_t gx = std::min<int64_t>(nwg, 65536);
+    const size_t lds = P->masking ? (size_t)kGWaves * 2 * K * Lg.per_pair() : 0;
+    hipLaunchKernelGGL(kern, dim3((unsigned)gx, (unsigned)((nwg + gx - 1) / gx)), dim3(64 * kGWaves),
+                       lds, st, G, Lg);
   };
-#ifndef LDDL_GK128
-#define LDDL_GK128 4
+#ifndef LDDL_GK
+#define LDDL_GK 2
 #endif
-  if (P->seq <= 131) launch(gather_kernel<LDDL_GK128, 2>, LDDL_GK128);
-  else if (P->seq <= 259) launch(gather_kernel<4, 4>, 4);
-  else launch(gather_kernel<2, 8>, 2);
+  if (P->seq <= 600) launch(gather_kernel<LDDL_GK>, LDDL_GK);
+  else launch(gather_kernel<1>, 1);  // (LDS: seq-entry decision tables)
   LDDL_HIP(hipGetLastError());
   if (d_tok_off)
     LDDL_HIP(hipMemcpyAsync(d_tok_off, P->tok_off, 8 * (P->n_pairs + 1), hipMemcpyDeviceToDevice, st));
