@@ -1361,21 +1361,19 @@ __global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(Gather
       G.is_rn[q] = (uint8_t)((uint32_t)r.nb_rn >> 31);
     }
   }
+  // a lane's 4 tokens: one 16-byte load from A (x < na) and/or one from B (x + 3 >= na), each
+  // at the offset of token x in that window (dense is padded by 4 tokens on both sides, so a
+  // load overhanging its window stays in bounds); element e comes from A iff x + e < na
   auto load_tokens = [&](int32_t x, tok4_t* v) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int32_t n = na[k] + nb[k];
-      if (x + 3 < na[k]) {
-        v[k] = *reinterpret_cast<const tok4_t*>(G.dense + aoff[k] + x);
-      } else if (x >= na[k] && x + 3 < n) {
-        v[k] = *reinterpret_cast<const tok4_t*>(G.dense + boff[k] + (x - na[k]));
-      } else {
+      tok4_t a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+      if (x < na[k]) a = *reinterpret_cast<const tok4_t*>(G.dense + aoff[k] + x);
+      if (x + 3 >= na[k] && x < n) b = *reinterpret_cast<const tok4_t*>(G.dense + boff[k] + (x - na[k]));
+      const int32_t ra = na[k] - x;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int32_t xe = x + e;
-          v[k][e] = xe < na[k] ? G.dense[aoff[k] + xe] : xe < n ? G.dense[boff[k] + (xe - na[k])] : 0;
-        }
-      }
+      for (int e = 0; e < 4; ++e) v[k][e] = e < ra ? a[e] : b[e];
     }
   };
   tok4_t v[K];
@@ -1402,12 +1400,20 @@ __global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(Gather
     for (int k = 0; k < K; ++k) {
       const int32_t n = na[k] + nb[k];
       if (G.masking) {
+        // bits x .. x+4 of the bitmap (x is a multiple of 4: they span words x/32 and x/32 + 1
+        // only when x % 32 == 28); element e is bit x + e (A) or x + e + 1 (B)
+        const int wi = x >> 5;
+        uint32_t win = bm[k][wi] >> (x & 31);
+        if ((x & 31) == 28) win |= (wi + 1 < W ? bm[k][wi + 1] : 0u) << 4;
+        const int32_t ra = na[k] - x, rn_ = n - x;
+        const uint32_t am = ra >= 4 ? 0xFu : ra <= 0 ? 0u : ((1u << ra) - 1u);
+        const uint32_t vm = rn_ >= 4 ? 0xFu : rn_ <= 0 ? 0u : ((1u << rn_) - 1u);
+        const uint32_t m4 = ((win & am) | ((win >> 1) & ~am)) & vm;
         bool mk[4];
         int rank = rk[k], tot = 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int32_t xe = x + e, b = xe < na[k] ? xe : xe + 1;
-          mk[e] = xe < n && ((bm[k][b >> 5] >> (b & 31)) & 1u);
+          mk[e] = (m4 >> e) & 1u;
           const uint64_t M = ballot(mk[e]);
           rank += __popcll(M & before);
           tot += __popcll(M & hm);
@@ -1658,7 +1664,9 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   int64_t n_kept_tok = 0;
   LDDL_HIP(hipMemcpyAsync(&n_kept_tok, P->kscan + P->n_kept_sent, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
-  TRY(P->alloc(&P->dense, n_kept_tok, st));
+  // 4 tokens of padding on both sides: the gather's 16-byte loads may overhang a window
+  TRY(P->alloc(&P->dense, n_kept_tok + 8, st));
+  P->dense += 4;
   if (P->n_kept_sent)
     hipLaunchKernelGGL(densify_kernel, dim3((unsigned)((P->n_kept_sent + 255) / 256)), dim3(256), 0,
                        st, P->ks_start, P->ks_len, P->kscan, P->n_kept_sent, d_ids, P->dense);
