@@ -1,6 +1,8 @@
 // Host-side context: device copies of the normaliser table and the vocab hash.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -43,6 +45,7 @@ class DevArena {
     }
     out = Block{};
     out.size = want;
+    if (getenv("LDDL_ARENA_DEBUG")) fprintf(stderr, "[arena] hipMalloc %zu bytes (%zu cached)\n", want, free_.size());
     hipError_t e = hipMalloc(&out.p, want);
     if (e != hipSuccess) {  // release the cached blocks and retry once
       (void)hipGetLastError();

@@ -123,6 +123,9 @@ __device__ inline uint32_t temper(uint32_t y) {
   return y;
 }
 
+#ifndef LDDL_FY_NW
+#define LDDL_FY_NW 1
+#endif
 struct WaveRng {
   uint32_t* mt;  // LDS raw state [624]
   uint32_t* tw;  // unused (the block is tempered on read; keeps LDS at one 624-word state)
@@ -215,47 +218,78 @@ struct WaveRng {
     return v;
   }
   // Fisher-Yates draws of random.shuffle over n items: j_i = _randbelow(i+1), i = n-1 .. 1,
-  // delivered as sink(i, j_i). Wave-parallel over 64 words at a time. Word t of the window is
-  // drawn for step i_t = s0 - t + R_t (R_t = rejections before t) and rejected iff
-  // (w_t >> (32 - bit_length(i_t + 1))) > i_t. R is the fixed point of R_t = #{u < t : rejected
-  // under R_u}, found by Jacobi iteration on ballots: the recurrence is causal, so every pass
-  // fixes at least the first wrong lane, and in practice 4-8 passes settle a whole window across
-  // any number of bit-length buckets. Each pass is a handful of VALU ops and one ballot.
-  template <typename Sink>
+  // delivered as sink(i, j_i). Wave-parallel over a window of 64 * NW words (lane l holds words
+  // l, 64 + l, ...). Word t of the window is drawn for step i_t = s0 - t + R_t (R_t = rejections
+  // before t) and rejected iff (w_t >> (32 - bit_length(i_t + 1))) > i_t, i.e. iff
+  // (w_t >> clz(i_t + 1)) > i_t. R is the fixed point of R_t = #{u < t : rejected under R_u},
+  // found by Jacobi iteration on ballots: the recurrence is causal, so every pass fixes at least
+  // the first wrong word, and in practice a handful of passes settle a window. The NW words of a
+  // lane are independent within a pass, so a wider window costs latency once per pass (the
+  // chain is latency-bound) while covering NW times the words.
+  template <int NW, typename Sink>
   __device__ void fy_draws(int64_t n, Sink sink) {
     const int lane = threadIdx.x;
     int32_t s0 = (int32_t)(n - 1);  // next step (uniform); n < 2^30 (host-checked)
     while (s0 >= 1) {
       if (mti >= kN) twist();
-      const int L = min(64, kN - mti);
-      const uint32_t w = lane < L ? temper(mt[mti + lane]) : 0u;
-      const uint64_t Lm = L >= 64 ? ~0ull : ((1ull << L) - 1);
-      int32_t R = 0, i;
-      uint64_t rej = 0;
-      uint32_t x;
+      const int L = min(64 * NW, kN - mti);
+      uint32_t w[NW];
+      uint64_t Lm[NW], rej[NW];
+      int32_t R[NW], i[NW];
+      uint32_t x[NW];
+#pragma unroll
+      for (int c = 0; c < NW; ++c) {
+        const int t = 64 * c + lane;
+        w[c] = t < L ? temper(mt[mti + t]) : 0u;
+        const int lc = L - 64 * c;
+        Lm[c] = lc >= 64 ? ~0ull : lc <= 0 ? 0ull : ((1ull << lc) - 1);
+        R[c] = 0;
+        rej[c] = 0;
+      }
       while (true) {  // R = 0 is the first guess; at most L + 1 passes (causality)
-        i = s0 - lane + R;
-        const int k = 32 - __clz((uint32_t)(i + 1));
-        x = w >> ((32 - k) & 31);  // meaningful for i >= 1 only
-        // lane masks straight from the compares (no boolean round trip through a VGPR)
-        const uint64_t bm = Lm & __builtin_amdgcn_sicmp(i, 0, 38 /* sgt */) &
-                            __builtin_amdgcn_uicmp(x, (uint32_t)i, 34 /* ugt */);
+        bool same = true;
+        uint64_t bm[NW];
+#pragma unroll
+        for (int c = 0; c < NW; ++c) {
+          i[c] = s0 - (64 * c + lane) + R[c];
+          x[c] = w[c] >> (__clz((uint32_t)(i[c] + 1)) & 31);  // meaningful for i >= 1 only
+          // lane masks straight from the compares (no boolean round trip through a VGPR)
+          bm[c] = Lm[c] & __builtin_amdgcn_sicmp(i[c], 0, 38 /* sgt */) &
+                  __builtin_amdgcn_uicmp(x[c], (uint32_t)i[c], 34 /* ugt */);
+          same &= bm[c] == rej[c];
+        }
 #ifdef LDDL_STAMPS
         ++n_pass;
 #endif
-        if (bm == rej) break;
-        rej = bm;
-        R = (int32_t)popc_below(rej);
+        if (same) break;
+        int32_t below = 0;
+#pragma unroll
+        for (int c = 0; c < NW; ++c) {
+          rej[c] = bm[c];
+          R[c] = below + (int32_t)popc_below(rej[c]);
+          below += __popcll(rej[c]);
+        }
       }
 #ifdef LDDL_STAMPS
       ++n_win;
 #endif
-      // words consumed: up to the first lane past the last step (i < 1) or the window end
-      const uint64_t fin = Lm & __builtin_amdgcn_sicmp(i, 1, 40 /* slt */);
-      const int E = fin ? __ffsll((unsigned long long)fin) - 1 : L;
-      if (lane < E && !((rej >> lane) & 1ull)) sink((int64_t)i, x);
+      // words consumed: up to the first word past the last step (i < 1) or the window end
+      int E = L;
+#pragma unroll
+      for (int c = NW - 1; c >= 0; --c) {
+        const uint64_t fin = Lm[c] & __builtin_amdgcn_sicmp(i[c], 1, 40 /* slt */);
+        if (fin) E = 64 * c + __ffsll((unsigned long long)fin) - 1;
+      }
+      int nrej = 0;
+#pragma unroll
+      for (int c = 0; c < NW; ++c) {
+        const int t = 64 * c + lane;
+        if (t < E && !((rej[c] >> lane) & 1ull)) sink((int64_t)i[c], x[c]);
+        const int ec = E - 64 * c;
+        nrej += __popcll(rej[c] & (ec >= 64 ? ~0ull : ec <= 0 ? 0ull : ((1ull << ec) - 1)));
+      }
       mti += E;
-      s0 -= E - __popcll(rej & (E >= 64 ? ~0ull : ((1ull << E) - 1)));
+      s0 -= E - nrej;
       s0 = uni(s0);
       mti = uni(mti);
     }
@@ -499,7 +533,10 @@ __device__ int32_t span_token(const PlanArgs& A, int64_t k0, int64_t j) {
   return A.dense[A.kscan[k0] + j];
 }
 
-__global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
+#ifndef LDDL_PLAN_MINW
+#define LDDL_PLAN_MINW 8
+#endif
+__global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* s_mt = reinterpret_cast<uint32_t*>(smem);
   uint32_t* s_tw = nullptr;
@@ -627,12 +664,12 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
           // random.shuffle(cand_indexes): draws j_i (i = nc-1 .. 1) to the pool
           if (A.jbytes == 1) {
             uint8_t* jd = static_cast<uint8_t*>(A.jpool) + jb;
-            rng.fy_draws(nc, [&](int64_t i, uint32_t j) {
+            rng.template fy_draws<LDDL_FY_NW>(nc, [&](int64_t i, uint32_t j) {
               if (fits) jd[i] = (uint8_t)j;
             });
           } else {
             uint16_t* jd = static_cast<uint16_t*>(A.jpool) + jb;
-            rng.fy_draws(nc, [&](int64_t i, uint32_t j) {
+            rng.template fy_draws<LDDL_FY_NW>(nc, [&](int64_t i, uint32_t j) {
               if (fits) jd[i] = (uint16_t)j;
             });
           }
@@ -661,7 +698,7 @@ __global__ void __launch_bounds__(64) plan_replay_kernel(PlanArgs A) {
   STAMP_ADD(0, st_t);
   {
     int32_t* js = A.jseq + base;
-    rng.fy_draws(np, [&](int64_t i, uint32_t j) { js[i] = (int32_t)j; });
+    rng.template fy_draws<LDDL_FY_NW>(np, [&](int64_t i, uint32_t j) { js[i] = (int32_t)j; });
   }
   STAMP_ADD(6, st_t);
 #ifdef LDDL_STAMPS
@@ -1081,7 +1118,8 @@ __global__ void __launch_bounds__(256) pair_prep_kernel(const int64_t* __restric
                                                         const int64_t* __restrict__ kscan,
                                                         const int32_t* __restrict__ nmask,
                                                         const int64_t* __restrict__ moff,
-                                                        GatherRec* __restrict__ rec) {
+                                                        GatherRec* __restrict__ rec,
+                                                        int2* __restrict__ cnt) {
   const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (q >= n) return;
   const int64_t slot = src[q];
@@ -1095,17 +1133,16 @@ __global__ void __launch_bounds__(256) pair_prep_kernel(const int64_t* __restric
   r.nm = nmask ? nmask[slot] : 0;
   r.pad = 0;
   rec[q] = r;
+  cnt[q] = make_int2(r.na + (r.nb_rn & 0x7FFFFFFF), r.nm);  // compact input of the two scans
 }
 
 struct PairTokens {
-  const GatherRec* r;
-  __device__ int64_t operator()(int64_t q) const {
-    return (int64_t)r[q].na + (r[q].nb_rn & 0x7FFFFFFF);
-  }
+  const int2* c;
+  __device__ int64_t operator()(int64_t q) const { return c[q].x; }
 };
 struct PairMasks {
-  const GatherRec* r;
-  __device__ int64_t operator()(int64_t q) const { return r[q].nm; }
+  const int2* c;
+  __device__ int64_t operator()(int64_t q) const { return c[q].y; }
 };
 
 // Kept tokens packed densely in kept-sentence order: kept sentence k's pieces are
@@ -1331,7 +1368,6 @@ __global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(Gather
   const int64_t wg = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
   const int64_t q0 = (wg * kGWaves + w) * 2 * K;  // pairs q0 + 2k + h
   const uint64_t hm = h ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
-  const uint64_t before = ((1ull << lane) - 1ull) & hm;  // lanes before this one in its half
   const int W = Lg.W;
 
   int64_t tof[K], aoff[K], boff[K], po[K], mb[K];
@@ -1415,8 +1451,11 @@ __global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(Gather
         for (int e = 0; e < 4; ++e) {
           mk[e] = (m4 >> e) & 1u;
           const uint64_t M = ballot(mk[e]);
-          rank += __popcll(M & before);
-          tot += __popcll(M & hm);
+          const uint32_t lo = (uint32_t)M, hi = (uint32_t)(M >> 32);
+          const int plo = __popc(lo), phi = __popc(hi);  // wave-uniform
+          // masked elements in the lanes before this one, minus the lower half's for the upper
+          rank += (int)__builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u)) - (h ? plo : 0);
+          tot += h ? phi : plo;
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1859,19 +1898,21 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   const int64_t npairs = P->n_pairs;
   TRY(P->alloc(&P->tok_off, npairs + 1, st));
   TRY(P->alloc(&P->rec, npairs, st));
+  int2* pcnt;
+  TRY(P->alloc(&pcnt, npairs, st));
   if (npairs)
     hipLaunchKernelGGL(pair_prep_kernel, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, st,
                        P->src, npairs, P->desc, P->kscan, prm->masking ? P->nmask : nullptr,
-                       P->moff, P->rec);
+                       P->moff, P->rec, pcnt);
   LDDL_HIP(hipGetLastError());
   int64_t* scr2;
   TRY(P->alloc(&scr2, scan_scratch_elems(npairs), st));
-  if (scan_exclusive(PairTokens{P->rec}, npairs, P->tok_off, scr2, st) != hipSuccess)
+  if (scan_exclusive(PairTokens{pcnt}, npairs, P->tok_off, scr2, st) != hipSuccess)
     TRY(-100);
   LDDL_HIP(hipMemcpyAsync(&P->n_tokens, P->tok_off + npairs, 8, hipMemcpyDeviceToHost, st));
   if (prm->masking) {
     TRY(P->alloc(&P->pos_off, npairs + 1, st));
-    if (scan_exclusive(PairMasks{P->rec}, npairs, P->pos_off, scr2, st) != hipSuccess)
+    if (scan_exclusive(PairMasks{pcnt}, npairs, P->pos_off, scr2, st) != hipSuccess)
       TRY(-100);
     LDDL_HIP(hipMemcpyAsync(&P->n_masked, P->pos_off + npairs, 8, hipMemcpyDeviceToHost, st));
   }
