@@ -1,5 +1,6 @@
 // Device-side shared definitions: context tables, vocab hash, wave primitives.
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -84,14 +85,35 @@ constexpr int32_t kLenMask = (1 << 30) - 1;
 // ---- wave helpers (wave64) ----
 __device__ inline int lane_id() { return __lane_id(); }
 
+// Inclusive prefix sum over the 64 lanes (all lanes active) with DPP: row_shr 1/2/4/8 sums
+// within each 16-lane row, then row_bcast:15 and row_bcast:31 carry the row totals (GFX9 DPP).
+// Six VALU ops with DPP source modifiers per 32-bit half; no LDS traffic, no lane masks.
+template <int kCtrl, int kRowMask, bool kBound>
+__device__ inline uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xF, kBound);
+}
+template <int kCtrl, int kRowMask, bool kBound>
+__device__ inline uint32_t scan_step(uint32_t v) {
+  return v + dpp_u32<kCtrl, kRowMask, kBound>(v);
+}
+template <int kCtrl, int kRowMask, bool kBound>
+__device__ inline uint64_t scan_step(uint64_t v) {
+  const uint32_t lo = dpp_u32<kCtrl, kRowMask, kBound>((uint32_t)v);
+  const uint32_t hi = dpp_u32<kCtrl, kRowMask, kBound>((uint32_t)(v >> 32));
+  return v + (((uint64_t)hi << 32) | lo);
+}
 template <typename T>
 __device__ inline T wave_incl_scan(T v) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    T o = __shfl_up(v, d, 64);
-    if (lane_id() >= d) v += o;
-  }
-  return v;
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit scan");
+  using U = std::conditional_t<sizeof(T) == 4, uint32_t, uint64_t>;
+  U u = (U)v;
+  u = scan_step<0x111, 0xF, true>(u);   // row_shr:1
+  u = scan_step<0x112, 0xF, true>(u);   // row_shr:2
+  u = scan_step<0x114, 0xF, true>(u);   // row_shr:4
+  u = scan_step<0x118, 0xF, true>(u);   // row_shr:8
+  u = scan_step<0x142, 0xA, false>(u);  // row_bcast:15 -> rows 1, 3
+  u = scan_step<0x143, 0xC, false>(u);  // row_bcast:31 -> rows 2, 3
+  return (T)u;
 }
 
 // Philox4x32-10 (Salmon et al., SC'11)
