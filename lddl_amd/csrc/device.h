@@ -102,6 +102,10 @@ __device__ inline uint64_t scan_step(uint64_t v) {
   const uint32_t hi = dpp_u32<kCtrl, kRowMask, kBound>((uint32_t)(v >> 32));
   return v + (((uint64_t)hi << 32) | lo);
 }
+// v of lane l - 1 (lane 0: its own v) / of lane l + 1 (lane 63: its own v): whole-wave DPP shifts
+__device__ inline int wave_prev(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false); }
+__device__ inline int wave_next(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xF, 0xF, false); }
+
 template <typename T>
 __device__ inline T wave_incl_scan(T v) {
   static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit scan");

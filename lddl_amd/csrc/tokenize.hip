@@ -392,16 +392,19 @@ __device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
     }
   }
   const uint64_t V2 = ballot(cplen == 2), V3 = ballot(cplen == 3), V4 = ballot(cplen == 4);
-  const uint64_t C1 = (V2 | V3 | V4) << 1, C2 = (V3 | V4) << 2, C3 = V4 << 3;
-  const bool covered = cont && (((C1 | C2 | C3) >> lane) & 1ull);
-  const int dist = !covered ? 0 : ((C1 >> lane) & 1ull) ? 1 : ((C2 >> lane) & 1ull) ? 2 : 3;
-  // a covered continuation inherits its lead's class; cp_last marks a code point's last byte
-  const int lead_len = __shfl((int)(cls | ((uint32_t)cplen << 4)), lane - dist, 64);
-  if (covered) {
-    cls = (uint32_t)lead_len & 3u;
-    cplen = 0;
+  bool cp_last = cplen <= 1;
+  if (V2 | V3 | V4) {  // multi-byte code points in the window (wave-uniform branch)
+    const uint64_t C1 = (V2 | V3 | V4) << 1, C2 = (V3 | V4) << 2, C3 = V4 << 3;
+    const bool covered = cont && (((C1 | C2 | C3) >> lane) & 1ull);
+    const int dist = !covered ? 0 : ((C1 >> lane) & 1ull) ? 1 : ((C2 >> lane) & 1ull) ? 2 : 3;
+    // a covered continuation inherits its lead's class; cp_last marks a code point's last byte
+    const int lead_len = __shfl((int)(cls | ((uint32_t)cplen << 4)), lane - dist, 64);
+    if (covered) {
+      cls = (uint32_t)lead_len & 3u;
+      cplen = 0;
+    }
+    cp_last = covered ? (dist == (lead_len >> 4) - 1) : (cplen <= 1);
   }
-  const bool cp_last = covered ? (dist == (lead_len >> 4) - 1) : (cplen <= 1);
   const uint64_t S = ballot(spk >= 0), S6 = ballot(spk == kMask);
   const uint64_t inside = (S << 1) | (S << 2) | (S << 3) | (S << 4) | (S6 << 5);
   const bool in_sp = ((S | inside) >> lane) & 1ull;
@@ -727,9 +730,12 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
   __syncthreads();
   const int lane = lane_id();
   BatchLds& W = s_w[threadIdx.x >> 6];
-  const int64_t s_first = (int64_t)blockIdx.x * kBW + (threadIdx.x >> 6);
-  const int64_t stride = (int64_t)gridDim.x * kBW;
-  int64_t head = 0, tail = 0;  // ordinals of in-flight sentences: [head, tail)
+  // sentence indices fit int32 (lddl_tokenize: n_sent < INT32_MAX); 32-bit state keeps the
+  // loop's scalar registers from spilling
+  const int32_t s_first = (int32_t)blockIdx.x * kBW + (int32_t)(threadIdx.x >> 6);
+  const int32_t stride = (int32_t)gridDim.x * kBW;
+  const int32_t n_sent32 = (int32_t)n_sent;
+  int32_t head = 0, tail = 0;  // ordinals of in-flight sentences: [head, tail)
   int qn = 0;
   bool cur = false;
   int cur_slot = 0;
@@ -749,11 +755,11 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
       const int slot = act ? W.q_slot[u] : -1;
       const int incl = wave_incl_scan(npc);
       const int excl = incl - npc;
-      const int prev_slot = __shfl(slot, lane > 0 ? lane - 1 : 0, 64);
+      const int prev_slot = wave_prev(slot);
       const uint64_t F = ballot(act && (lane == 0 || slot != prev_slot));
       const int s0 = 63 - __clzll(F & (lane == 63 ? ~0ull : ((2ull << lane) - 1)));
       const int seg_excl = excl - __shfl(excl, s0, 64);
-      const int next_slot = __shfl(slot, lane < 63 ? lane + 1 : 63, 64);
+      const int next_slot = wave_next(slot);
       const bool seg_last = act && (lane == 63 || u + 1 >= u1 || next_slot != slot);
       if (act) {
         const int o = W.r_count[slot] + seg_excl;
@@ -890,8 +896,8 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
 
   while (true) {
     if (!cur) {
-      const int64_t s = s_first + tail * stride;
-      if (s >= n_sent) break;
+      const int32_t s = s_first + tail * stride;  // < n_sent + stride < 2^31
+      if (s >= n_sent32) break;
       if (tail - head == kRing) {  // ring full: make room
         flush();
         retire();
@@ -906,7 +912,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
         b1 = sent_off[s + 1];
       }
       nb0 = nb1 = -1;
-      if (s + stride < n_sent) {
+      if (s < n_sent32 - stride) {
         nb0 = sent_off[s + stride];
         nb1 = sent_off[s + stride + 1];
       }
