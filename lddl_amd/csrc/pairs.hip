@@ -128,7 +128,7 @@ __device__ inline uint32_t temper(uint32_t y) {
 #endif
 struct WaveRng {
   uint32_t* mt;  // LDS raw state [624]
-  uint32_t* tw;  // unused (the block is tempered on read; keeps LDS at one 624-word state)
+  uint32_t* tw;  // unused (a tempered copy of the block in LDS cut occupancy: 7 KB -> 5 waves/SIMD)
   int mti;       // next word of the block (uniform)
   int wbase;     // window base (uniform)
   uint32_t win;  // this lane's tempered word temper(mt[wbase + lane])
@@ -246,16 +246,28 @@ struct WaveRng {
         R[c] = 0;
         rej[c] = 0;
       }
+      // with u = i + 1 (the draw's bound): x = w >> clz(u), rejected iff x >= u; every step of
+      // the window is >= 1 when s0 >= 64 NW, otherwise the steps < 1 are masked out
+      const bool tail = s0 < 64 * NW;
+      int32_t u1[NW];
+#pragma unroll
+      for (int c = 0; c < NW; ++c) u1[c] = s0 + 1 - (64 * c + lane);
       while (true) {  // R = 0 is the first guess; at most L + 1 passes (causality)
         bool same = true;
         uint64_t bm[NW];
 #pragma unroll
         for (int c = 0; c < NW; ++c) {
-          i[c] = s0 - (64 * c + lane) + R[c];
-          x[c] = w[c] >> (__clz((uint32_t)(i[c] + 1)) & 31);  // meaningful for i >= 1 only
+          const int32_t u = u1[c] + R[c];
+          x[c] = w[c] >> (__clz((uint32_t)u) & 31);  // meaningful for u >= 2 only
           // lane masks straight from the compares (no boolean round trip through a VGPR)
-          bm[c] = Lm[c] & __builtin_amdgcn_sicmp(i[c], 0, 38 /* sgt */) &
-                  __builtin_amdgcn_uicmp(x[c], (uint32_t)i[c], 34 /* ugt */);
+          uint64_t m = Lm[c] & __builtin_amdgcn_uicmp(x[c], (uint32_t)u, 35 /* uge */);
+#ifdef LDDL_FY_TAILBR
+          if (tail) m &= __builtin_amdgcn_sicmp(u, 1, 38 /* sgt */);
+#else
+          (void)tail;
+          m &= __builtin_amdgcn_sicmp(u, 1, 38 /* sgt */);
+#endif
+          bm[c] = m;
           same &= bm[c] == rej[c];
         }
 #ifdef LDDL_STAMPS
@@ -273,6 +285,8 @@ struct WaveRng {
 #ifdef LDDL_STAMPS
       ++n_win;
 #endif
+#pragma unroll
+      for (int c = 0; c < NW; ++c) i[c] = u1[c] + R[c] - 1;
       // words consumed: up to the first word past the last step (i < 1) or the window end
       int E = L;
 #pragma unroll
@@ -1767,7 +1781,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   A.stamps = d_stamps;
 #endif
   if (prm->seq > 512) TRY((set_error("replay planner supports target_seq_length <= 512"), -1));
-  const size_t lds = 4 * kN + 4 * (kDocLds + 4) + 16;
+  const size_t lds = 4 * kN + 4 * (kDocLds + 4) + 16;  // ~4.5 KB: 8 waves/SIMD fit the CU's LDS
   A.joff = joff;
   A.ncand = ncand;
   // pools: decisions (int32, shuffled order) and shuffle draws (uint16), sized from the kept

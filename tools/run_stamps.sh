@@ -3,5 +3,5 @@ cd /root/repo
 export TMPDIR=/tmp
 O=gpurun_out/$1
 mkdir -p $O
-LDDL_AMD_LIB=lddl_amd/_lib_diag/liblddl_amd.so timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 1 --warmup 0 --no-alt-rng --no-segmented-line --no-extra-lines --batch-bytes 4294967296 > $O/stamps.log 2>&1 || exit 1
+LDDL_AMD_LIB=lddl_amd/_lib_diag/liblddl_amd.so timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 1 --warmup 0 --no-alt-rng --no-segmented-line --no-extra-lines > $O/stamps.log 2>&1 || exit 1
 echo ALLDONE
