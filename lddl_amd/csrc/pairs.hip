@@ -1179,15 +1179,17 @@ __global__ void __launch_bounds__(256) densify_kernel(const int64_t* __restrict_
   const int32_t incl = wave_incl_scan(len);
   const int32_t total = __shfl(incl, 63, 64);
   const int64_t base = kscan[k0];
+  // the sentence loop indices are wave-uniform: lane values via readlane, not LDS permutes
+  auto rl = [](int32_t v, int i) { return __builtin_amdgcn_readlane(v, i); };
   int j = 0;
   for (int32_t c0 = 0; c0 < total; c0 += 64) {
     const int32_t x = c0 + lane, hi = min(c0 + 63, total - 1);
-    while (__shfl(incl, j, 64) <= c0) ++j;  // first sentence overlapping the chunk
+    while (rl(incl, j) <= c0) ++j;  // first sentence overlapping the chunk
     int64_t src = 0;
     for (int jj = j;; ++jj) {
-      const int32_t e = __shfl(incl, jj, 64);
-      const int32_t b = e - __shfl(len, jj, 64);
-      const int64_t s = __shfl(st, jj, 64);
+      const int32_t e = rl(incl, jj);
+      const int32_t b = e - rl(len, jj);
+      const int64_t s = ((int64_t)rl((int32_t)(st >> 32), jj) << 32) | (uint32_t)rl((int32_t)st, jj);
       if (x >= b && x < e) src = s + (x - b);
       if (e > hi) break;
     }
