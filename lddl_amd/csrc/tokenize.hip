@@ -837,10 +837,69 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
       }
       wave_sync();  // every normalised word is in registers: the rows become piece columns
       int npc = 0;
+#ifdef LDDL_TOK_COOP
+      // A/B experiment (the north_star matcher): a half-wave per hard word,
+      // lane (l & 31) probes piece length (l & 31) + 1 at the current start, the ballot's
+      // highest hit is the greedy longest match; the owner lane's piece column gets the pieces
+      (void)known_miss;
+      {
+        const int hl = lane & 31;
+        const uint64_t hm = (lane >> 5) ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
+        int my_n = 0;  // lane < hn: pieces of its own word (set by its half's leader below)
+        for (int w2 = 0; w2 < hn; w2 += 2) {
+          const int src = w2 + (lane >> 5);
+          const bool valid = src < hn;
+          const int sl = valid ? src : 0;
+          auto sh64 = [&](uint64_t x) {
+            return ((uint64_t)(uint32_t)__shfl((int)(x >> 32), sl, 64) << 32) |
+                   (uint32_t)__shfl((int)(uint32_t)x, sl, 64);
+          };
+          const B32 v{sh64(uw.v.w0), sh64(uw.v.w1), sh64(uw.v.w2), sh64(uw.v.w3)};
+          const int nb = __shfl(uw.nb, sl, 64), st = __shfl(uw.status, sl, 64);
+          const uint64_t ends = sh64(uw.ends);
+          int start = 0, n = valid ? (st < 0 ? -1 : 0) : 0;
+          bool live = valid && st == 0 && nb > 0;
+          while (ballot(live)) {
+            const int L = hl + 1;
+            const bool cand = live && start + L <= nb && L <= T.max_piece_bytes &&
+                              ((ends >> (start + L)) & 1ull);
+            const int32_t id = cand ? probe32(T, shr_bytes(v, start), L, start > 0 ? 1u : 0u) : -1;
+            const uint64_t M = ballot(id >= 0) & hm;
+            if (live) {
+              if (!M) {  // no piece at this start: the whole word is [UNK]
+                if (hl == 0) W.pcs[sl] = T.special_id[kUnk];
+                n = 1;
+                live = false;
+              } else {
+                const int best = 63 - __clzll(M);  // lane of the longest hit
+                const int32_t bid = __shfl(id, best, 64);
+                if (n == kPcs) {
+                  n = -1;
+                  live = false;
+                } else {
+                  if (hl == 0) W.pcs[64 * n + sl] = bid;
+                  ++n;
+                  start += (best & 31) + 1;
+                  if (start >= nb) live = false;
+                }
+              }
+            }
+          }
+          // the owner lanes take their counts from the halves' leaders
+          const int c0 = __shfl(n, 0, 64), c1 = __shfl(n, 32, 64);
+          if (lane == w2) my_n = c0;
+          if (lane == w2 + 1) my_n = c1;
+        }
+        if (lane < hn) npc = my_n;
+        if (npc < 0) npc = -1;
+      }
+      if (lane < hn) {
+#else
       if (lane < hn) {
         Pcs pc{W.pcs + lane};
         if (uw.status == 0) npc = wordpiece32(T, s_bloom, uw.v, uw.nb, uw.ends, pc, known_miss);
         else if (uw.status < 0) npc = -1;
+#endif
         if (npc < 0) {  // the sentence goes to the lane kernel
           atomicOr(&W.r_flags[W.q_slot[u]], kFallback);
           npc = 0;
