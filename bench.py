@@ -46,6 +46,12 @@ def partition_docs(corp, partition_bytes):
     return cuts.astype(np.int64)
 
 
+# LDDL_BENCH_SHARE_DEVICE=1: every rank on cuda:0 with gloo collectives (CPU tensors) - a rehearsal
+# of the N > 1 bench logic on a one-GPU box; the driver's N > 1 runs use one GPU per rank + RCCL
+SHARE_DEVICE = os.environ.get('LDDL_BENCH_SHARE_DEVICE') == '1'
+RED_DEV = 'cpu' if SHARE_DEVICE else None
+
+
 def make_batch(rank, args):
     from lddl_amd import synth
     corp = synth.generate(seed=args.seed, n_bytes=args.batch_bytes, doc_begin=rank * 50_000_000,
@@ -164,7 +170,7 @@ def timed_segmented(args, rank, world, ctx, dev):
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt, float(n_tok)], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt, float(n_tok)], dtype=torch.float64, device=RED_DEV or dev)
         dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         dt, n_tok = float(t[0].item()), int(t[1].item())
@@ -409,8 +415,12 @@ def main():
         print(json.dumps(run_c5(args)), flush=True)
         return
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if SHARE_DEVICE:  # rehearsal of the multi-rank path on a one-GPU box (never the driver's run)
+            torch.cuda.set_device(0)
+            dist.init_process_group('gloo')
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     from lddl_amd.context import Context
     from lddl_amd.pairs import make_pairs
     from lddl_amd.balance import balance
@@ -506,10 +516,10 @@ def main():
             dist.barrier()
         dt = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            t = torch.tensor([dt], dtype=torch.float64, device=RED_DEV or dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
-            n = torch.tensor([out_tokens], dtype=torch.float64, device=dev)
+            n = torch.tensor([out_tokens], dtype=torch.float64, device=RED_DEV or dev)
             dist.all_reduce(n, op=dist.ReduceOp.SUM)
             out_tokens = int(n.item())
         return dt, out_tokens, evs, stats, sent_len

@@ -353,7 +353,9 @@ __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v,
 // holding a byte the register fast path cannot take. The caller stores what it needs.
 struct WinResult {
   int n_units;
-  int64_t next;
+  int next_lane;  // the next window starts at this lane's byte (64: after lane 63; -1: the last
+                  // segment is consumed to its end)
+  int64_t next;   // classify_window only: the same as a byte offset
   uint64_t slow;
   uint64_t US, UE;  // unit starts (a trailing incomplete unit included) / complete unit ends
   int ukind;        // this lane's unit kind when its US bit is set
@@ -361,13 +363,14 @@ struct WinResult {
   bool fallback;    // a unit of >= 64 bytes: the sentence goes to the lane kernel
 };
 
-// byte = text[pos + lane] (already loaded by the caller, which may prefetch it), any value when
-// pos + lane >= b1.
-__device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
-                                     const uint8_t* __restrict__ text, int64_t pos, int64_t b1,
-                                     uint32_t byte) {
+// Per-lane form: this lane's byte offset i, the end b1 of its sentence, and byte = text[i] (any
+// value when i >= b1). A window may hold two segments — the tail of one sentence and the head of
+// the next — with BRK holding the bit of the second segment's first lane (0: one segment);
+// units never cross it. tail_known: the byte after lane 63 is past the end of lane 63's sentence.
+__device__ WinResult classify_lanes(const Tables& T, const uint32_t* s_ascii,
+                                    const uint8_t* __restrict__ text, int64_t i, int64_t b1,
+                                    uint32_t byte, uint64_t BRK, bool tail_known) {
   const int lane = lane_id();
-  const int64_t i = pos + lane;
   const bool in = i < b1;
   uint32_t cls = kSpace;  // beyond the sentence: a separator
   int cplen = 1;          // bytes of the code point starting here (0: covered continuation)
@@ -418,9 +421,8 @@ __device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
   R.fallback = false;
   R.ukind = spk >= 0 ? 2 + spk : cat == kCatIso ? 1 : 0;
   R.unit_byte = cat != kCatSep;
-  const bool tail_known = pos + 64 >= b1;  // position 64 is past the sentence end
-  const uint64_t US = S | (ISO & LEAD) | (RUN & ~(RUN << 1));
-  uint64_t RE = RUN & ~(RUN >> 1);
+  const uint64_t US = S | (ISO & LEAD) | (RUN & ~((RUN << 1) & ~BRK));
+  uint64_t RE = RUN & ~((RUN >> 1) & ~(BRK >> 1));
   if (!tail_known) RE &= ~(1ull << 63);
   const uint64_t UE = ((S & ~S6) << 4) | (S6 << 5) | (ISO & CPL & ~inside) | RE;
   R.US = US;
@@ -431,18 +433,27 @@ __device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
     const int last = 63 - __clzll(US);
     if (last == 0) {  // a unit of >= 64 bytes
       R.fallback = true;
-      R.next = b1;
+      R.next_lane = -1;
       return R;
     }
-    R.next = pos + last;
+    R.next_lane = last;
   } else if (tail_known) {
-    R.next = b1;
+    R.next_lane = -1;
   } else {
     // a separator code point straddling the window end restarts the next window at its lead
     const int hl = 63 - __clzll(LEAD);
     const int hc = 63 - __clzll(CPL);
-    R.next = pos + (hl > hc ? hl : 64);
+    R.next_lane = hl > hc ? hl : 64;
   }
+  return R;
+}
+
+// One-sentence window [pos, pos + 64) of a sentence ending at b1; byte = text[pos + lane].
+__device__ WinResult classify_window(const Tables& T, const uint32_t* s_ascii,
+                                     const uint8_t* __restrict__ text, int64_t pos, int64_t b1,
+                                     uint32_t byte) {
+  WinResult R = classify_lanes(T, s_ascii, text, pos + lane_id(), b1, byte, 0ull, pos + 64 >= b1);
+  R.next = R.next_lane < 0 ? b1 : pos + R.next_lane;
   return R;
 }
 
@@ -744,6 +755,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
   // the queue flush runs), and the next sentence's offsets one sentence ahead
   uint32_t pbyte = 0x20u;
   int64_t ppos = -1;
+  int pk = 64;  // the prefetched window's second-segment lane
   int64_t nb0 = -1, nb1 = -1;
 
   // place queue units [u0, u1) (all resolved) in order: segmented scan per sentence
@@ -988,18 +1000,72 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
       ++tail;
     }
     if (pos < b1) {
-      const uint32_t byte = ppos == pos ? pbyte : (pos + lane < b1 ? text[pos + lane] : 0x20u);
-      const WinResult R = classify_window(T, s_ascii, text, pos, b1, byte);
+      // a tail shorter than a window shares it with the head of the wave's next sentence (lanes
+      // >= k): sentences average ~2 windows, so this saves ~1 window in 6
+      int k = 64;
+      int slotB = cur_slot;
+      int64_t b0B = 0, b1B = 0;
+#ifdef LDDL_TOK_NO_COMBINE  // A/B experiment only: one sentence per window
+      if (false) {
+#else
+      if (b1 - pos < 64 && nb0 >= 0 && tail - head < kRing) {
+#endif
+        const int32_t sn = s_first + tail * stride;  // the sentence nb0 / nb1 belong to
+        k = (int)(b1 - pos);
+        slotB = (int)(tail % kRing);
+        b0B = nb0;
+        b1B = nb1;
+        if (lane == 0) {
+          W.r_b0[slotB] = b0B;
+          W.r_sent[slotB] = sn;
+          W.r_count[slotB] = 0;
+          W.r_flags[slotB] = 0;
+          W.r_pending[slotB] = 0;
+        }
+        ++tail;
+        nb0 = nb1 = -1;
+        if (sn < n_sent32 - stride) {
+          nb0 = sent_off[sn + stride];
+          nb1 = sent_off[sn + stride + 1];
+        }
+      }
+      const bool segB = lane >= k;
+      const int64_t il = segB ? b0B + (lane - k) : pos + lane;
+      const int64_t b1l = segB ? b1B : b1;
+      const uint32_t byte = (ppos == pos && pk == k) ? pbyte : (il < b1l ? text[il] : 0x20u);
+      const bool tail_known = k < 64 ? b0B + (64 - k) >= b1B : pos + 64 >= b1;
+      const WinResult R = classify_lanes(T, s_ascii, text, il, b1l, byte, k < 64 ? 1ull << k : 0ull,
+                                         tail_known);
+      // where the next window starts, in the last segment's sentence
+      const int64_t lb1 = k < 64 ? b1B : b1;
+      int64_t next;
+      if (R.next_lane < 0) {
+        next = lb1;
+      } else {
+        const int nl = R.next_lane < 64 ? R.next_lane : 63;
+        next = ((int64_t)__builtin_amdgcn_readlane((int)(il >> 32), nl) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)il, nl);
+        if (R.next_lane == 64) ++next;
+      }
 #ifndef LDDL_TOK_NO_PREFETCH
-      if (R.next < b1) {
-        ppos = R.next;
-        pbyte = R.next + lane < b1 ? text[R.next + lane] : 0x20u;
+      // the next window's bytes, on the same lane mapping it will use (checked by pos and k)
+      if (next < lb1) {
+#ifdef LDDL_TOK_NO_COMBINE
+        const int kk = 64;
+#else
+        const int kk = lb1 - next < 64 && nb0 >= 0 && tail - head < kRing ? (int)(lb1 - next) : 64;
+#endif
+        const int64_t ip = lane >= kk ? nb0 + (lane - kk) : next + lane;
+        pbyte = ip < (lane >= kk ? nb1 : lb1) ? text[ip] : 0x20u;
+        ppos = next;
+        pk = kk;
       } else if (nb0 >= 0) {  // the next sentence's first window
         ppos = nb0;
+        pk = 64;
         pbyte = nb0 + lane < nb1 ? text[nb0 + lane] : 0x20u;
       }
 #endif
-      if (R.fallback) {
+      if (R.fallback) {  // (one segment only: a two-segment window's first units are complete)
         if (lane == 0) W.r_flags[cur_slot] |= kFallback;
         pos = b1;
       } else {
@@ -1010,19 +1076,31 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
         const int n = R.n_units;
         const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
         if ((R.US >> lane) & 1ull) {
-          const int k = qn + (int)popc_below(R.US);
-          W.q_rel[k] = (int32_t)(pos - b0 + lane);
-          W.q_kind[k] = (uint8_t)R.ukind;
-          W.q_slot[k] = (uint8_t)cur_slot;
-          W.q_slow[k] = 0;
+          const int q = qn + (int)popc_below(R.US);
+          W.q_rel[q] = (int32_t)(il - (segB ? b0B : b0));
+          W.q_kind[q] = (uint8_t)R.ukind;
+          W.q_slot[q] = (uint8_t)(segB ? slotB : cur_slot);
+          W.q_slow[q] = 0;
         }
         if ((R.UE >> lane) & 1ull)
           W.q_len[qn + (int)popc_below(R.UE)] = (uint8_t)(lane - (63 - __clzll(R.US & upto)) + 1);
         if (((R.slow >> lane) & 1ull) && R.unit_byte) W.q_slow[qn + __popcll(R.US & upto) - 1] = 1;
-        if (lane == 0) W.r_pending[cur_slot] += n;
+        if (k < 64) {  // the first segment's sentence is complete: the second one becomes current
+          const int na = __popcll(R.UE & ((1ull << k) - 1));
+          if (lane == 0) {
+            W.r_pending[cur_slot] += na;
+            W.r_flags[cur_slot] |= kClosed;
+            W.r_pending[slotB] += n - na;
+          }
+          cur_slot = slotB;
+          b0 = b0B;
+          b1 = b1B;
+        } else if (lane == 0) {
+          W.r_pending[cur_slot] += n;
+        }
         wave_sync();
         qn += n;
-        pos = R.next;
+        pos = next;
       }
     }
     if (pos >= b1) {
