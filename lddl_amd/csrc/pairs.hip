@@ -1477,8 +1477,13 @@ __global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(Gather
         for (int e = 0; e < 4; ++e) {
           if (mk[e]) {
             const int32_t xe = x + e, pos = xe < na[k] ? xe + 1 : xe + 2;
+#ifdef LDDL_GATHER_NT_MASKS  // A/B experiment only
+            __builtin_nontemporal_store((uint16_t)pos, G.out_pos + po[k] + rank);
+            __builtin_nontemporal_store(v[k][e], G.out_lab + po[k] + rank);
+#else
             G.out_pos[po[k] + rank] = (uint16_t)pos;
             G.out_lab[po[k] + rank] = v[k][e];
+#endif
             const int32_t d = dec[k][pos];
             if (d != kKeep) v[k][e] = d;
             ++rank;
@@ -1488,6 +1493,15 @@ __global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(Gather
       }
       // non-temporal: the output is streamed, never re-read by this step
       int32_t* out = G.out_tok + tof[k];
+#ifdef LDDL_GATHER_PLAIN_STORE  // A/B experiment only
+      if (x + 3 < n) {
+        *reinterpret_cast<tok4_t*>(out + x) = v[k];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (x + e < n) out[x + e] = v[k][e];
+      }
+#else
       if (x + 3 < n) {
         __builtin_nontemporal_store(v[k], reinterpret_cast<tok4_t*>(out + x));
       } else {
@@ -1495,6 +1509,7 @@ __global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(Gather
         for (int e = 0; e < 4; ++e)
           if (x + e < n) __builtin_nontemporal_store(v[k][e], out + x + e);
       }
+#endif
       more |= n > cb + 128;
     }
     if (!ballot(more)) break;
