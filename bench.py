@@ -615,9 +615,9 @@ def main():
     #  * planner kernel alone: its compulsory inputs and outputs - sentence lengths (4 B) and
     #    document offsets (8 B) per duplicate pass, a 16-B A/B window descriptor per pair and 6 B
     #    (position + decision) per mask.
-    # `roofline` is the kernel with the longer launch; `issue_roofline` sets each kernel's VALU
-    # instruction count (committed PMC pass of the same batch size) against the chip's VALU issue
-    # rate, the bound these kernels actually sit on.
+    # `roofline` is the kernel with the longer launch; `issue_roofline` sets each kernel's VALU and
+    # SALU instruction counts (committed PMC pass of the same batch size) against the chip's issue
+    # rates, the bounds these kernels actually sit on.
     n_bytes, n_sent = corp.text.size, corp.n_sent
     plan_bytes = (4 * 5 * st['kept_sent'] + 8 * 5 * st['kept_doc'] + 16 * n_pairs +
                   6 * st['masked'])
@@ -641,16 +641,24 @@ def main():
 
     def traffic(kernel):
         return pmc_kernels.get(kernel, {}).get('hbm_bytes_per_launch')
-    valu_peak = 256 * 4 * 2.4e9 / 4  # wave64 VALU instructions / s: 256 CUs x 4 SIMDs x 2.4 GHz / 4
+    # issue peaks per chip (profiles/r02_issue_rate_probe.txt, tools/ubench/issue_rate.hip): a
+    # SIMD issues one wave64 VALU instruction per 2 cycles (32-wide SIMD, >= 2 waves) and one SALU
+    # instruction per 4 cycles (the CU's scalar unit serves its 4 SIMDs in turn)
+    valu_peak = 256 * 4 * 2.4e9 / 2
+    salu_peak = 256 * 4 * 2.4e9 / 4
 
     def issue(kernel, ms):
-        v = pmc_kernels.get(kernel, {}).get('SQ_INSTS_VALU')
+        k = pmc_kernels.get(kernel, {})
+        v, sc = k.get('SQ_INSTS_VALU'), k.get('SQ_INSTS_SALU')
         if not v or not ms:
             return None
-        a = v / (ms * 1e-3)
-        return {'kernel': kernel, 'bound': 'valu_issue', 'valu_instructions_per_launch': v,
-                'achieved': a, 'peak': valu_peak, 'unit': 'wave64 VALU instr/s',
-                'frac': a / valu_peak, 'source': pmc_src}
+        a, sa = v / (ms * 1e-3), (sc or 0) / (ms * 1e-3)
+        return {'kernel': kernel, 'bound': 'salu_issue' if sa / salu_peak > a / valu_peak else 'valu_issue',
+                'valu_instructions_per_launch': v, 'achieved': a, 'peak': valu_peak,
+                'unit': 'wave64 VALU instr/s', 'frac': a / valu_peak,
+                'salu_instructions_per_launch': sc, 'salu_achieved': sa, 'salu_peak': salu_peak,
+                'salu_frac': sa / salu_peak, 'source': pmc_src,
+                'note': 'PMC pass taken on an earlier build of the same batch size'}
 
     plan_roof = {'kernel': 'plan_replay_kernel' if args.rng == 'replay' else
                  'plan_native_kernel x2 + mask_native_kernel + order_native_kernel (HIP events '
@@ -659,12 +667,12 @@ def main():
                  'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': plan_gbs / HBM_PEAK_GBS,
                  'traffic': traffic('plan_replay_kernel') if args.rng == 'replay' else None,
                  'algorithmic_bytes_per_launch': plan_bytes, 'launch_ms': plan_ms,
-                 'note': 'VALU-issue-bound (issue_roofline), not HBM-bound (DESIGN.md 4)'}
+                 'note': 'instruction-issue-bound (issue_roofline), not HBM-bound (DESIGN.md 4)'}
     tok_roof = {'kernel': 'tokenize_batch_kernel', 'bound': 'hbm', 'achieved': achieved,
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                 'traffic': traffic('tokenize_batch_kernel'), 'algorithmic_bytes_per_launch': tok_bytes,
                 'launch_ms': tok_ms,
-                'note': 'VALU-issue-bound (issue_roofline), not HBM-bound (DESIGN.md 4)'}
+                'note': 'instruction-issue-bound (issue_roofline), not HBM-bound (DESIGN.md 4)'}
     stage_roof = {'kernel': 'pair stage (compaction, densify, plan, shuffle, resolve, layout, '
                             'gather)', 'bound': 'hbm', 'achieved': stage_gbs,
                   'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': stage_gbs / HBM_PEAK_GBS,

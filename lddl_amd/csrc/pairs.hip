@@ -19,6 +19,7 @@
 //           the partition shuffle of pretrain.py:401).
 //   gather  one wave per pair: coalesced copy of A and B token spans from the tokenizer output,
 //           applying the mask decisions and emitting positions + labels.
+#include <algorithm>
 #include <cstdio>
 #include <vector>
 
@@ -123,9 +124,37 @@ __device__ inline uint32_t temper(uint32_t y) {
   return y;
 }
 
-#ifndef LDDL_FY_NW
-#define LDDL_FY_NW 1
-#endif
+// kFyGuess.m[s0]: the expected rejection pattern of a 64-word Fisher-Yates window whose first
+// word is drawn for step s0 (fy_draws' starting point), built by walking the window with the
+// expected rejection rate 1 - u / 2^bit_length(u) of each bound u and rejecting a word whenever
+// the running expectation passes the next half integer. Only a starting guess: any pattern
+// converges to the same draws.
+constexpr int kFyGuessN = 512;
+struct FyGuess {
+  uint64_t m[kFyGuessN];
+};
+constexpr FyGuess make_fy_guess() {
+  FyGuess g{};
+  for (int s0 = 0; s0 < kFyGuessN; ++s0) {
+    uint64_t m = 0;
+    double r = 0.0;
+    int R = 0;
+    for (int t = 0; t < 64; ++t) {
+      const int u = s0 + 1 - t + R;
+      if (u <= 1) break;
+      int k = 0;
+      while ((1 << k) <= u) ++k;
+      r += 1.0 - (double)u / (double)(1 << k);
+      if (r >= R + 0.5) {
+        m |= 1ull << t;
+        ++R;
+      }
+    }
+    g.m[s0] = m;
+  }
+  return g;
+}
+__constant__ FyGuess kFyGuess = make_fy_guess();
 struct WaveRng {
   uint32_t* mt;  // LDS raw state [624]
   uint32_t* tw;  // unused (a tempered copy of the block in LDS cut occupancy: 7 KB -> 5 waves/SIMD)
@@ -218,94 +247,94 @@ struct WaveRng {
     return v;
   }
   // Fisher-Yates draws of random.shuffle over n items: j_i = _randbelow(i+1), i = n-1 .. 1,
-  // delivered as sink(i, j_i). Wave-parallel over a window of 64 * NW words (lane l holds words
-  // l, 64 + l, ...). Word t of the window is drawn for step i_t = s0 - t + R_t (R_t = rejections
-  // before t) and rejected iff (w_t >> (32 - bit_length(i_t + 1))) > i_t, i.e. iff
-  // (w_t >> clz(i_t + 1)) > i_t. R is the fixed point of R_t = #{u < t : rejected under R_u},
-  // found by Jacobi iteration on ballots: the recurrence is causal, so every pass fixes at least
-  // the first wrong word, and in practice a handful of passes settle a window. The NW words of a
-  // lane are independent within a pass, so a wider window costs latency once per pass (the
-  // chain is latency-bound) while covering NW times the words.
-  template <int NW, typename Sink>
+  // delivered as sink(i, j_i). Wave-parallel over a window of 64 words (lane t holds word t).
+  // Word t of the window is drawn for step i_t = s0 - t + R_t (R_t = rejections before t) and
+  // rejected iff (w_t >> (32 - bit_length(i_t + 1))) > i_t, i.e. with u = i + 1 (the draw's
+  // bound) iff (w_t >> clz(u)) >= u. R is the fixed point of R_t = #{v < t : rejected under
+  // R_v}, found by Jacobi iteration on ballots: the recurrence is causal, so every pass fixes at
+  // least the first wrong word. The iteration starts from kFyGuess[s0], the rejection pattern a
+  // window starting at step s0 has when every word is rejected with its expected rate (fewer
+  // passes than starting from "no rejection"); any guess converges to the same fixed point.
+  // The pass is kept to one VALU compare + one scalar compare-and-branch: for s0 >= 64 every
+  // bound in the window is >= 2; a tail window clamps its bounds below 2 to "never rejected".
+  template <typename Sink>
   __device__ void fy_draws(int64_t n, Sink sink) {
     const int lane = threadIdx.x;
     int32_t s0 = (int32_t)(n - 1);  // next step (uniform); n < 2^30 (host-checked)
     while (s0 >= 1) {
       if (mti >= kN) twist();
-      const int L = min(64 * NW, kN - mti);
-      uint32_t w[NW];
-      uint64_t Lm[NW], rej[NW];
-      int32_t R[NW], i[NW];
-      uint32_t x[NW];
-#pragma unroll
-      for (int c = 0; c < NW; ++c) {
-        const int t = 64 * c + lane;
-        w[c] = t < L ? temper(mt[mti + t]) : 0u;
-        const int lc = L - 64 * c;
-        Lm[c] = lc >= 64 ? ~0ull : lc <= 0 ? 0ull : ((1ull << lc) - 1);
-        R[c] = 0;
-        rej[c] = 0;
-      }
-      // with u = i + 1 (the draw's bound): x = w >> clz(u), rejected iff x >= u; every step of
-      // the window is >= 1 when s0 >= 64 NW, otherwise the steps < 1 are masked out
-      const bool tail = s0 < 64 * NW;
-      int32_t u1[NW];
-#pragma unroll
-      for (int c = 0; c < NW; ++c) u1[c] = s0 + 1 - (64 * c + lane);
-      while (true) {  // R = 0 is the first guess; at most L + 1 passes (causality)
-        bool same = true;
-        uint64_t bm[NW];
-#pragma unroll
-        for (int c = 0; c < NW; ++c) {
-          const int32_t u = u1[c] + R[c];
-          x[c] = w[c] >> (__clz((uint32_t)u) & 31);  // meaningful for u >= 2 only
-          // lane masks straight from the compares (no boolean round trip through a VGPR)
-          uint64_t m = Lm[c] & __builtin_amdgcn_uicmp(x[c], (uint32_t)u, 35 /* uge */);
-#ifdef LDDL_FY_TAILBR
-          if (tail) m &= __builtin_amdgcn_sicmp(u, 1, 38 /* sgt */);
+      const int L = min(64, kN - mti);
+      // lanes past the block end hold w = 0: x = 0 never reaches a bound >= 1
+      const uint32_t w = lane < L ? temper(mt[mti + lane]) : 0u;
+      const int32_t u1 = s0 + 1 - lane;
+      uint64_t rej = s0 < kFyGuessN ? kFyGuess.m[s0] : 0ull;
+      if (L < 64) rej &= (1ull << L) - 1;
+      int32_t R = (int32_t)popc_below(rej);
+      uint32_t x;
+      if (s0 >= 64) {
+#ifndef LDDL_FY_NOASM
+        // the pass as 4 VALU + one scalar compare-and-branch (the compiler's form adds a
+        // select, an exec AND and a second branch per pass)
+        int32_t u;
+        asm volatile(
+            "s_branch 2f\n"
+            "1:\n\t"
+            "s_mov_b64 %[rej], vcc\n\t"
+            "v_mbcnt_lo_u32_b32 %[R], vcc_lo, 0\n\t"
+            "v_mbcnt_hi_u32_b32 %[R], vcc_hi, %[R]\n"
+            "2:\n\t"
+            "v_add_u32 %[u], %[u1], %[R]\n\t"
+            "v_ffbh_u32 %[x], %[u]\n\t"
+            "v_lshrrev_b32 %[x], %[x], %[w]\n\t"
+            "v_cmp_ge_u32 vcc, %[x], %[u]\n\t"
+            "s_cmp_eq_u64 vcc, %[rej]\n\t"
+            "s_cbranch_scc0 1b\n"
+            : [rej] "+s"(rej), [R] "+v"(R), [x] "=&v"(x), [u] "=&v"(u)
+            : [u1] "v"(u1), [w] "v"(w)
+            : "vcc", "scc");
 #else
-          (void)tail;
-          m &= __builtin_amdgcn_sicmp(u, 1, 38 /* sgt */);
-#endif
-          bm[c] = m;
-          same &= bm[c] == rej[c];
-        }
+        while (true) {
+          const int32_t u = u1 + R;  // >= 2
+          x = w >> __clz((uint32_t)u);
+          const uint64_t bm = __builtin_amdgcn_uicmp(x, (uint32_t)u, 35 /* uge */);
 #ifdef LDDL_STAMPS
-        ++n_pass;
+          ++n_pass;
 #endif
-        if (same) break;
-        int32_t below = 0;
-#pragma unroll
-        for (int c = 0; c < NW; ++c) {
-          rej[c] = bm[c];
-          R[c] = below + (int32_t)popc_below(rej[c]);
-          below += __popcll(rej[c]);
+          if (bm == rej) break;
+          rej = bm;
+          R = (int32_t)popc_below(rej);
+        }
+#endif
+      } else {
+        while (true) {
+          const int32_t u = u1 + R;
+          // u <= 1 (past the last step): shift 31 keeps x <= 1 < the 0xFFFFFFFF threshold
+          const uint32_t sh = u > 1 ? (uint32_t)__clz((uint32_t)u) : 31u;
+          x = w >> sh;
+          const uint32_t thr = u > 1 ? (uint32_t)u : 0xFFFFFFFFu;
+          const uint64_t bm = __builtin_amdgcn_uicmp(x, thr, 35 /* uge */);
+#ifdef LDDL_STAMPS
+          ++n_pass;
+#endif
+          if (bm == rej) break;
+          rej = bm;
+          R = (int32_t)popc_below(rej);
         }
       }
 #ifdef LDDL_STAMPS
       ++n_win;
 #endif
-#pragma unroll
-      for (int c = 0; c < NW; ++c) i[c] = u1[c] + R[c] - 1;
+      const int32_t i = u1 + R - 1;
       // words consumed: up to the first word past the last step (i < 1) or the window end
       int E = L;
-#pragma unroll
-      for (int c = NW - 1; c >= 0; --c) {
-        const uint64_t fin = Lm[c] & __builtin_amdgcn_sicmp(i[c], 1, 40 /* slt */);
-        if (fin) E = 64 * c + __ffsll((unsigned long long)fin) - 1;
+      if (s0 < 64) {
+        const uint64_t fin = __builtin_amdgcn_sicmp(i, 1, 40 /* slt */) & (L >= 64 ? ~0ull : ((1ull << L) - 1));
+        if (fin) E = __ffsll((unsigned long long)fin) - 1;
       }
-      int nrej = 0;
-#pragma unroll
-      for (int c = 0; c < NW; ++c) {
-        const int t = 64 * c + lane;
-        if (t < E && !((rej[c] >> lane) & 1ull)) sink((int64_t)i[c], x[c]);
-        const int ec = E - 64 * c;
-        nrej += __popcll(rej[c] & (ec >= 64 ? ~0ull : ec <= 0 ? 0ull : ((1ull << ec) - 1)));
-      }
-      mti += E;
-      s0 -= E - nrej;
-      s0 = uni(s0);
-      mti = uni(mti);
+      if (lane < E && !((rej >> lane) & 1ull)) sink((int64_t)i, x);
+      const int nrej = __popcll(rej & (E >= 64 ? ~0ull : ((1ull << E) - 1)));
+      mti = uni(mti + E);
+      s0 = uni(s0 - (E - nrej));
     }
     __syncthreads();
     wbase = -1024;  // the register window is stale
@@ -476,6 +505,7 @@ struct PlanArgs {
   int32_t* overflow;   // set when the pool is too small (the host re-plans with a larger one)
   int64_t* part_npairs;
   uint64_t* stamps;  // diagnostic build: [n_part][8]
+  uint64_t* tl;      // diagnostic build: [n_part][2] s_memrealtime at start / end (100 MHz)
 };
 
 constexpr int kDocLds = 512;  // partitions with <= this many documents cache offsets in LDS
@@ -562,6 +592,9 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
   uint64_t st_acc[kStampRegions] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   [[maybe_unused]] uint64_t st_t = STAMP_T();
+#ifdef LDDL_STAMPS
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   WaveRng rng{s_mt, s_tw, 0, 0, 0u
 #ifdef LDDL_STAMPS
               , 0, 0
@@ -678,12 +711,12 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
           // random.shuffle(cand_indexes): draws j_i (i = nc-1 .. 1) to the pool
           if (A.jbytes == 1) {
             uint8_t* jd = static_cast<uint8_t*>(A.jpool) + jb;
-            rng.template fy_draws<LDDL_FY_NW>(nc, [&](int64_t i, uint32_t j) {
+            rng.fy_draws(nc, [&](int64_t i, uint32_t j) {
               if (fits) jd[i] = (uint8_t)j;
             });
           } else {
             uint16_t* jd = static_cast<uint16_t*>(A.jpool) + jb;
-            rng.template fy_draws<LDDL_FY_NW>(nc, [&](int64_t i, uint32_t j) {
+            rng.fy_draws(nc, [&](int64_t i, uint32_t j) {
               if (fits) jd[i] = (uint16_t)j;
             });
           }
@@ -712,13 +745,17 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
   STAMP_ADD(0, st_t);
   {
     int32_t* js = A.jseq + base;
-    rng.template fy_draws<LDDL_FY_NW>(np, [&](int64_t i, uint32_t j) { js[i] = (int32_t)j; });
+    rng.fy_draws(np, [&](int64_t i, uint32_t j) { js[i] = (int32_t)j; });
   }
   STAMP_ADD(6, st_t);
 #ifdef LDDL_STAMPS
   st_acc[7] = rng.n_pass * 1000000 / (rng.n_win ? rng.n_win : 1);  // passes per window x 1e6
   if (leader && A.stamps)
     for (int r = 0; r < kStampRegions; ++r) A.stamps[(int64_t)p * kStampRegions + r] = st_acc[r];
+  if (leader && A.tl) {
+    A.tl[2 * (int64_t)p] = rt0;
+    A.tl[2 * (int64_t)p + 1] = __builtin_amdgcn_s_memrealtime();
+  }
 #endif
   if (leader) A.part_npairs[p] = np;
 }
@@ -1796,6 +1833,10 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   TRY(P->alloc(&d_stamps, n_part * kStampRegions, st));
   LDDL_HIP(hipMemsetAsync(d_stamps, 0, 8 * n_part * kStampRegions, st));
   A.stamps = d_stamps;
+  uint64_t* d_tl;
+  TRY(P->alloc(&d_tl, n_part * 2, st));
+  LDDL_HIP(hipMemsetAsync(d_tl, 0, 16 * n_part, st));
+  A.tl = d_tl;
 #endif
   if (prm->seq > 512) TRY((set_error("replay planner supports target_seq_length <= 512"), -1));
   const size_t lds = 4 * kN + 4 * (kDocLds + 4) + 16;  // ~4.5 KB: 8 waves/SIMD fit the CU's LDS
@@ -1896,6 +1937,39 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     for (int r = 0; r < kStampRegions - 1; ++r)
       fprintf(stderr, " %s=%.3g (%.1f%%)", names[r], tot[r] / n_part, 100.0 * tot[r] / (all + 1e-9));
     fprintf(stderr, " %s=%.3f\n", names[kStampRegions - 1], tot[kStampRegions - 1] / n_part / 1e6);
+    // timeline (100 MHz real-time clock): partition durations and concurrency over the launch
+    std::vector<uint64_t> t(2 * n_part);
+    LDDL_HIP(hipMemcpyAsync(t.data(), d_tl, 16 * n_part, hipMemcpyDeviceToHost, st));
+    LDDL_HIP(hipStreamSynchronize(st));
+    uint64_t t0 = ~0ull, t1 = 0;
+    std::vector<double> dur(n_part);
+    for (int64_t q = 0; q < n_part; ++q) {
+      t0 = std::min(t0, t[2 * q]);
+      t1 = std::max(t1, t[2 * q + 1]);
+      dur[q] = (t[2 * q + 1] - t[2 * q]) / 1e5;  // ms
+    }
+    std::vector<double> sd = dur;
+    std::sort(sd.begin(), sd.end());
+    const double span = (t1 - t0) / 1e5;
+    fprintf(stderr, "[timeline] span %.2f ms, partition ms min %.2f p10 %.2f p50 %.2f p90 %.2f max %.2f\n",
+            span, sd[0], sd[n_part / 10], sd[n_part / 2], sd[n_part * 9 / 10], sd[n_part - 1]);
+    const int nb = 40;
+    fprintf(stderr, "[timeline] active partitions per %.2f ms bin:", span / nb);
+    for (int b = 0; b < nb; ++b) {
+      const uint64_t a = t0 + (t1 - t0) * b / nb, e = t0 + (t1 - t0) * (b + 1) / nb;
+      double act = 0;  // partition-time inside the bin / bin length
+      for (int64_t q = 0; q < n_part; ++q) {
+        const uint64_t s0 = std::max(a, t[2 * q]), s1 = std::min(e, t[2 * q + 1]);
+        if (s1 > s0) act += (double)(s1 - s0);
+      }
+      fprintf(stderr, " %.0f", act / (double)(e - a));
+    }
+    fprintf(stderr, "\n[timeline] start ms of partitions by index decile:");
+    for (int k = 0; k <= 10; ++k) {
+      const int64_t q = std::min<int64_t>(n_part - 1, n_part * k / 10);
+      fprintf(stderr, " %.1f", (t[2 * q] - t0) / 1e5);
+    }
+    fprintf(stderr, "\n");
   }
 #endif
   // layout

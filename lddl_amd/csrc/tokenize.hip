@@ -10,20 +10,21 @@
 // bytes; sentence s writes its pieces to ids[sent_off[s] ...] and its kept count (<= max_pieces)
 // to sent_len[s] (bit 30 set if the kept pieces contain a literal [CLS]/[SEP]).
 //
-// Two kernels:
-//   tokenize_wave_kernel   one wavefront per sentence (grid-stride). The sentence is consumed in
-//                          64-byte windows, one byte per lane (coalesced loads). Lanes classify
-//                          their code point (ASCII via an LDS copy of the table page, UTF-8 leads
-//                          decoded in place), ballots find the pre-tokenizer units (word runs,
-//                          isolated chars, literal special tokens), then lane k runs greedy
-//                          longest-match WordPiece on unit k: ASCII words of <= 16 bytes with the
-//                          word held in two 64-bit registers (SWAR lowercase, hash keys by shift
-//                          and mask), everything else from a per-lane LDS buffer. A wave prefix
-//                          scan of the per-unit piece counts places the pieces. A unit that does
-//                          not fit a window, a word of > kPcs pieces or a normalised word of
-//                          > kNorm bytes sends the whole sentence to the fallback list.
+// Kernels:
+//   tokenize_batch_kernel  the product path. Persistent workgroups of kBW waves (one per CU,
+//                          sharing an LDS Bloom filter of the vocab); each wave streams its
+//                          sentences (grid-stride) in 64-byte windows, one byte per lane. Lanes
+//                          classify code points, ballots find the pre-tokenizer units, which go
+//                          to an LDS queue spanning sentences; every kSF queued units are
+//                          resolved in two phases (A: one vocab probe per unit, B: greedy
+//                          longest-match WordPiece of the multi-piece / non-ASCII units only)
+//                          and placed in queue order by a segmented scan (details above the
+//                          kernel). A unit that does not fit (> kNorm normalised bytes, > kPcs
+//                          pieces) sends its sentence to the fallback list.
 //   tokenize_lane_kernel   one lane per listed sentence, sequential (unbounded words, 100-char
 //                          rule); also the whole-corpus path when LDDL_TOKENIZE_PATH=lane.
+//   tokenize_wave_kernel   round-1 design, one wavefront per sentence with no cross-sentence
+//                          queue; kept only as the LDDL_TOKENIZE_PATH=wave diagnostic.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
