@@ -13,7 +13,7 @@
 // Kernels:
 //   tokenize_batch_kernel  the product path. Persistent workgroups of kBW waves (one per CU,
 //                          sharing an LDS Bloom filter of the vocab); each wave streams its
-//                          sentences (grid-stride) in 64-byte windows, one byte per lane. Lanes
+//                          sentences (dynamic chunks) in 64-byte windows, one byte per lane. Lanes
 //                          classify code points, ballots find the pre-tokenizer units, which go
 //                          to an LDS queue spanning sentences; every kSF queued units are
 //                          resolved in two phases (A: one vocab probe per unit, B: greedy
@@ -29,6 +29,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <vector>
+#include <cstdio>
 
 #include "common.h"
 #include "ctx.h"
@@ -707,6 +709,10 @@ constexpr int kSF = LDDL_TOK_SF;   // units resolved per pass (kSF / 64 phase-A 
 constexpr int kQ = kSF + 64;       // queue capacity (a window adds <= 64 units)
 constexpr int kRing = 64;          // sentences in flight per wave
 constexpr int kBW = LDDL_TOK_BW;   // waves per workgroup (one workgroup per CU shares the Bloom filter)
+#ifndef LDDL_TOK_CHUNK
+#define LDDL_TOK_CHUNK 128
+#endif
+constexpr int kChunk = LDDL_TOK_CHUNK;  // consecutive sentences claimed at a time
 using HIdx = std::conditional_t<(kSF > 256), uint16_t, uint8_t>;
 constexpr int32_t kHardBit = INT32_MIN;  // q_res: pieces are in column (res & 63) of pcs
 
@@ -730,13 +736,19 @@ enum : int32_t { kClosed = 1, kFallback = 2 };
 #ifndef LDDL_TOK_MIN_WAVES
 #define LDDL_TOK_MIN_WAVES 1
 #endif
+#ifdef LDDL_STAMPS
+__device__ unsigned long long* g_tok_tl;  // diagnostic build: [wave][2] s_memrealtime start / end
+#endif
 __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_kernel(
     Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
     int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
-    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n) {
+    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr) {
   __shared__ uint32_t s_ascii[128];
   __shared__ uint32_t s_bloom[kBloomWords];
   __shared__ BatchLds s_w[kBW];
+#ifdef LDDL_STAMPS
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   for (int c = threadIdx.x; c < 128; c += blockDim.x) s_ascii[c] = tab_entry(T, (uint32_t)c);
   for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
   __syncthreads();
@@ -744,9 +756,34 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
   BatchLds& W = s_w[threadIdx.x >> 6];
   // sentence indices fit int32 (lddl_tokenize: n_sent < INT32_MAX); 32-bit state keeps the
   // loop's scalar registers from spilling
-  const int32_t s_first = (int32_t)blockIdx.x * kBW + (int32_t)(threadIdx.x >> 6);
-  const int32_t stride = (int32_t)gridDim.x * kBW;
   const int32_t n_sent32 = (int32_t)n_sent;
+  // Sentences come in chunks of kChunk consecutive sentences: wave w starts with chunk w, then
+  // takes the next unclaimed chunk from chunk_ctr (initialised to the number of waves x kChunk).
+  // A static share per wave would leave a long tail: waves of one SIMD are issued oldest first,
+  // so the first finishes ~25 % before the last, which then runs alone and latency-bound.
+  // q0 = the next sentence to open, q1 = the one after it (whose chunk ends at ce); >= n_sent:
+  // none left.
+  int32_t ce = 0;
+  auto grab = [&]() -> int32_t {
+    int32_t c = 0;
+    if (lane == 0) c = atomicAdd(chunk_ctr, kChunk);
+    c = __builtin_amdgcn_readfirstlane(c);
+    ce = c < n_sent32 - kChunk ? c + kChunk : n_sent32;
+    return c < n_sent32 ? c : n_sent32;
+  };
+  auto succ = [&](int32_t x) -> int32_t {
+    if (x >= n_sent32) return n_sent32;
+    if (x + 1 < ce) return x + 1;
+    return grab();
+  };
+  int32_t q0, q1;
+  {
+    const int32_t w = (int32_t)blockIdx.x * kBW + (int32_t)(threadIdx.x >> 6);
+    const int64_t c0 = (int64_t)w * kChunk;
+    q0 = c0 < n_sent32 ? (int32_t)c0 : n_sent32;
+    ce = c0 + kChunk < n_sent32 ? (int32_t)(c0 + kChunk) : n_sent32;
+    q1 = succ(q0);
+  }
   int32_t head = 0, tail = 0;  // ordinals of in-flight sentences: [head, tail)
   int qn = 0;
   bool cur = false;
@@ -757,6 +794,10 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
   uint32_t pbyte = 0x20u;
   int64_t ppos = -1;
   int pk = 64;  // the prefetched window's second-segment lane
+  // ... and the segment ends it was loaded against: consecutive sentences of a chunk are
+  // adjacent, so an empty sentence starts where the next one does and a start alone does not
+  // identify the window
+  int64_t pb1 = -1, pbB = -1;
   int64_t nb0 = -1, nb1 = -1;
 
   // place queue units [u0, u1) (all resolved) in order: segmented scan per sentence
@@ -968,7 +1009,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
 
   while (true) {
     if (!cur) {
-      const int32_t s = s_first + tail * stride;  // < n_sent + stride < 2^31
+      const int32_t s = q0;
       if (s >= n_sent32) break;
       if (tail - head == kRing) {  // ring full: make room
         flush();
@@ -984,9 +1025,11 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
         b1 = sent_off[s + 1];
       }
       nb0 = nb1 = -1;
-      if (s < n_sent32 - stride) {
-        nb0 = sent_off[s + stride];
-        nb1 = sent_off[s + stride + 1];
+      q0 = q1;
+      q1 = succ(q1);
+      if (q0 < n_sent32) {
+        nb0 = sent_off[q0];
+        nb1 = sent_off[q0 + 1];
       }
       if (lane == 0) {
         W.r_b0[cur_slot] = b0;
@@ -1011,7 +1054,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
 #else
       if (b1 - pos < 64 && nb0 >= 0 && tail - head < kRing) {
 #endif
-        const int32_t sn = s_first + tail * stride;  // the sentence nb0 / nb1 belong to
+        const int32_t sn = q0;  // the sentence nb0 / nb1 belong to
         k = (int)(b1 - pos);
         slotB = (int)(tail % kRing);
         b0B = nb0;
@@ -1025,15 +1068,18 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
         }
         ++tail;
         nb0 = nb1 = -1;
-        if (sn < n_sent32 - stride) {
-          nb0 = sent_off[sn + stride];
-          nb1 = sent_off[sn + stride + 1];
+        q0 = q1;
+        q1 = succ(q1);
+        if (q0 < n_sent32) {
+          nb0 = sent_off[q0];
+          nb1 = sent_off[q0 + 1];
         }
       }
       const bool segB = lane >= k;
       const int64_t il = segB ? b0B + (lane - k) : pos + lane;
       const int64_t b1l = segB ? b1B : b1;
-      const uint32_t byte = (ppos == pos && pk == k) ? pbyte : (il < b1l ? text[il] : 0x20u);
+      const bool pf = ppos == pos && pk == k && pb1 == b1 && (k == 64 || pbB == b1B);
+      const uint32_t byte = pf ? pbyte : (il < b1l ? text[il] : 0x20u);
       const bool tail_known = k < 64 ? b0B + (64 - k) >= b1B : pos + 64 >= b1;
       const WinResult R = classify_lanes(T, s_ascii, text, il, b1l, byte, k < 64 ? 1ull << k : 0ull,
                                          tail_known);
@@ -1060,9 +1106,13 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
         pbyte = ip < (lane >= kk ? nb1 : lb1) ? text[ip] : 0x20u;
         ppos = next;
         pk = kk;
+        pb1 = lb1;
+        pbB = kk < 64 ? nb1 : -1;
       } else if (nb0 >= 0) {  // the next sentence's first window
         ppos = nb0;
         pk = 64;
+        pb1 = nb1;
+        pbB = -1;
         pbyte = nb0 + lane < nb1 ? text[nb0 + lane] : 0x20u;
       }
 #endif
@@ -1121,6 +1171,13 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
     retire();
   }
   retire();
+#ifdef LDDL_STAMPS
+  if (lane == 0 && g_tok_tl) {
+    const int64_t wv = (int64_t)blockIdx.x * kBW + (threadIdx.x >> 6);
+    g_tok_tl[2 * wv] = rt0;
+    g_tok_tl[2 * wv + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 }  // namespace
@@ -1134,7 +1191,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
   if (!c) LDDL_FAIL(-1, "null ctx");
   if (n_sent < 0 || n_bytes < 0 || max_pieces <= 0 || max_pieces > (1 << 24))
     LDDL_FAIL(-1, "bad sizes (max_pieces must be in 1 .. 2^24)");
-  if (n_sent >= (int64_t)INT32_MAX) LDDL_FAIL(-1, "too many sentences in one call (%lld)", (long long)n_sent);
+  if (n_sent >= (int64_t)INT32_MAX - (1 << 22)) LDDL_FAIL(-1, "too many sentences in one call (%lld)", (long long)n_sent);
   if (n_sent == 0) return 0;
   hipStream_t st = as_stream(stream);
   const char* path = getenv("LDDL_TOKENIZE_PATH");  // diagnostics: "lane" = fallback kernel only
@@ -1152,8 +1209,10 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
   constexpr int kFbHead = 1;
 #endif
   DevArena::Block fbb;
-  LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)(n_sent + kFbHead), st, fbb));
+  // + the batch kernel's chunk counter after the list
+  LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)(n_sent + kFbHead + 1), st, fbb));
   int32_t* fb = static_cast<int32_t*>(fbb.p);
+  int32_t* chunk_ctr = fb + kFbHead + n_sent;
   LDDL_HIP(hipMemsetAsync(fb, 0, sizeof(int32_t) * kFbHead, st));
   int n_cu = 256;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -1172,9 +1231,47 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     // each wave streams >= ~16 sentences so its unit queue stays full across sentences
     const int64_t want = (n_sent + 16 * kBW - 1) / (16 * kBW);
     const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1)));
+#ifdef LDDL_STAMPS
+    unsigned long long* tl = nullptr;
+    LDDL_HIP(hipMalloc(&tl, 16 * grid * kBW));
+    LDDL_HIP(hipMemsetAsync(tl, 0, 16 * grid * kBW, st));
+    LDDL_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tok_tl), &tl, sizeof(tl), 0, hipMemcpyHostToDevice, st));
+#endif
+    // the first grid x kBW chunks are taken statically (chunk w by wave w)
+    const int64_t first = std::min<int64_t>(grid * kBW * kChunk, (int64_t)INT32_MAX);
+    LDDL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(chunk_ctr), (int)first, 1, st));
     hipLaunchKernelGGL(tokenize_batch_kernel, dim3((unsigned)grid), dim3(64 * kBW), 0, st, c->tab,
                        d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + kFbHead,
-                       reinterpret_cast<uint32_t*>(fb));
+                       reinterpret_cast<uint32_t*>(fb), chunk_ctr);
+#ifdef LDDL_STAMPS
+    {  // wave timeline (100 MHz real-time clock)
+      const int64_t nw = grid * kBW;
+      std::vector<unsigned long long> t(2 * nw);
+      LDDL_HIP(hipMemcpyAsync(t.data(), tl, 16 * nw, hipMemcpyDeviceToHost, st));
+      LDDL_HIP(hipStreamSynchronize(st));
+      unsigned long long t0 = ~0ull, t1 = 0;
+      std::vector<double> e(nw);
+      for (int64_t q = 0; q < nw; ++q) {
+        t0 = std::min(t0, t[2 * q]);
+        t1 = std::max(t1, t[2 * q + 1]);
+      }
+      for (int64_t q = 0; q < nw; ++q) e[q] = (t[2 * q + 1] - t0) / 1e5;
+      std::sort(e.begin(), e.end());
+      const double span = (t1 - t0) / 1e5;
+      fprintf(stderr, "[tok timeline] span %.2f ms, wave end ms: min %.2f p10 %.2f p50 %.2f p90 %.2f max %.2f\n",
+              span, e[0], e[nw / 10], e[nw / 2], e[nw * 9 / 10], e[nw - 1]);
+      const int nb = 40;
+      fprintf(stderr, "[tok timeline] waves alive per %.2f ms bin:", span / nb);
+      for (int b = 0; b < nb; ++b) {
+        const double te = span * (b + 0.5) / nb;
+        int64_t alive = 0;
+        for (int64_t q = 0; q < nw; ++q) alive += e[q] > te;
+        fprintf(stderr, " %lld", (long long)alive);
+      }
+      fprintf(stderr, "\n");
+      LDDL_HIP(hipFree(tl));
+    }
+#endif
   }
   const int64_t fgrid = std::min<int64_t>((n_sent + kBlock - 1) / kBlock, (int64_t)n_cu * 2);
   hipLaunchKernelGGL(tokenize_lane_kernel, dim3((unsigned)fgrid), dim3(kBlock), 0, st, c->tab,

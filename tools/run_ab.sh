@@ -9,7 +9,7 @@ mkdir -p $O
 for v in "$@"; do
   if [ "$v" = base ]; then L=lddl_amd/_lib/liblddl_amd.so; else L=lddl_amd/_lib_$v/liblddl_amd.so; fi
   if [ "$v" != base ]; then
-    LDDL_AMD_LIB=$L timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_pairs_gpu.py tests/test_output_gpu.py > $O/tests_$v.log 2>&1 || exit 1
+    LDDL_AMD_LIB=$L timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu ${AB_TESTS:-tests/test_pairs_gpu.py tests/test_output_gpu.py} > $O/tests_$v.log 2>&1 || exit 1
   fi
 done
 for r in 1 2; do
