@@ -4,9 +4,12 @@ and the VALU-issue roofline when the batch size matches.
 
     python tools/make_pmc_json.py gpurun_out/<dir> <batch_bytes> <label> > profiles/pmc.json
 
-HBM bytes: FETCH_SIZE and WRITE_SIZE (KB) in their own passes (MI355X_MICROARCH.md: FETCH_SIZE
-under-reports wide coalesced streaming reads by 2x on gfx950; these kernels' loads are byte- and
-gather-granular, not that shape, so no correction is applied - stated in the json).
+HBM bytes: FETCH_SIZE and WRITE_SIZE (KB) in their own passes. MI355X_MICROARCH.md: on gfx950
+FETCH_SIZE tallies 128-B memory requests at 64 B, i.e. reports half the bytes of coalesced
+streaming reads; the tokenizer's sequential text reads confirm an under-count here (FETCH_SIZE
+8.1 GB for >= 10.65 GB of text and offsets read once). The read side is therefore doubled
+(hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE), which can only overstate the traffic of
+kernels whose requests are smaller than a line.
 """
 import glob
 import json
@@ -33,12 +36,12 @@ def main(src, batch_bytes, label):
             kernels.setdefault(short(k), {}).update(cs)
     for k, cs in kernels.items():
         if 'FETCH_SIZE' in cs or 'WRITE_SIZE' in cs:
-            cs['hbm_bytes_per_launch'] = (cs.get('FETCH_SIZE', 0.0) + cs.get('WRITE_SIZE', 0.0)) * 1024.0
+            cs['hbm_bytes_per_launch'] = (2.0 * cs.get('FETCH_SIZE', 0.0) + cs.get('WRITE_SIZE', 0.0)) * 1024.0
     out = {'batch_bytes': batch_bytes,
            'source': ('rocprofv3 --pmc passes (one counter group per run) over bench.py --steps 1 '
                       '--warmup 0 ({}); mean per dispatch; FETCH_SIZE/WRITE_SIZE KB -> '
-                      'hbm_bytes_per_launch, no gfx950 x2 streaming-read correction (byte / '
-                      'gather-granular loads)').format(label),
+                      'hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE counts '
+                      '128-B read requests at 64 B; MI355X_MICROARCH.md HBM section)').format(label),
            'kernels': kernels}
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
     print()
