@@ -57,16 +57,36 @@ def _npy_u16(b):
     return np.load(io.BytesIO(b)).astype(np.uint16)
 
 
-_ODD_ASCII_WS = re.compile('[\x1c-\x1f]')
+# whitespace of Python's str.split() (str.isspace()) that the kernel's ASCII splitter (space and
+# \t-\r, the bytes.split() set) does not treat as a separator
+_ODD_WS = re.compile('[\x1c-\x1f\x85\xa0\u1680\u2000-\u200a\u2028\u2029\u202f\u205f\u3000]')
+
+
+# UTF-8 byte sequences that every string holding such whitespace contains (\xe2\x80 also
+# starts common punctuation: those strings get the exact regex check)
+_ODD_WS_SEQ = (b'\x1c', b'\x1d', b'\x1e', b'\x1f', b'\xc2\x85', b'\xc2\xa0', b'\xe1\x9a\x80',
+               b'\xe2\x80', b'\xe2\x81\x9f', b'\xe3\x80\x80')
 
 
 def _canon(s):
-    """The string as the GPU splitter sees it: the reference splits with Python's str.split()
-    (Unicode whitespace, bert.py:80-81); the kernel splits on ASCII space / \\t-\\r. Strings
-    holding any other whitespace are re-joined with single spaces first (same tokens)."""
-    if s.isascii() and not _ODD_ASCII_WS.search(s):
-        return s
-    return ' '.join(s.split())
+    """The string as the GPU splitter sees it, UTF-8 encoded: the reference splits with Python's
+    str.split() (Unicode whitespace, bert.py:80-81); the kernel splits on ASCII space / \\t-\\r.
+    Strings holding any other whitespace are re-joined with single spaces first (same tokens)."""
+    b = s.encode('utf-8')
+    if any(q in b for q in _ODD_WS_SEQ) and _ODD_WS.search(s):
+        return ' '.join(s.split()).encode('utf-8')
+    return b
+
+
+def _ntok(b):
+    """len(b.split()) (ASCII whitespace) without building the token list: a string of tokens
+    joined by single spaces (what the preprocessor writes) has count(' ') + 1."""
+    if not b:
+        return 0
+    if (b[0] == 32 or b[-1] == 32 or b'  ' in b or b'\t' in b or b'\n' in b or b'\r' in b or
+            b'\x0b' in b or b'\x0c' in b):
+        return len(b.split())
+    return b.count(b' ') + 1
 
 
 def _pack(batch, static):
@@ -75,10 +95,10 @@ def _pack(batch, static):
     str.split(), bert.py:80-81) and offsets and, with static masking, the labels strings and
     decoded positions. Runs in the DataLoader workers, so the main process never has to wait for
     the batch's shape."""
-    As = [_canon(s[0]).encode('utf-8') for s in batch]
-    Bs = [_canon(s[1]).encode('utf-8') for s in batch]
-    na = np.fromiter(map(len, map(bytes.split, As)), np.int32, len(batch))
-    nb = np.fromiter(map(len, map(bytes.split, Bs)), np.int32, len(batch))
+    As = [_canon(s[0]) for s in batch]
+    Bs = [_canon(s[1]) for s in batch]
+    na = np.fromiter(map(_ntok, As), np.int32, len(batch))
+    nb = np.fromiter(map(_ntok, Bs), np.int32, len(batch))
     la = np.fromiter(map(len, As), np.int64, len(batch))
     lb = np.fromiter(map(len, Bs), np.int64, len(batch))
     a_off = np.zeros(len(batch) + 1, np.int64)
@@ -87,7 +107,7 @@ def _pack(batch, static):
     parts = As + Bs
     extra = None
     if static:
-        labs = [_canon(s[4]).encode('utf-8') for s in batch]
+        labs = [_canon(s[4]) for s in batch]
         lab_off = np.zeros(len(batch) + 1, np.int64)
         lab_off[1:] = np.cumsum([len(x) for x in labs])
         lab_off += b_off[-1]

@@ -145,3 +145,26 @@ def test_load_balance_flags():
     a = LB.attach_args().parse_args(['--indir', 'x', '--num-shards', '4', '--bin-ids', '0', '2'])
     assert (a.indir, a.outdir, a.num_shards, a.bin_ids, a.keep_orig) == ('x', None, 4, [0, 2],
                                                                           False)
+
+
+def test_pack_token_counts_match_str_split():
+    """The loader's host pack (lddl_amd/torch/bert.py _canon/_ntok) gives the GPU splitter bytes
+    whose ASCII-whitespace tokens are the reference's str.split() tokens (bert.py:80-81)."""
+    import random
+    from lddl_amd.torch.bert import _canon, _ntok
+    ws = [' ', '  ', '\t', '\n', '\x0b', '\x0c', '\r', '\x1c', '\x1f', '\x85', '\xa0', ' ',
+          ' ', ' ', ' ', ' ', ' ', ' ', '　']
+    words = ['the', '##ing', 'café', '–', '’s', '中文', '…', 'x​y', 'a⁠b', '[MASK]']
+    rng = random.Random(5)
+    cases = ['', ' ', 'a', ' a', 'a ', 'a  b', 'a　b', '\xa0', 'a–b c']
+    for _ in range(2000):
+        n = rng.randint(0, 8)
+        s = ''.join(rng.choice(words) + (rng.choice(ws) if rng.random() < 0.3 else ' ')
+                    for _ in range(n))
+        if rng.random() < 0.2:
+            s = rng.choice(ws) + s
+        cases.append(s)
+    for s in cases:
+        b = _canon(s)
+        assert b.split() == [t.encode('utf-8') for t in s.split()], repr(s)
+        assert _ntok(b) == len(s.split()), repr(s)
