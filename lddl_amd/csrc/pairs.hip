@@ -483,7 +483,11 @@ struct PlanArgs {
   const int32_t* ks_len;
   const int64_t* kd_off;
   const int64_t* kp_off;
-  const int32_t* dense;  // kept tokens, packed (densify_kernel)
+  const int64_t* ks_start;  // kept sentence k's pieces at ids[ks_start[k] ...]: the tokenizer's
+  const int32_t* ids;       // layout (`dense` is filled by this launch's tail workgroups)
+  int32_t* dense;           // out: kept tokens, packed (densify_group)
+  int64_t n_kept_sent;
+  int32_t n_part, n_dense_wg;  // workgroups >= n_part fill `dense`
   const int64_t* part_seed;
   // params
   int32_t seq, dup, masking, vocab_size, cls_id, sep_id, mask_id, max_pred;
@@ -572,9 +576,45 @@ struct LenWin {
   }
 };
 
-// token j (0-based) of the span that starts at kept sentence k0 (slow path only)
+// token j (0-based) of the span that starts at kept sentence k0 (slow path only: a literal
+// [CLS]/[SEP] in the pair), read from the tokenizer's layout
 __device__ int32_t span_token(const PlanArgs& A, int64_t k0, int64_t j) {
-  return A.dense[A.kscan[k0] + j];
+  const int64_t x = A.kscan[k0] + j;
+  int64_t k = k0;
+  while (A.kscan[k + 1] <= x) ++k;
+  return A.ids[A.ks_start[k] + (x - A.kscan[k])];
+}
+
+// Kept tokens packed densely (see densify_kernel below):
+// one wave: kept sentences [k0, k0 + 64)
+__device__ inline void densify_group(int64_t k0, const int64_t* __restrict__ ks_start,
+                                     const int32_t* __restrict__ ks_len,
+                                     const int64_t* __restrict__ kscan, int64_t n,
+                                     const int32_t* __restrict__ ids, int32_t* __restrict__ dense) {
+  const int lane = threadIdx.x & 63;
+  const int64_t k = k0 + lane;
+  const bool ok = k < n;
+  const int32_t len = ok ? ks_len[k] & kLenMask : 0;
+  const int64_t st = ok ? ks_start[k] : 0;
+  const int32_t incl = wave_incl_scan(len);
+  const int32_t total = __shfl(incl, 63, 64);
+  const int64_t base = kscan[k0];
+  // the sentence loop indices are wave-uniform: lane values via readlane, not LDS permutes
+  auto rl = [](int32_t v, int i) { return __builtin_amdgcn_readlane(v, i); };
+  int j = 0;
+  for (int32_t c0 = 0; c0 < total; c0 += 64) {
+    const int32_t x = c0 + lane, hi = min(c0 + 63, total - 1);
+    while (rl(incl, j) <= c0) ++j;  // first sentence overlapping the chunk
+    int64_t src = 0;
+    for (int jj = j;; ++jj) {
+      const int32_t e = rl(incl, jj);
+      const int32_t b = e - rl(len, jj);
+      const int64_t s = ((int64_t)rl((int32_t)(st >> 32), jj) << 32) | (uint32_t)rl((int32_t)st, jj);
+      if (x >= b && x < e) src = s + (x - b);
+      if (e > hi) break;
+    }
+    if (x < total) dense[base + x] = ids[src];
+  }
 }
 
 #ifndef LDDL_PLAN_MINW
@@ -588,6 +628,15 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
   const int p = blockIdx.x;
   const int lane = threadIdx.x;
   const bool leader = lane == 0;
+  if (p >= A.n_part) {
+    // Workgroups past the partitions pack `dense` (what densify_kernel would do after this
+    // launch). Dispatched in order, they start as the last partitions' waves are placed and
+    // run in the slots the planner's tail leaves idle (a separate launch before or beside the
+    // planner delays its dispatch).
+    for (int64_t g = p - A.n_part; g * 64 < A.n_kept_sent; g += A.n_dense_wg)
+      densify_group(g * 64, A.ks_start, A.ks_len, A.kscan, A.n_kept_sent, A.ids, A.dense);
+    return;
+  }
 #ifdef LDDL_STAMPS
   uint64_t st_acc[kStampRegions] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -1206,32 +1255,9 @@ __global__ void __launch_bounds__(256) densify_kernel(const int64_t* __restrict_
                                                       const int64_t* __restrict__ kscan, int64_t n,
                                                       const int32_t* __restrict__ ids,
                                                       int32_t* __restrict__ dense) {
-  const int lane = threadIdx.x & 63;
   const int64_t k0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
   if (k0 >= n) return;
-  const int64_t k = k0 + lane;
-  const bool ok = k < n;
-  const int32_t len = ok ? ks_len[k] & kLenMask : 0;
-  const int64_t st = ok ? ks_start[k] : 0;
-  const int32_t incl = wave_incl_scan(len);
-  const int32_t total = __shfl(incl, 63, 64);
-  const int64_t base = kscan[k0];
-  // the sentence loop indices are wave-uniform: lane values via readlane, not LDS permutes
-  auto rl = [](int32_t v, int i) { return __builtin_amdgcn_readlane(v, i); };
-  int j = 0;
-  for (int32_t c0 = 0; c0 < total; c0 += 64) {
-    const int32_t x = c0 + lane, hi = min(c0 + 63, total - 1);
-    while (rl(incl, j) <= c0) ++j;  // first sentence overlapping the chunk
-    int64_t src = 0;
-    for (int jj = j;; ++jj) {
-      const int32_t e = rl(incl, jj);
-      const int32_t b = e - rl(len, jj);
-      const int64_t s = ((int64_t)rl((int32_t)(st >> 32), jj) << 32) | (uint32_t)rl((int32_t)st, jj);
-      if (x >= b && x < e) src = s + (x - b);
-      if (e > hi) break;
-    }
-    if (x < total) dense[base + x] = ids[src];
-  }
+  densify_group(k0, ks_start, ks_len, kscan, n, ids, dense);
 }
 
 struct KeptLen {
@@ -1774,7 +1800,9 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   // 4 tokens of padding on both sides: the gather's 16-byte loads may overhang a window
   TRY(P->alloc(&P->dense, n_kept_tok + 8, st));
   P->dense += 4;
-  if (P->n_kept_sent)
+  // replay mode: the planner launch's tail workgroups pack `dense` (plan_replay_kernel)
+  const bool dense_in_plan = prm->rng == LDDL_RNG_REPLAY && n_part > 0 && !getenv("LDDL_DENSIFY_INLINE");
+  if (P->n_kept_sent && !dense_in_plan)
     hipLaunchKernelGGL(densify_kernel, dim3((unsigned)((P->n_kept_sent + 255) / 256)), dim3(256), 0,
                        st, P->ks_start, P->ks_len, P->kscan, P->n_kept_sent, d_ids, P->dense);
   LDDL_HIP(hipGetLastError());
@@ -1809,7 +1837,12 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   A.ks_len = P->ks_len;
   A.kd_off = P->kd_off;
   A.kp_off = P->kp_off;
+  A.ks_start = P->ks_start;
+  A.ids = d_ids;
   A.dense = P->dense;
+  A.n_kept_sent = dense_in_plan ? P->n_kept_sent : 0;
+  A.n_part = (int32_t)n_part;
+  A.n_dense_wg = getenv("LDDL_DENSE_WG") ? std::max(1, atoi(getenv("LDDL_DENSE_WG"))) : 4096;
   A.part_seed = d_part_seed;
   A.seq = prm->seq;
   A.dup = prm->dup;
@@ -1878,7 +1911,9 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     A.pool_used = pool_ctl;
     A.overflow = reinterpret_cast<int32_t*>(pool_ctl + 1);
     LDDL_HIP(hipEventRecord(P->ev[0], st));
-    hipLaunchKernelGGL(plan_replay_kernel, dim3((unsigned)n_part), dim3(64), lds, st, A);
+    hipLaunchKernelGGL(plan_replay_kernel,
+                       dim3((unsigned)n_part + (A.n_kept_sent ? (unsigned)A.n_dense_wg : 0u)), dim3(64),
+                       lds, st, A);
     LDDL_HIP(hipGetLastError());
     LDDL_HIP(hipEventRecord(P->ev[1], st));
     if (!prm->masking) break;
