@@ -665,8 +665,31 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
   int64_t jpool_cur = 0, jpool_end = 0;  // ... and of the shuffle-draw pool
   LenWin La, Lb;
   int64_t np = 0;
+#ifndef LDDL_PLAN_PRIO
+#define LDDL_PLAN_PRIO 4  // priority levels used (s_setprio has 4); 0 = age order only
+#endif
+#if LDDL_PLAN_PRIO > 0
+  // issue priority by progress: a SIMD issues its highest-priority (then oldest) wave first, so
+  // waves that are behind (e.g. a partition dispatched into a freed slot) catch up and the waves
+  // of a SIMD finish together instead of leaving the last ones running alone
+  int prio_q = -1;
+  const int64_t prio_tot = (int64_t)A.dup * nd;
+#endif
   for (int dp = 0; dp < A.dup; ++dp) {
     for (int64_t di = 0; di < nd; ++di) {
+#if LDDL_PLAN_PRIO > 0
+      {
+        const int q = (int)(((int64_t)LDDL_PLAN_PRIO * ((int64_t)dp * nd + di)) / prio_tot);
+        if (q != prio_q) {
+          prio_q = q;
+          const int lvl = LDDL_PLAN_PRIO - 1 - q;  // 3 .. 0 over the partition
+          if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+          else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+          else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+          else __builtin_amdgcn_s_setprio(0);
+        }
+      }
+#endif
       const int64_t s0 = doc_off(di);
       const int ns = (int)(doc_off(di + 1) - s0);
       La.reset(A.ks_len + s0, ns);
