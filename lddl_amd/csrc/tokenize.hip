@@ -1094,8 +1094,11 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
                (uint32_t)__builtin_amdgcn_readlane((int)il, nl);
         if (R.next_lane == 64) ++next;
       }
-#ifndef LDDL_TOK_NO_PREFETCH
-      // the next window's bytes, on the same lane mapping it will use (checked by pos and k)
+#ifdef LDDL_TOK_PREFETCH
+      // the next window's bytes, on the same lane mapping it will use (checked by pos and k).
+      // Off by default since the sentence chunks: consecutive windows of a wave read adjacent
+      // text that the previous window's loads already brought into L2 (2 GiB: 33.2 ms with
+      // the prefetch, 32.8 without; profiles/r02_tok_variants_chunks.txt)
       if (next < lb1) {
 #ifdef LDDL_TOK_NO_COMBINE
         const int kk = 64;
