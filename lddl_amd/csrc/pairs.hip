@@ -395,24 +395,24 @@ struct WaveRng {
       const int avail = kN - mti;
       int len = 0;
       int32_t tok = 0;
-      if (lane + 1 < avail) {
-        const uint32_t w0 = temper(mt[mti + lane]), w1 = temper(mt[mti + lane + 1]);
+      {
+        // mask / keep decided for every lane without branches (words past the block are read
+        // from the LDS after it and never used); only the random-token lanes loop
+        const uint32_t w0 = temper(mt[mti + lane]), w1 = temper(mt[mti + lane + 1]),
+                       w2 = temper(mt[mti + lane + 2]);
         const uint64_t N = ((uint64_t)(w0 >> 5) << 26) | (w1 >> 6);
-        if (N < lt08) {
-          len = 2;
-          tok = mask_id;
-        } else if (lane + 3 < avail) {
-          if (temper(mt[mti + lane + 2]) < 0x80000000u) {
-            len = 4;
-            tok = kKeep;
-          } else {
-            for (int j = lane + 4; j < avail; ++j) {
-              const uint32_t r = temper(mt[mti + j]) >> (32 - kV);
-              if (r < (uint32_t)V) {
-                len = j + 1 - lane;
-                tok = (int32_t)r;
-                break;
-              }
+        const bool is_mask = lane + 1 < avail && N < lt08;
+        const bool v3 = lane + 3 < avail;
+        const bool is_keep = !is_mask && v3 && w2 < 0x80000000u;
+        len = is_mask ? 2 : is_keep ? 4 : 0;
+        tok = is_mask ? mask_id : kKeep;
+        if (v3 && !is_mask && !is_keep) {
+          for (int j = lane + 4; j < avail; ++j) {
+            const uint32_t r = temper(mt[mti + j]) >> (32 - kV);
+            if (r < (uint32_t)V) {
+              len = j + 1 - lane;
+              tok = (int32_t)r;
+              break;
             }
           }
         }
