@@ -707,7 +707,10 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
 #endif
 constexpr int kSF = LDDL_TOK_SF;   // units resolved per pass (kSF / 64 phase-A rounds)
 constexpr int kQ = kSF + 64;       // queue capacity (a window adds <= 64 units)
-constexpr int kRing = 64;          // sentences in flight per wave
+#ifndef LDDL_TOK_RING
+#define LDDL_TOK_RING 64
+#endif
+constexpr int kRing = LDDL_TOK_RING;  // sentences in flight per wave
 constexpr int kBW = LDDL_TOK_BW;   // waves per workgroup (one workgroup per CU shares the Bloom filter)
 #ifndef LDDL_TOK_CHUNK
 #define LDDL_TOK_CHUNK 128
@@ -744,13 +747,19 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
     int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
     int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr) {
   __shared__ uint32_t s_ascii[128];
+#ifdef LDDL_TOK_BLOOM_GLOBAL  // A/B: Bloom filter read through the caches, LDS for more waves
+  const uint32_t* s_bloom = T.bloom;
+#else
   __shared__ uint32_t s_bloom[kBloomWords];
+#endif
   __shared__ BatchLds s_w[kBW];
 #ifdef LDDL_STAMPS
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
   for (int c = threadIdx.x; c < 128; c += blockDim.x) s_ascii[c] = tab_entry(T, (uint32_t)c);
+#ifndef LDDL_TOK_BLOOM_GLOBAL
   for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
+#endif
   __syncthreads();
   const int lane = lane_id();
   BatchLds& W = s_w[threadIdx.x >> 6];
@@ -1233,7 +1242,9 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_batch_kernel, 64 * kBW, 0));
     // each wave streams >= ~16 sentences so its unit queue stays full across sentences
     const int64_t want = (n_sent + 16 * kBW - 1) / (16 * kBW);
-    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1)));
+    int64_t grid = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1)));
+    // tests: a smaller grid makes small inputs take the dynamic chunk claims
+    if (const char* g = getenv("LDDL_TOKENIZE_GRID")) grid = std::max<int64_t>(1, std::min<int64_t>(grid, atoll(g)));
 #ifdef LDDL_STAMPS
     unsigned long long* tl = nullptr;
     LDDL_HIP(hipMalloc(&tl, 16 * grid * kBW));

@@ -132,3 +132,19 @@ def test_tokenize_long_and_empty_sentences(ctxs):
         e, eo = tok.tokenize(text, off, max_pieces=mp)
         np.testing.assert_array_equal(o, eo)
         np.testing.assert_array_equal(ids, e)
+
+
+@pytest.mark.parametrize('grid', ['1', '3'])
+def test_tokenize_dynamic_chunks_vs_oracle(ctxs, monkeypatch, grid):
+    """With a grid of 1 or 3 workgroups (LDDL_TOKENIZE_GRID) most sentences are claimed through
+    the batch kernel's atomic chunk counter, in chunks of consecutive (adjacent) sentences; the
+    output is the oracle's, with runs of empty sentences at chunk boundaries included."""
+    from oracle import oracle as O
+    monkeypatch.setenv('LDDL_TOKENIZE_GRID', grid)
+    text, off = _adversarial_corpus(seed=31, n=9000)
+    tok = O.Tokenizer(VOCAB_UNCASED, lowercase=True)
+    for mp in (512, 9):
+        ids, o = ctxs['uncased'].tokenize_host(text, off, max_pieces=mp)
+        e, eo = tok.tokenize(text, off, max_pieces=mp)
+        np.testing.assert_array_equal(o, eo)
+        np.testing.assert_array_equal(ids, e)
