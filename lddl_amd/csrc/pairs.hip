@@ -1965,7 +1965,12 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     // gfx950), minus headroom for the kernel's static LDS
     const size_t kLdsBudget = std::min<size_t>(150 * 1024, c->lds_per_block > 10 * 1024
                                                                ? c->lds_per_block - 10 * 1024 : 0);
-    if (cap <= 65536 && 2 * (size_t)(cap + kShufStage) <= kLdsBudget)
+    const bool force_global = getenv("LDDL_SHUFFLE_GLOBAL") != nullptr;  // tests: the large-partition path
+    if (force_global)
+      hipLaunchKernelGGL(apply_shuffle_kernel<int32_t>, dim3((unsigned)n_part), dim3(64),
+                         4 * (size_t)kShufStage, st, P->kd_off, P->kp_off, prm->dup, part_npairs,
+                         jseq, P->order, (int64_t)0);
+    else if (cap <= 65536 && 2 * (size_t)(cap + kShufStage) <= kLdsBudget)
       hipLaunchKernelGGL(apply_shuffle_kernel<uint16_t>, dim3((unsigned)n_part), dim3(64),
                          2 * (size_t)(cap + kShufStage), st, P->kd_off, P->kp_off, prm->dup,
                          part_npairs, jseq, P->order, cap);

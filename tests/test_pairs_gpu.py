@@ -78,3 +78,11 @@ def test_mask_pool_overflow_replans(ctx, docs_dev, monkeypatch):
     name = 's128_mask'
     monkeypatch.setenv('LDDL_AMD_MASK_POOL', '100')
     test_pairs_golden_gpu(name, ctx, docs_dev)
+
+
+def test_partition_shuffle_global_path(ctx, docs_dev, monkeypatch):
+    """The partition shuffle's path for partitions beyond the LDS budget (swaps in global
+    memory, inverse permutation by cycles) gives the reference's pair order."""
+    monkeypatch.setenv('LDDL_SHUFFLE_GLOBAL', '1')
+    for name in ('s128_mask', PAIR_CASES[0]):
+        test_pairs_golden_gpu(name, ctx, docs_dev)
