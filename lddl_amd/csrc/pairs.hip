@@ -736,8 +736,10 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
         rng.trunc_draws(na, nb, max_num, a_front, b_front);
         STAMP_ADD(5, st_t);
         const int64_t slot = base + np;
-        if (leader) A.desc[slot] = PairDesc{s0 + chunk0, b_ks, a_front, na, b_front,
-                                            nb | (int32_t)((uint32_t)rn << 31)};
+        // every lane stores the same record: the wave's identical writes merge into one, and no
+        // exec-mask branch (3 scalar instructions + a branch) is spent on a leader-only store
+        A.desc[slot] = PairDesc{s0 + chunk0, b_ks, a_front, na, b_front,
+                                nb | (int32_t)((uint32_t)rn << 31)};
         if (A.masking) {
           // candidates = positions of [CLS] A [SEP] B [SEP] whose token is not [CLS]/[SEP]; only
           // their count matters here (fy_resolve_kernel recovers the positions)
@@ -800,7 +802,7 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
             if (fits && lane < cmax) A.mtok[mb + c0 + lane] = mytok;
           }
           STAMP_ADD(4, st_t);
-          if (leader) {
+          {  // (all lanes, as the descriptor above)
             A.nmask[slot] = num;
             A.moff[slot] = mb;
             A.joff[slot] = jb;
