@@ -54,7 +54,7 @@ def build_product(verbose=False, jobs=8, diag=False, variant=None, defines=()):
     srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')) + glob.glob(os.path.join(CSRC, '*.cpp')))
     flags = ['-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function',
              '-I' + os.path.join(ROOT, 'include'), '-I' + CSRC] + (['-DLDDL_STAMPS'] if diag else []) + \
-        ['-D' + d for d in defines]
+        ['-D' + d for d in defines] + os.environ.get('LDDL_EXTRA_FLAGS', '').split()
     objs, jobs_list = [], []
     for s in srcs:
         o = os.path.join(objdir, os.path.basename(s) + '.o')
