@@ -286,6 +286,42 @@ __device__ inline int32_t probe32(const Tables& T, const B32& a, int len, uint32
   }
 }
 
+// probe32 split in two, so that several probes' first table loads are in flight together:
+// probe_first computes the key and issues the load of the home slot, probe_finish examines it
+// and walks the collision chain (rarely more than the home slot).
+struct Probe {
+  uint64_t k0;
+  uint32_t k1, want, slot;
+  VEnt e;
+};
+__device__ inline Probe probe_first(const Tables& T, const B32& a, int len, uint32_t cont) {
+  Probe q;
+  q.k0 = keep_bytes(a.w0, len);
+  q.k1 = (uint32_t)keep_bytes(a.w1, len - 8 < 4 ? len - 8 : 4);
+  q.want = kMetaValid | (cont ? kMetaCont : 0u) | (len > 12 ? kMetaLong : 0u) | ((uint32_t)len << 21);
+  q.slot = (uint32_t)vhash(q.k0, q.k1, len, cont) & T.vmask;
+  q.e = T.vhash[q.slot];
+  return q;
+}
+__device__ inline int32_t probe_finish(const Tables& T, const B32& a, int len, Probe q) {
+  for (;;) {
+    if (!(q.e.meta & kMetaValid)) return -1;
+    if (q.e.k0 == q.k0 && q.e.k1 == q.k1 && (q.e.meta & ~0x1FFFFFu) == q.want) {
+      const int32_t id = meta_id(q.e.meta);
+      if (len <= 12) return id;
+      const uint8_t* p = T.vbytes + T.voff[id];
+      bool ok = true;
+      for (int i = 12; i < len; ++i) {
+        const uint64_t wv = i < 16 ? a.w1 : i < 24 ? a.w2 : a.w3;
+        ok &= p[i] == (uint8_t)(wv >> (8 * (i & 7)));
+      }
+      if (ok) return id;
+    }
+    q.slot = (q.slot + 1) & T.vmask;
+    q.e = T.vhash[q.slot];
+  }
+}
+
 // Bloom candidates for the pieces starting at a's first byte: bit L-1 set iff the filter may
 // contain (cont, bytes[0, L)), L = 1 .. maxl (<= 32).
 __device__ inline uint32_t bloom_candidates32(const uint32_t* bloom, const B32& a, int maxl,
@@ -851,35 +887,59 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
     const int m = qn < kSF ? qn : kSF;
     // phase A: specials and single-piece words
     int nh = 0;
-    for (int r0 = 0; r0 < m; r0 += 64) {
-      const int u = r0 + lane;
-      bool hard = false;
-      if (u < m) {
-        const int kind = W.q_kind[u], len = W.q_len[u];
-        int32_t res = 0;
-        int npc = 1;
-        if (kind >= 2) {
-          res = T.special_id[kind - 2];
-        } else if (!W.q_slow[u] && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32) {
-          B32 v = load32(text, n_bytes, W.r_b0[W.q_slot[u]] + W.q_rel[u]);
-          if (T.ascii_mode == 1) v = B32{swar_lower(v.w0), swar_lower(v.w1), swar_lower(v.w2), swar_lower(v.w3)};
-          res = probe32(T, v, len, 0);
-          hard = res < 0;
-        } else {
-          hard = true;
-        }
+    {  // all rounds' text loads, then all first table loads, then the checks: one latency each
+      constexpr int kR = kSF / 64;
+      static_assert(kSF % 64 == 0, "phase A rounds");
+      bool elig[kR], hardr[kR];
+      int lenr[kR];
+      int32_t resr[kR];
+      B32 vv[kR];
+      Probe pr[kR];
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int u = 64 * r + lane;
+        elig[r] = hardr[r] = false;
+        lenr[r] = 0;
+        resr[r] = 0;
+        if (u < m) {
+          const int kind = W.q_kind[u], len = W.q_len[u];
+          lenr[r] = len;
+          if (kind >= 2) {
+            resr[r] = T.special_id[kind - 2];
+          } else if (!W.q_slow[u] && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32) {
+            elig[r] = true;
+            vv[r] = load32(text, n_bytes, W.r_b0[W.q_slot[u]] + W.q_rel[u]);
+          } else {
+            hardr[r] = true;
+          }
 #ifdef LDDL_TOK_NO_WP  // A/B experiment only: classification + placement without WordPiece
-        hard = false;
-        res = len;
+          elig[r] = hardr[r] = false;
+          resr[r] = len;
 #endif
-        if (!hard) {
-          W.q_res[u] = res;
-          W.q_npc[u] = (uint8_t)npc;
         }
       }
-      const uint64_t H = ballot(hard);
-      if (hard) W.h_idx[nh + (int)popc_below(H)] = (HIdx)u;
-      nh += __popcll(H);
+#pragma unroll
+      for (int r = 0; r < kR; ++r)
+        if (elig[r]) {
+          if (T.ascii_mode == 1)
+            vv[r] = B32{swar_lower(vv[r].w0), swar_lower(vv[r].w1), swar_lower(vv[r].w2), swar_lower(vv[r].w3)};
+          pr[r] = probe_first(T, vv[r], lenr[r], 0);
+        }
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        if (elig[r]) {
+          resr[r] = probe_finish(T, vv[r], lenr[r], pr[r]);
+          hardr[r] = resr[r] < 0;
+        }
+        const int u = 64 * r + lane;
+        if (u < m && !hardr[r]) {
+          W.q_res[u] = resr[r];
+          W.q_npc[u] = 1;
+        }
+        const uint64_t H = ballot(hardr[r]);
+        if (hardr[r]) W.h_idx[nh + (int)popc_below(H)] = (HIdx)u;
+        nh += __popcll(H);
+      }
     }
     wave_sync();
     // phase B in chunks of 64 hard units, each chunk placed with the units before the next one
