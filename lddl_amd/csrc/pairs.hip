@@ -160,6 +160,7 @@ struct WaveRng {
   uint32_t* tw;  // unused (a tempered copy of the block in LDS cut occupancy: 7 KB -> 5 waves/SIMD)
   int mti;       // next word of the block (uniform)
   int wbase;     // window base (uniform)
+  int wend;      // min(wbase + 64, kN) while the window is valid, 0 when stale (uniform)
   uint32_t win;  // this lane's tempered word temper(mt[wbase + lane])
 #ifdef LDDL_STAMPS
   uint64_t n_pass = 0, n_win = 0;  // diagnostics: Jacobi passes / Fisher-Yates windows
@@ -192,6 +193,7 @@ struct WaveRng {
     __syncthreads();
     mti = 0;
     wbase = 0;
+    wend = 64;
     win = temper(mt[l]);
   }
 
@@ -236,12 +238,13 @@ struct WaveRng {
       twist();
     } else {
       wbase = uni(mti);
+      wend = uni(min(mti + 64, kN));
       const int k = mti + (int)threadIdx.x;
       win = k < kN ? temper(mt[k]) : 0u;
     }
   }
   __device__ uint32_t u32() {
-    if (mti >= wbase + 64 || mti >= kN) refill();
+    if (mti >= wend) refill();  // one scalar compare per draw
     const uint32_t v = rdlane(win, mti - wbase);
     mti = uni(mti + 1);
     return v;
@@ -337,7 +340,8 @@ struct WaveRng {
       s0 = uni(s0 - (E - nrej));
     }
     __syncthreads();
-    wbase = -1024;  // the register window is stale
+    wbase = -1024;
+    wend = 0;  // the register window is stale
   }
   // _truncate_seq_pair draws (pretrain.py:161-176). T = na + nb - max_num trims; trim t hits A
   // iff A is the longer side at that point, which has a closed form: with d = na - nb the first
@@ -356,6 +360,7 @@ struct WaveRng {
       const int pairs = (kN - mti) >> 1;
       if (pairs == 0) {  // the trim's two words straddle the block end
         wbase = -1024;
+        wend = 0;
         const int32_t front = below_half() ? 1 : 0;
         const bool sa = done < d || (done >= ad && ((done - ad) & 1));
         if (sa) a_front += front;
@@ -373,6 +378,7 @@ struct WaveRng {
       done += cnt;
     }
     wbase = -1024;
+    wend = 0;
     const int32_t nA = (d > 0 ? min(d, T) : 0) + (T > ad ? (T - ad) / 2 : 0);
     na -= nA;
     nb -= T - nA;
@@ -443,6 +449,7 @@ struct WaveRng {
       mti = uni(mti + pos);
       c += take;
       wbase = -1024;
+      wend = 0;
       if (c < cnt && pos < 64) {  // the next decision's words straddle the block end
         int32_t t2;
         if (rand53() < lt08) t2 = mask_id;
@@ -451,6 +458,7 @@ struct WaveRng {
         if (lane == c) res = t2;
         ++c;
         wbase = -1024;
+        wend = 0;
       }
     }
     return res;
