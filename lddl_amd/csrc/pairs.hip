@@ -466,13 +466,25 @@ struct WaveRng {
 
   // random() = N / 2^53 with N = (w1 >> 5) * 2^26 + (w2 >> 6). `random() < p` is decided exactly
   // on N: N < ceil(p * 2^53) (see k_short / kLt08), so no floating point is needed.
+  // two consecutive words with one window check when both are in the window
+  __device__ void u32x2(uint32_t& a, uint32_t& b) {
+    if (mti + 1 < wend) {
+      a = rdlane(win, mti - wbase);
+      b = rdlane(win, mti + 1 - wbase);
+      mti = uni(mti + 2);
+    } else {
+      a = u32();
+      b = u32();
+    }
+  }
   __device__ uint64_t rand53() {
-    const uint32_t a = u32() >> 5, b = u32() >> 6;
-    return ((uint64_t)a << 26) | b;
+    uint32_t a, b;
+    u32x2(a, b);
+    return ((uint64_t)(a >> 5) << 26) | (b >> 6);
   }
   __device__ bool below_half() {  // random() < 0.5  <=>  N < 2^52  <=>  w1 < 2^31
-    const uint32_t a = u32();
-    (void)u32();
+    uint32_t a, b;
+    u32x2(a, b);
     return a < 0x80000000u;
   }
   __device__ uint32_t randbelow(uint32_t n) {
@@ -532,7 +544,7 @@ struct LenWin {
   int32_t win, pre;
   uint64_t fl;  // lanes whose sentence holds a literal [CLS]/[SEP]
   __device__ void reset(const int32_t* p, int nn) { len = p; n = nn; wbase = -1024; }
-  __device__ bool has(int j) const { return j >= wbase && j < wbase + 64; }
+  __device__ bool has(int j) const { return (unsigned)(j - wbase) < 64u; }  // (j >= 0)
   __device__ void load(int j) {
     wbase = j;
     const int k = j + (int)threadIdx.x;
