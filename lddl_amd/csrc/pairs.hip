@@ -494,6 +494,7 @@ struct WaveRng {
     return r;
   }
   __device__ int64_t randint(int64_t a, int64_t b) { return a + randbelow((uint32_t)(b - a + 1)); }
+  __device__ int32_t randint32(int32_t a, int32_t b) { return a + (int32_t)randbelow((uint32_t)(b - a + 1)); }
 
 };
 
@@ -530,6 +531,7 @@ struct PlanArgs {
   int64_t* part_npairs;
   uint64_t* stamps;  // diagnostic build: [n_part][8]
   uint64_t* tl;      // diagnostic build: [n_part][2] s_memrealtime at start / end (100 MHz)
+  const int16_t* num_tab;  // [n] = max(1, round((n) * ratio)) (half-even, binary64), n <= seq
 };
 
 constexpr int kDocLds = 512;  // partitions with <= this many documents cache offsets in LDS
@@ -670,15 +672,17 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
 #endif
   };
   rng.seed_i64(A.part_seed[p]);
-  const int64_t d0 = A.kp_off[p], nd = A.kp_off[p + 1] - d0;
+  const int64_t d0 = A.kp_off[p];
+  const int32_t nd = (int32_t)(A.kp_off[p + 1] - d0);  // (partition-local indices are 32-bit)
   const int64_t kbase = A.kd_off[d0];
   const bool doc_lds = nd + 1 <= kDocLds;
   if (doc_lds)
     for (int64_t d = lane; d <= nd; d += 64) s_doc[d] = (int32_t)(A.kd_off[d0 + d] - kbase);
   __syncthreads();
-  auto doc_off = [&](int64_t d) -> int64_t {  // kept-sentence index of document d (partition-local)
-    return doc_lds ? kbase + uni(s_doc[d]) : A.kd_off[d0 + d];
+  auto doc_loc = [&](int32_t d) -> int32_t {  // first kept sentence of document d, partition-local
+    return doc_lds ? uni(s_doc[d]) : (int32_t)(A.kd_off[d0 + d] - kbase);
   };
+  const int32_t* ks_len_p = A.ks_len + kbase;
   const int64_t base = (int64_t)A.dup * kbase;
   const int32_t max_num = A.seq - 3;
   int64_t pool_cur = 0, pool_end = 0;    // this wave's current chunk of the mask pool
@@ -694,34 +698,37 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
   // of a SIMD finish together instead of leaving the last ones running alone
   int prio_q = -1;
   const int64_t prio_tot = (int64_t)A.dup * nd;
+  // the priority steps at the document counts where progress crosses a quarter (no 64-bit
+  // division per document)
+  int32_t prio_next = 0, prio_done = 0;
 #endif
   for (int dp = 0; dp < A.dup; ++dp) {
-    for (int64_t di = 0; di < nd; ++di) {
+    for (int32_t di = 0; di < nd; ++di) {
 #if LDDL_PLAN_PRIO > 0
-      {
-        const int q = (int)(((int64_t)LDDL_PLAN_PRIO * ((int64_t)dp * nd + di)) / prio_tot);
-        if (q != prio_q) {
-          prio_q = q;
-          const int lvl = LDDL_PLAN_PRIO - 1 - q;  // 3 .. 0 over the partition
-          if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
-          else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
-          else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
-          else __builtin_amdgcn_s_setprio(0);
-        }
+      if (prio_done >= prio_next) {
+        ++prio_q;
+        prio_next = (int32_t)(((int64_t)(prio_q + 1) * prio_tot + LDDL_PLAN_PRIO - 1) / LDDL_PLAN_PRIO);
+        const int lvl = LDDL_PLAN_PRIO - 1 - prio_q;
+        if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+        else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+        else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
       }
+      ++prio_done;
 #endif
-      const int64_t s0 = doc_off(di);
-      const int ns = (int)(doc_off(di + 1) - s0);
-      La.reset(A.ks_len + s0, ns);
+      const int32_t ls0 = doc_loc(di);
+      const int64_t s0 = kbase + ls0;
+      const int ns = doc_loc(di + 1) - ls0;
+      La.reset(ks_len_p + ls0, ns);
       int32_t target = max_num;
-      if (rng.rand53() < A.k_short) target = (int32_t)rng.randint(2, max_num);
+      if (rng.rand53() < A.k_short) target = rng.randint32(2, max_num);
       // chunks: sentences are accumulated until the target length or the document end
       // (pretrain.py:276-280); after a random-next pair the unused sentences are put back
       // (320-321), so the next chunk starts right after A
       for (int chunk0 = 0; chunk0 < ns;) {
         const int i = La.find(chunk0, ns, target);  // the chunk is [chunk0, i]
         const int chunk_n = i - chunk0 + 1;
-        const int a_end = chunk_n >= 2 ? (int)rng.randint(1, chunk_n - 1) : 1;
+        const int a_end = chunk_n >= 2 ? rng.randint32(1, chunk_n - 1) : 1;
         int32_t flags = 0;
         const int64_t la = La.sum(chunk0, chunk0 + a_end, flags);
         int64_t lb = 0, b_ks;
@@ -731,17 +738,17 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
         if (chunk_n == 1 || rng.below_half()) {
           rn = 1;
           const int64_t target_b = target - la;
-          int64_t rd = 0;
+          int32_t rd = 0;
           for (int t = 0; t < 10; ++t) {
-            rd = rng.randint(0, nd - 1);
+            rd = rng.randint32(0, nd - 1);
             if (rd != di) break;
           }
           if (rd == di) rn = 0;
-          const int64_t r0 = doc_off(rd);
-          const int rns = (int)(doc_off(rd + 1) - r0);
-          const int rstart = (int)rng.randint(0, rns - 1);
-          b_ks = r0 + rstart;
-          Lb.reset(A.ks_len + r0, rns);
+          const int32_t r0l = doc_loc(rd);
+          const int rns = doc_loc(rd + 1) - r0l;
+          const int rstart = rng.randint32(0, rns - 1);
+          b_ks = kbase + (r0l + rstart);
+          Lb.reset(ks_len_p + r0l, rns);
           const int jb = Lb.find(rstart, rns, target_b);  // B is [rstart, jb] (314-317)
           lb = Lb.sum(rstart, jb + 1, flags);
           next0 = chunk0 + a_end;
@@ -774,7 +781,7 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
             nc = uni(c);
           }
           STAMP_ADD(1, st_t);
-          int32_t num = (int32_t)rint((double)(na + nb + 3) * A.ratio);  // round(): half-even
+          int32_t num = A.num_tab[na + nb + 3];  // (host table, below)
           if (num < 1) num = 1;
           if (num > nc) num = nc;
           // pool space for this pair's shuffle draws (nc) and masks (num): bump allocation in
@@ -1901,6 +1908,18 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   A.ratio = prm->masked_lm_ratio;
   A.k_short = short_threshold(prm->short_seq_prob);
   A.seq_r64 = ((prm->seq + 63) / 64) * 64;
+  {  // num_to_predict for every pair length n <= seq: round(n * ratio) as CPython computes it
+    std::vector<int16_t> h(prm->seq + 4);
+    for (int n = 0; n < (int)h.size(); ++n) {
+      const double v = rint((double)n * prm->masked_lm_ratio);
+      h[n] = (int16_t)std::min<double>(v, 32767.0);
+    }
+    int16_t* d_tab;
+    TRY(P->alloc(&d_tab, (int64_t)h.size(), st));
+    LDDL_HIP(hipMemcpyAsync(d_tab, h.data(), 2 * h.size(), hipMemcpyHostToDevice, st));
+    LDDL_HIP(hipStreamSynchronize(st));  // (h is a host temporary)
+    A.num_tab = d_tab;
+  }
   A.desc = P->desc;
   A.jseq = jseq;
   A.nmask = P->nmask;
