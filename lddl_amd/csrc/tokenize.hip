@@ -1065,11 +1065,13 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
       const int sl = (int)(head % kRing);
       const int st = W.r_flags[sl];
       if (!(st & kClosed) || W.r_pending[sl] > 0) break;
-      if (lane == 0) {
+      {
         const int32_t sid = W.r_sent[sl];
-        if (st & kFallback) fb_list[atomicAdd(fb_n, 1u)] = sid;
-        else
+        if (st & kFallback) {
+          if (lane == 0) fb_list[atomicAdd(fb_n, 1u)] = sid;
+        } else {
           sent_len[sid] = (W.r_count[sl] < max_pieces ? W.r_count[sl] : max_pieces) | (st & kLenHasClsSep);
+        }
       }
       ++head;
     }
@@ -1100,7 +1102,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
         nb0 = sent_off[q0];
         nb1 = sent_off[q0 + 1];
       }
-      if (lane == 0) {
+      {  // every lane writes the same values (one merged write each, no exec-mask branch)
         W.r_b0[cur_slot] = b0;
         W.r_sent[cur_slot] = (int32_t)s;
         W.r_count[cur_slot] = 0;
@@ -1128,7 +1130,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
         slotB = (int)(tail % kRing);
         b0B = nb0;
         b1B = nb1;
-        if (lane == 0) {
+        {
           W.r_b0[slotB] = b0B;
           W.r_sent[slotB] = sn;
           W.r_count[slotB] = 0;
@@ -1210,7 +1212,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
         if (((R.slow >> lane) & 1ull) && R.unit_byte) W.q_slow[qn + __popcll(R.US & upto) - 1] = 1;
         if (k < 64) {  // the first segment's sentence is complete: the second one becomes current
           const int na = __popcll(R.UE & ((1ull << k) - 1));
-          if (lane == 0) {
+          {  // (all lanes read the same old values and write the same new ones)
             W.r_pending[cur_slot] += na;
             W.r_flags[cur_slot] |= kClosed;
             W.r_pending[slotB] += n - na;
@@ -1218,7 +1220,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
           cur_slot = slotB;
           b0 = b0B;
           b1 = b1B;
-        } else if (lane == 0) {
+        } else {
           W.r_pending[cur_slot] += n;
         }
         wave_sync();
@@ -1227,7 +1229,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
       }
     }
     if (pos >= b1) {
-      if (lane == 0) W.r_flags[cur_slot] |= kClosed;
+      W.r_flags[cur_slot] |= kClosed;
       wave_sync();
       cur = false;
     }
