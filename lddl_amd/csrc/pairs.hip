@@ -639,8 +639,11 @@ __device__ inline void densify_group(int64_t k0, const int64_t* __restrict__ ks_
   }
 }
 
+// waves per SIMD the compiler must keep: 8 caps the kernel at 78 SGPRs (140 spilled to VGPR
+// lanes); 6 lets it use all 106 (59 spilled) at 7 waves/SIMD, 176 -> 169.6 ms per 10 GB
+// (profiles/r02_plan_minw_ab.txt)
 #ifndef LDDL_PLAN_MINW
-#define LDDL_PLAN_MINW 8
+#define LDDL_PLAN_MINW 6
 #endif
 __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
