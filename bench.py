@@ -369,8 +369,10 @@ def run_c5(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=5)
-    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=None,
+                    help='timed steps (default 5; c5: 200 batches, so that the 8 bin loaders\' '
+                         'worker start-up and shuffle-buffer fill stay outside the rate)')
+    ap.add_argument('--warmup', type=int, default=None, help='untimed steps (default 1; c5: 20)')
     ap.add_argument('--batch-bytes', type=int, default=None,
                     help='sentence text per GPU per step (default: the 10 GB corpus of C2 in one '
                          'step, HBM-resident; 4 GiB for c4, for HBM headroom of the balance)')
@@ -401,6 +403,10 @@ def main():
                     help='replay: CPython MT19937 per partition, bit-exact with the reference; '
                          'native: Philox counter RNG, documents and pairs in parallel')
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 200 if args.workload == 'c5' else 5
+    if args.warmup is None:
+        args.warmup = 20 if args.workload == 'c5' else 1
     if args.seq is None:
         args.seq = 128 if args.workload == 'c2' else 512
     if args.batch_bytes is None:  # C2: the whole 10 GB corpus of BASELINE configs[1] per step
