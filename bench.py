@@ -52,6 +52,32 @@ SHARE_DEVICE = os.environ.get('LDDL_BENCH_SHARE_DEVICE') == '1'
 RED_DEV = 'cpu' if SHARE_DEVICE else None
 
 
+def launch_command(argv, env, n_devices, gpus):
+    """`python bench.py --gpus N` with N > 1 and no launcher around it: the command that starts N
+    fresh one-GPU ranks (torch.distributed.run, the reference's `mpirun -np` launch model,
+    examples/local_example.sh:56-70). None when this process is already a rank (WORLD_SIZE set) or
+    N == 1. Raises SystemExit when N exceeds the visible devices (unless LDDL_BENCH_SHARE_DEVICE=1,
+    the one-GPU rehearsal) or disagrees with an outer launcher's WORLD_SIZE.
+
+    Called before anything touches the GPU: the parent only counts devices (no HIP init on this
+    image) and waits for the child; it never re-execs itself."""
+    if 'WORLD_SIZE' in env:
+        if int(env['WORLD_SIZE']) != gpus and gpus != 1:
+            raise SystemExit('bench.py: --gpus {} but WORLD_SIZE={}'.format(gpus, env['WORLD_SIZE']))
+        return None
+    if gpus <= 1:
+        return None
+    if env.get('LDDL_BENCH_SHARE_DEVICE') != '1' and gpus > n_devices:
+        raise SystemExit('bench.py: --gpus {} but only {} GPU(s) are visible'.format(gpus, n_devices))
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+            '--nproc-per-node', str(gpus), '--master-addr', '127.0.0.1', '--master-port', str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
 def make_batch(rank, args):
     from lddl_amd import synth
     corp = synth.generate(seed=args.seed, n_bytes=args.batch_bytes, doc_begin=rank * 50_000_000,
@@ -62,14 +88,42 @@ def make_batch(rank, args):
     return corp, part, seeds
 
 
+def granted_cores():
+    """Host cores this process may actually use: the CPU affinity mask, capped by the cgroup CPU
+    quota (cgroup v2 cpu.max, else v1 cfs_quota_us / cfs_period_us). os.cpu_count() reports the
+    whole machine. Returns (cores, derivation string)."""
+    import math
+    aff = len(os.sched_getaffinity(0))
+    quota, src = None, 'none'
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, p = f.read().split()[:2]
+        if q != 'max':
+            quota, src = int(q) / int(p), 'cgroup v2 cpu.max {}/{}'.format(q, p)
+    except (OSError, ValueError):
+        try:
+            with open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us') as f:
+                q = int(f.read())
+            with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as f:
+                p = int(f.read())
+            if q > 0:
+                quota, src = q / p, 'cgroup v1 cfs quota {}/{}'.format(q, p)
+        except (OSError, ValueError):
+            pass
+    cores = aff if quota is None else max(1, min(aff, int(math.floor(quota + 1e-9))))
+    return cores, 'sched_getaffinity = {}, CPU quota = {} ({}), os.cpu_count() = {}'.format(
+        aff, 'none' if quota is None else '{:g}'.format(quota), src, os.cpu_count())
+
+
 def cpu_baseline(corp, part, seeds, args):
     """The oracle (C restatement of the reference algorithm) on a bounded sample of the same
-    workload, one single-threaded process per host core used (the reference's
+    workload, one single-threaded process per granted host core (the reference's
     Dask/mpi4py pipeline runs one single-threaded worker per core): worker w takes its own run
     of ~cpu_sample_bytes of consecutive partitions. value = all workers' output tokens / wall."""
     import multiprocessing as mp
     from oracle.cpu_worker import cpu_worker
-    n_proc = max(1, min(args.cpu_procs, os.cpu_count() or 1))
+    cores, derivation = granted_cores()
+    n_proc = max(1, cores if args.cpu_procs is None else min(args.cpu_procs, cores))
     doc_bytes = corp.sent_off[corp.doc_sent_off]
     jobs, p0 = [], 0
     for _ in range(n_proc):
@@ -110,10 +164,11 @@ def cpu_baseline(corp, part, seeds, args):
                             'outside the +-25% band SURVEY 8d asks for: it is a stronger baseline '
                             'than the reference, not a timing of it (the reference cannot run on '
                             'the GPU box)').format(per_core / BASELINE_ANCHOR_PER_CORE),
-            'sample': '{} single-threaded processes x ~{:.0f} MB of consecutive partitions = {:.1f} '
-                      'MB of the same synthetic batch (tokenize + pairs + static masking, '
-                      'oracle/lddl_oracle.c), {:.1f} s wall; host os.cpu_count() = {}'.format(
-                          len(jobs), args.cpu_sample_bytes / 1e6, mb, wall, os.cpu_count())}
+            'granted_cores': cores, 'os_cpu_count': os.cpu_count(),
+            'sample': '{} single-threaded processes (one per granted core: {}) x ~{:.0f} MB of '
+                      'consecutive partitions = {:.1f} MB of the same synthetic batch (tokenize + '
+                      'pairs + static masking, oracle/lddl_oracle.c), {:.1f} s wall'.format(
+                          len(jobs), derivation, args.cpu_sample_bytes / 1e6, mb, wall)}
 
 
 def timed_segmented(args, rank, world, ctx, dev):
@@ -238,15 +293,22 @@ class TinyBert(torch.nn.Module):
         self.mlm = torch.nn.Linear(hidden, vocab)
         self.nsp = torch.nn.Linear(hidden, 2)
 
-    def forward(self, b, ignore_index=-1):
+    def forward(self, b, ignore_index=-1, mlm_cap=0.2):
+        """No host syncs: the MLM head runs on a fixed number of slots (mlm_cap of the batch,
+        above the 0.15 masking rate), the masked ones first (stable sort of the label mask);
+        unmasked slots among them carry ignore_index and drop out of the loss."""
         ids = b['input_ids']
         L = ids.size(1)
         h = self.tok(ids) + self.typ(b['token_type_ids']) + self.pos.weight[:L][None]
         h = self.norm(h) * b['attention_mask'][..., None]
         h = h + self.mlp(h)
-        lab = b['labels']
-        sel = lab != ignore_index
-        mlm = torch.nn.functional.cross_entropy(self.mlm(h[sel]).float(), lab[sel])
+        lab = b['labels'].reshape(-1)
+        k = max(1, int(mlm_cap * lab.numel()))
+        idx = torch.sort((lab != ignore_index).to(torch.int8), descending=True,
+                         stable=True).indices[:k]
+        hs = h.reshape(-1, h.size(-1)).index_select(0, idx)
+        mlm = torch.nn.functional.cross_entropy(self.mlm(hs).float(), lab.index_select(0, idx),
+                                                ignore_index=ignore_index)
         nsp = torch.nn.functional.cross_entropy(self.nsp(h[:, 0]).float(),
                                                 b['next_sentence_labels'])
         return mlm + nsp
@@ -390,8 +452,9 @@ def main():
     ap.add_argument('--seed', type=int, default=1234)
     ap.add_argument('--gen-threads', type=int, default=16)
     ap.add_argument('--cpu-sample-bytes', type=int, default=48 << 20)
-    ap.add_argument('--cpu-procs', type=int, default=16,
-                    help='CPU baseline processes (one per host core used; the GPU box grants 16)')
+    ap.add_argument('--cpu-procs', type=int, default=None,
+                    help='CPU baseline processes (default: one per granted host core, '
+                         'granted_cores(); a value above the grant is capped to it)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-alt-rng', dest='alt_rng', action='store_false',
                     help='skip timing the other RNG mode (reported as alt_rng)')
@@ -411,13 +474,20 @@ def main():
         args.seq = 128 if args.workload == 'c2' else 512
     if args.batch_bytes is None:  # C2: the whole 10 GB corpus of BASELINE configs[1] per step
         args.batch_bytes = 10_000_000_000 if args.workload == 'c2' else (4 << 30)
+        if SHARE_DEVICE and args.gpus > 1:  # all ranks share one GPU's HBM in the rehearsal
+            args.batch_bytes = min(args.batch_bytes, 2 << 30)
 
+    if args.workload == 'c5' and args.gpus > 1:
+        raise SystemExit('C5 is measured per replica (--gpus 1)')
+    cmd = launch_command(sys.argv[1:], os.environ, torch.cuda.device_count(), args.gpus)
+    if cmd is not None:  # N fresh one-GPU ranks; rank 0 prints the JSON line
+        import subprocess
+        sys.stdout.flush()
+        raise SystemExit(subprocess.call(cmd, env=dict(os.environ)))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if args.workload == 'c5':
-        if world > 1:
-            raise SystemExit('C5 is measured per replica (--gpus 1)')
         print(json.dumps(run_c5(args)), flush=True)
         return
     if world > 1:

@@ -121,7 +121,9 @@ def _pack(batch, static):
 
 
 def _dev(a, device):
-    return torch.from_numpy(np.ascontiguousarray(a)).to(device, non_blocking=True)
+    """Host array -> device through a pinned staging copy: a copy from pageable memory would
+    make the host wait for everything queued before it (the consumer's training step)."""
+    return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(device, non_blocking=True)
 
 
 def _to_encoded_inputs(batch, tokenizer, sequence_length_alignment=8, ignore_index=-1):
