@@ -171,10 +171,13 @@ def cpu_baseline(corp, part, seeds, args):
                           len(jobs), derivation, args.cpu_sample_bytes / 1e6, mb, wall)}
 
 
-def timed_segmented(args, rank, world, ctx, dev):
+def timed_segmented(args, rank, world, ctx, dev, params=None):
     """The step from raw document text (what the reference hands to sent_tokenize,
-    pretrain.py:86): GPU Punkt segmentation (untrained parameters, as offline nltk runs) ->
-    WordPiece -> pairs + static masking, same synthetic documents (sentences joined by spaces)."""
+    pretrain.py:86): GPU Punkt segmentation -> WordPiece -> pairs + static masking, same
+    synthetic documents (sentences joined by spaces). params None: the untrained parameters
+    (what offline nltk runs, segment_eval_kernel<false>); else a PunktParams (trained model:
+    abbreviations, collocations, sentence starters, orthographic context — the English-model
+    configuration of the reference, segment_eval_kernel<true>)."""
     from lddl_amd import punkt, synth
     from lddl_amd.pairs import make_pairs
     text, doc_off = synth.generate_doc_text(seed=args.seed, n_bytes=args.batch_bytes,
@@ -187,7 +190,7 @@ def timed_segmented(args, rank, world, ctx, dev):
     d_doc = torch.from_numpy(doc_off).to(dev)
     d_part = torch.from_numpy(part).to(dev)
     d_seed = torch.from_numpy(seeds).to(dev)
-    punkt.set_params(ctx, None)
+    punkt.set_params(ctx, params)
     info = {}
 
     def step(ev=None):
@@ -200,9 +203,9 @@ def timed_segmented(args, rank, world, ctx, dev):
         pb = make_pairs(ctx, so, ids, sl, ds, d_part, d_seed, seq=args.seq, dup=5, masking=True,
                         short_seq_prob=0.1, masked_lm_ratio=0.15, rng=args.rng)
         del ids, sl
-        if args.workload == 'c4':
+        if args.workload in ('c3', 'c4'):
             from lddl_amd.balance import balance
-            bb = balance(ctx, pb, 8, args.seq // 8)
+            bb = balance(ctx, pb, 8, args.seq // 8, num_shards=args.num_shards or 8)
             n = bb.n_tokens + 3 * bb.n_rows
             del bb
         else:
@@ -440,7 +443,13 @@ def main():
                          'step, HBM-resident; 4 GiB for c4, for HBM headroom of the balance)')
     ap.add_argument('--partition-bytes', type=int, default=1 << 20)
     ap.add_argument('--seq', type=int, default=None)
-    ap.add_argument('--workload', choices=['c2', 'c4', 'c5'], default='c2')
+    ap.add_argument('--workload', choices=['c2', 'c3', 'c4', 'c5'], default='c2')
+    ap.add_argument('--sub-batch-bytes', type=int, default=10_000_000_000,
+                    help='c3/c4: the resident corpus streams through tokenize -> pairs -> balance '
+                         'in sub-batches of about this many text bytes (one batch\'s tables in '
+                         'HBM at a time; balance state carried across them)')
+    ap.add_argument('--num-shards', type=int, default=None,
+                    help='c3/c4: balanced shards (default 8 per rank)')
     ap.add_argument('--c5-corpus-bytes', type=int, default=96 << 20)
     ap.add_argument('--c5-bin-size', type=int, default=64,
                     help='C5 loader bins (64 -> 8 bins, the reference example local_example.sh)')
@@ -462,6 +471,10 @@ def main():
                     help='skip the PCIe-inclusive and reference-partitioning lines (c2)')
     ap.add_argument('--no-segmented-line', dest='segmented_line', action='store_false',
                     help='skip timing the raw-document input (GPU Punkt segmentation in the step)')
+    ap.add_argument('--punkt-params', default=os.path.join(REPO, 'tests', 'golden',
+                                                           'punkt_params.json'),
+                    help='PunktParameters JSON for the trained-model segmentation line '
+                         '(with_segmentation.trained); empty string skips it')
     ap.add_argument('--rng', choices=['replay', 'native'], default='replay',
                     help='replay: CPython MT19937 per partition, bit-exact with the reference; '
                          'native: Philox counter RNG, documents and pairs in parallel')
@@ -472,8 +485,10 @@ def main():
         args.warmup = 20 if args.workload == 'c5' else 1
     if args.seq is None:
         args.seq = 128 if args.workload == 'c2' else 512
-    if args.batch_bytes is None:  # C2: the whole 10 GB corpus of BASELINE configs[1] per step
-        args.batch_bytes = 10_000_000_000 if args.workload == 'c2' else (4 << 30)
+    if args.batch_bytes is None:
+        # C2 / C3: the whole 10 GB corpus of BASELINE configs[1] / configs[2] per step; C4: the
+        # 200 GB corpus of configs[3] over 8 GPUs = 25 GB of text per GPU
+        args.batch_bytes = 25_000_000_000 if args.workload == 'c4' else 10_000_000_000
         if SHARE_DEVICE and args.gpus > 1:  # all ranks share one GPU's HBM in the rehearsal
             args.batch_bytes = min(args.batch_bytes, 2 << 30)
 
@@ -511,46 +526,89 @@ def main():
                 part_seed=torch.from_numpy(seeds).to(dev))
 
     diag = {}  # {'balance': {}}: balance() records synchronised phase times (untimed step only)
+    stream = args.workload in ('c3', 'c4')
+    n_shards = args.num_shards or 8 * world
+    subs = None
+    if stream:  # the resident corpus in K sub-batches of whole partitions (offsets rebased once)
+        K = max(1, -(-args.batch_bytes // args.sub_batch_bytes))
+        doc_b = corp.sent_off[corp.doc_sent_off[part]]
+        pc = np.unique(np.searchsorted(doc_b, np.arange(K + 1) * doc_b[-1] / K, 'left'))
+        pc[-1] = len(part) - 1
+        subs = []
+        for p0, p1 in zip(pc[:-1], pc[1:]):
+            d0, d1 = part[p0], part[p1]
+            s0, s1 = corp.doc_sent_off[d0], corp.doc_sent_off[d1]
+            b0, b1 = corp.sent_off[s0], corp.sent_off[s1]
+            up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+            subs.append(dict(text=text[b0:b1], sent_off=up(corp.sent_off[s0:s1 + 1] - b0),
+                             doc_off=up(corp.doc_sent_off[d0:d1 + 1] - s0),
+                             part_off=up(part[p0:p1 + 1] - d0), part_seed=up(seeds[p0:p1])))
+
+    def record(ev, i):
+        if ev is not None:
+            if i == 0:
+                ev.append([torch.cuda.Event(enable_timing=True) for _ in range(3)])
+            ev[-1][i].record()
 
     def step(ev=None, rng=args.rng, b=None):
+        """ev: list that collects one (start, tokenized, paired) event triple per (sub-)batch."""
         b = base if b is None else b
         if args.chunks > 1 and args.workload == 'c2':
             return step_chunked(ev, rng, b)
-        if ev is not None:
-            ev[0].record()
-        ids, sent_len = ctx.tokenize(b['text'], b['sent_off'])
-        if ev is not None:
-            ev[1].record()
-        pb = make_pairs(ctx, b['sent_off'], ids, sent_len, doc_off, b['part_off'], b['part_seed'],
-                        seq=args.seq, dup=5, masking=True, short_seq_prob=0.1,
-                        masked_lm_ratio=0.15, rng=rng)
-        del ids
-        if args.workload == 'c4':
-            bb = balance(ctx, pb, 8, args.seq // 8, timings=diag.get('balance'))
-            n_tok = bb.n_tokens + 3 * bb.n_rows
-            del bb
-        else:
-            n_tok = int(pb.tokens.numel()) + 3 * pb.n_pairs
-        if ev is not None:
-            ev[2].record()
-        st = {'pairs': pb.n_pairs, 'masked': pb.n_masked, 'plan_ms': pb.plan_ms, 'tokens': n_tok,
-              'kept_sent': pb.n_kept_sentences, 'kept_doc': pb.n_kept_documents}
-        del pb  # nothing of a step outlives it (HBM is reused by the next step)
-        return n_tok, st, sent_len
+        sb = None
+        if stream:
+            from lddl_amd.balance import StreamBalancer
+            sb = StreamBalancer(ctx, 8, args.seq // 8, num_shards=n_shards)
+        n_tok = 0
+        st = {'pairs': 0, 'masked': 0, 'plan_ms': 0.0, 'tokens': 0, 'kept_sent': 0,
+              'kept_doc': 0, 'moved_rows': 0}
+        sent_lens = []
+        for sub in (subs if stream else [dict(b, doc_off=doc_off)]):
+            record(ev, 0)
+            ids, sent_len = ctx.tokenize(sub['text'], sub['sent_off'])
+            sent_lens.append(sent_len)
+            record(ev, 1)
+            pb = make_pairs(ctx, sub['sent_off'], ids, sent_len, sub['doc_off'], sub['part_off'],
+                            sub['part_seed'], seq=args.seq, dup=5, masking=True,
+                            short_seq_prob=0.1, masked_lm_ratio=0.15, rng=rng)
+            del ids
+            if sb is not None:
+                tm = None
+                if 'balance' in diag:
+                    tm = {}
+                bb = sb.step(pb, timings=tm)
+                if tm is not None:
+                    keys = list(tm)
+                    for p_, k_ in zip(keys, keys[1:]):
+                        diag['balance'][k_] = diag['balance'].get(k_, 0.0) + (tm[k_] - tm[p_]) * 1e3
+                n = bb.n_tokens + 3 * bb.n_rows
+                st['moved_rows'] += bb.moved_rows
+                del bb
+            else:
+                n = int(pb.tokens.numel()) + 3 * pb.n_pairs
+            record(ev, 2)
+            n_tok += n
+            for k_, v_ in (('pairs', pb.n_pairs), ('masked', pb.n_masked), ('plan_ms', pb.plan_ms),
+                           ('tokens', n), ('kept_sent', pb.n_kept_sentences),
+                           ('kept_doc', pb.n_kept_documents)):
+                st[k_] += v_
+            del pb  # nothing of a step outlives it (HBM is reused by the next step)
+        if sb is not None:
+            st['shard_counts_spread'] = int((sb.all_shard_counts.max(0) -
+                                             sb.all_shard_counts.min(0)).max())
+        return n_tok, st, sent_lens
 
     def step_chunked(ev, rng, b):
         """The same step with tokenization of chunk k+1 pipelined under the pairs of chunk k
         (lddl_amd.pairs.tokenize_and_pair_chunked); tokenize_ms then spans only chunk 0."""
         from lddl_amd.pairs import tokenize_and_pair_chunked
-        if ev is not None:
-            ev[0].record()
-            ev[1].record()
+        record(ev, 0)
+        record(ev, 1)
         pbs = tokenize_and_pair_chunked(ctx, b['text'], b['sent_off'], doc_off, b['part_off'],
                                         b['part_seed'], n_chunks=args.chunks, seq=args.seq, dup=5,
                                         masking=True, short_seq_prob=0.1, masked_lm_ratio=0.15,
                                         rng=rng)
-        if ev is not None:
-            ev[2].record()
+        record(ev, 2)
         n_tok = sum(int(p.tokens.numel()) + 3 * p.n_pairs for p in pbs)
         st = {'pairs': sum(p.n_pairs for p in pbs), 'masked': sum(p.n_masked for p in pbs),
               'plan_ms': sum(p.plan_ms for p in pbs), 'tokens': n_tok,
@@ -567,7 +625,7 @@ def main():
         for _ in range(args.warmup):
             step(rng=rng, b=b)
         torch.cuda.synchronize()
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        evs = [[] for _ in range(args.steps)]
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -649,26 +707,25 @@ def main():
             ref_part[r] = {'value': rtok / rdt, 'ms_per_step': rdt / args.steps * 1e3,
                            'plan_ms': float(np.mean([x['plan_ms'] for x in rst]))}
         del rb
-    tok_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    pair_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    tok_ms = float(np.mean([sum(e[0].elapsed_time(e[1]) for e in ev) for ev in evs]))
+    pair_ms = float(np.mean([sum(e[1].elapsed_time(e[2]) for e in ev) for ev in evs]))
     plan_ms = float(np.mean([s['plan_ms'] for s in stats]))
     st = stats[-1]
     n_pairs = st['pairs']
     if sent_len is None:  # chunked step: the tokenizer's own launch, timed once more (untimed step)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        _, sent_len = ctx.tokenize(text, sent_off)
+        _, sl = ctx.tokenize(text, sent_off)
         e1.record()
         torch.cuda.synchronize()
         tok_ms = e0.elapsed_time(e1)
-    pieces = int((sent_len & ((1 << 30) - 1)).sum())
+        sent_len = [sl]
+    pieces = sum(int((sl & ((1 << 30) - 1)).sum()) for sl in sent_len)
     bal_ms = None
-    if args.workload == 'c4':  # one more, untimed step with the balance phases timed
+    if stream:  # one more, untimed step with the balance phases timed (summed over sub-batches)
         diag['balance'] = {}
         step()
-        bt = diag.pop('balance')
-        keys = list(bt)
-        bal_ms = {k: (bt[k] - bt[p]) * 1e3 for p, k in zip(keys, keys[1:])}
+        bal_ms = diag.pop('balance')
     alt = None
     if args.alt_rng:  # the other RNG mode on the same batch, reported beside the headline
         other = 'native' if args.rng == 'replay' else 'replay'
@@ -678,6 +735,11 @@ def main():
     seg = None
     if args.segmented_line and world == 1:  # the same path from raw document text: Punkt first
         seg = timed_segmented(args, rank, world, ctx, dev)
+        if args.punkt_params:  # the trained-model kernel on the same documents
+            from lddl_amd.punkt import PunktParams
+            seg['trained'] = timed_segmented(args, rank, world, ctx, dev,
+                                             PunktParams.from_json(args.punkt_params))
+            seg['trained']['punkt_params'] = os.path.relpath(args.punkt_params, REPO)
     mem = torch.cuda.memory_stats()
     if rank != 0:
         dist.destroy_process_group()
@@ -771,10 +833,12 @@ def main():
             'workload': ('C2: synthetic English-like corpus (SURVEY 8d generator, seed {}), '
                          'seq {}, static masking, duplicate_factor 5, no binning; {} MiB of '
                          'sentence text per GPU per step, {} KiB partitions' if args.workload == 'c2'
-                         else 'C3/C4: synthetic English-like corpus (SURVEY 8d generator, seed {}), '
-                         'seq {} phase 2, static masking, duplicate_factor 5, 64 bins of 8 tokens + '
-                         'HBM load balance (RCCL count all-gather + all-to-all-v exchange when N > 1)'
-                         '; {} MiB of sentence text per GPU per step, {} KiB partitions').format(
+                         else args.workload.upper() + ': synthetic English-like corpus (SURVEY 8d '
+                         'generator, seed {}), seq {} phase 2, static masking, duplicate_factor 5, 64 '
+                         'bins of 8 tokens + streaming load balance into ' + str(n_shards) +
+                         ' shards (per sub-batch: RCCL count all-gather + all-to-all-v exchange '
+                         'when N > 1); {} MiB of sentence text per GPU per step, {} KiB partitions, '
+                         + str(len(subs or [0])) + ' sub-batch(es)').format(
                              args.seed, args.seq, args.batch_bytes >> 20, args.partition_bytes >> 10),
             'seq_len': args.seq, 'masking': 'static', 'duplicate_factor': 5,
             'rng': ('replay (CPython MT19937, random.seed per partition)' if args.rng == 'replay'
@@ -786,7 +850,8 @@ def main():
         'stages_ms': {'tokenize': tok_ms,
                       ('pairs_plan_and_gather' if args.workload == 'c2' else
                        'pairs_bin_and_balance'): pair_ms,
-                      'per_step_pairs': [round(e[1].elapsed_time(e[2]), 2) for e in evs],
+                      'per_step_pairs': [round(sum(e[1].elapsed_time(e[2]) for e in ev), 2)
+                                         for ev in evs],
                       'per_step_plan': [round(x['plan_ms'], 2) for x in stats]},
         'roofline': None,  # the dominant kernel's, filled below
         'roofline_planner': plan_roof,
@@ -798,6 +863,8 @@ def main():
     res['roofline'] = plan_roof if plan_ms >= tok_ms else tok_roof
     if bal_ms is not None:
         res['balance_phases_ms_untimed_step'] = bal_ms
+        res['balance'] = {'num_shards': n_shards, 'moved_rows_per_step': st.get('moved_rows'),
+                          'max_shard_spread_rows': st.get('shard_counts_spread')}
     if alt is not None:
         res['alt_rng'] = alt
     if seg is not None:

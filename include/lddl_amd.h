@@ -66,6 +66,16 @@ int lddl_ctx_info(const lddl_ctx* ctx, int32_t* vocab_size, int32_t* special_ids
  * bytes[off[i] .. off[i+1]) */
 int lddl_ctx_render_table(const lddl_ctx* ctx, const uint8_t** d_bytes, const int64_t** d_off);
 
+/* Device allocator of the library's per-call temporaries (pair plans, scans, binning scratch).
+ * Default: the ctx's own cache of hipMalloc blocks. With callbacks set, every temporary comes
+ * from alloc_fn(bytes, stream, user) and goes back through free_fn(p, stream, user) on the
+ * stream of its last use — a stream-ordered pool such as PyTorch's caching allocator
+ * (lddl_amd/context.py), so one allocator owns HBM. Both NULL restores the default. */
+typedef void* (*lddl_alloc_fn)(size_t bytes, void* stream, void* user);
+typedef void (*lddl_free_fn)(void* p, void* stream, void* user);
+int lddl_ctx_set_allocator(lddl_ctx* ctx, lddl_alloc_fn alloc_fn, lddl_free_fn free_fn,
+                           void* user);
+
 /* ---------------------------------------------------------------------------------------------
  * Tokenize sentences (device in, device out).
  * Replaces `tokenizer.tokenize(s, max_length=512, truncation=True)` per Punkt sentence
@@ -175,11 +185,13 @@ int lddl_bin_partitions(lddl_ctx* ctx, void* stream, const int32_t* d_num_tokens
                         const int64_t* d_part_off, int64_t n_part, int32_t bin_size, int32_t nbins,
                         int64_t* d_perm, int64_t* d_bin_id, int64_t* d_counts);
 
-/* The same regroup for ONE large segment (all rows of a rank before the load-balance exchange),
- * spread over many workgroups: d_perm / d_bin_id as above, d_counts[b] rows per bin. */
-int lddl_bin_stable(lddl_ctx* ctx, void* stream, const int32_t* d_num_tokens, int64_t n_rows,
-                    int32_t bin_size, int32_t nbins, int64_t* d_perm, int64_t* d_bin_id,
-                    int64_t* d_counts);
+/* The same regroup for ONE large segment (a rank's rows of one batch before the load-balance
+ * exchange), spread over many workgroups: d_perm / d_bin_id (may be NULL) as above, d_counts[b]
+ * rows per bin. num_tokens of row r = d_num_tokens[r], or, with d_num_tokens NULL, the pair's
+ * token count + 3 from a lddl_pairs_emit offset table: d_tok_off[r+1] - d_tok_off[r] + 3. */
+int lddl_bin_stable(lddl_ctx* ctx, void* stream, const int32_t* d_num_tokens,
+                    const int64_t* d_tok_off, int64_t n_rows, int32_t bin_size, int32_t nbins,
+                    int64_t* d_perm, int64_t* d_bin_id, int64_t* d_counts);
 
 /* ---------------------------------------------------------------------------------------------
  * Rendering of the parquet columns (lddl/dask/bert/pretrain.py:345-358):
@@ -188,11 +200,14 @@ int lddl_bin_stable(lddl_ctx* ctx, void* stream, const int32_t* d_num_tokens, in
  * Output row r renders pair d_rows[r] (d_rows NULL = identity) of a lddl_pairs_emit table.
  * lddl_render_lengths writes per-row byte lengths; the caller scans them (lddl_scan_i64) into
  * offsets and calls lddl_render_write. Label / position arguments may be NULL (no masking).
+ * It also writes the rows' num_tokens (uint16, len(A) + len(B) + 3) and, from d_is_rn,
+ * is_random_next in output order (each output pointer may be NULL).
  * ------------------------------------------------------------------------------------------- */
 int lddl_render_lengths(lddl_ctx* ctx, void* stream, const int32_t* d_tokens,
                         const int64_t* d_tok_off, const int32_t* d_len_a, const int32_t* d_lab,
                         const int64_t* d_pos_off, const int64_t* d_rows, int64_t n_rows,
-                        int64_t* d_a_len, int64_t* d_b_len, int64_t* d_l_len, int64_t* d_npy_len);
+                        int64_t* d_a_len, int64_t* d_b_len, int64_t* d_l_len, int64_t* d_npy_len,
+                        const uint8_t* d_is_rn, uint16_t* d_num_tokens_out, uint8_t* d_is_rn_out);
 int lddl_render_write(lddl_ctx* ctx, void* stream, const int32_t* d_tokens,
                       const int64_t* d_tok_off, const int32_t* d_len_a, const uint16_t* d_pos,
                       const int32_t* d_lab, const int64_t* d_pos_off, const int64_t* d_rows,
@@ -200,14 +215,41 @@ int lddl_render_write(lddl_ctx* ctx, void* stream, const int32_t* d_tokens,
                       const int64_t* d_l_off, const int64_t* d_npy_off, uint8_t* d_a_bytes,
                       uint8_t* d_b_bytes, uint8_t* d_l_bytes, uint8_t* d_npy_bytes);
 
-/* Ragged row gather (packing of the load-balance sample exchange): output row i is source row
- * d_rows[i] (NULL = i), elements d_src[d_src_off[r] .. d_src_off[r+1]) copied to
- * d_dst[d_dst_off[i] ...]. elem_bytes in {1, 2, 4, 8}; offsets count elements. */
-int lddl_gather_ragged(void* stream, const void* d_src, const int64_t* d_src_off, int32_t elem_bytes,
+/* ---------------------------------------------------------------------------------------------
+ * Row movement of the load balance (lddl_amd/balance.py; replaces the reference's filesystem
+ * shuffle, lddl/dask/load_balance.py:84-156). Rows are addressed over TWO sources: row r < n_a is
+ * row r of source A, else row r - n_a of source B (B may be NULL when every r < n_a); d_rows NULL
+ * = the identity (n_rows <= n_a). elem_bytes in {1, 2, 4, 8}; offsets count elements and are
+ * relative to their own source.
+ *   lddl_gather_ragged: elements src[off[r] .. off[r+1]) of output row i (r = d_rows[i]) copied to
+ *     d_dst[d_dst_off[i] ...].
+ *   lddl_take: d_dst[i] = src[r].
+ *   lddl_ragged_offsets: d_out[0..n_rows] = exclusive scan of the rows' sizes off[r+1] - off[r].
+ *   lddl_expand_segments: segment k covers d_out[seg_off[k] .. seg_off[k+1]); its element t is
+ *     v = seg[3k] + t * seg[3k+1], written as v when seg[3k+2] != 0, else as d_src[v]
+ *     (the balance plan's strided row runs, expanded on the device).
+ *   lddl_pairs_meta_pack: int32[n][4] {len(A)+len(B), len(A), is_random_next, masks} of rows d_rows
+ *     of a pair table (d_pos_off NULL: 0 masks); lddl_pairs_meta_unpack splits it into columns
+ *     (d_nmask may be NULL).
+ * ------------------------------------------------------------------------------------------- */
+int lddl_gather_ragged(void* stream, const void* d_src_a, const int64_t* d_off_a, int64_t n_a,
+                       const void* d_src_b, const int64_t* d_off_b, int32_t elem_bytes,
                        const int64_t* d_rows, int64_t n_rows, const int64_t* d_dst_off, void* d_dst);
+int lddl_take(void* stream, const void* d_a, int64_t n_a, const void* d_b, int32_t elem_bytes,
+              const int64_t* d_rows, int64_t n_rows, void* d_dst);
+int lddl_ragged_offsets(lddl_ctx* ctx, void* stream, const int64_t* d_off_a, int64_t n_a,
+                        const int64_t* d_off_b, const int64_t* d_rows, int64_t n_rows,
+                        int64_t* d_out);
+int lddl_expand_segments(void* stream, const int64_t* d_src, const int64_t* d_seg,
+                         const int64_t* d_seg_off, int64_t n_seg, int64_t total, int64_t* d_out);
+int lddl_pairs_meta_pack(void* stream, const int64_t* d_tok_off, const int32_t* d_len_a,
+                         const uint8_t* d_is_rn, const int64_t* d_pos_off, const int64_t* d_rows,
+                         int64_t n, int32_t* d_meta);
+int lddl_pairs_meta_unpack(void* stream, const int32_t* d_meta, int64_t n, int64_t* d_ntok,
+                           int32_t* d_len_a, uint8_t* d_is_rn, int64_t* d_nmask);
 
-/* Exclusive prefix sum: d_out[0..n] (d_out[n] = total) of d_in[0..n). */
-int lddl_scan_i64(void* stream, const int64_t* d_in, int64_t n, int64_t* d_out);
+/* Exclusive prefix sum: d_out[0..n] (d_out[n] = total) of d_in[0..n) (scratch from the ctx). */
+int lddl_scan_i64(lddl_ctx* ctx, void* stream, const int64_t* d_in, int64_t n, int64_t* d_out);
 
 /* ---------------------------------------------------------------------------------------------
  * Loader collate (lddl/torch/bert.py:69-149 `_to_encoded_inputs`), one batch, device in/out.

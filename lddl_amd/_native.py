@@ -45,13 +45,21 @@ SIGNATURES = {
     'lddl_pairs_plan_ms': (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float)]),
     'lddl_bin_partitions': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp,
                                            c_vp, c_vp]),
-    'lddl_bin_stable': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),
+    'lddl_bin_stable': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp,
+                                       c_vp]),
     'lddl_render_lengths': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
-                                           c_vp, c_vp, c_vp, c_vp]),
+                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'lddl_render_write': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                          c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    'lddl_scan_i64': (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),
-    'lddl_gather_ragged': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp]),
+    'lddl_scan_i64': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
+    'lddl_gather_ragged': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp, c_i64,
+                                          c_vp, c_vp]),
+    'lddl_take': (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_i64, c_vp]),
+    'lddl_ragged_offsets': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    'lddl_expand_segments': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
+    'lddl_pairs_meta_pack': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    'lddl_pairs_meta_unpack': (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    'lddl_ctx_set_allocator': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
     'lddl_collate_encode': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_i64]),

@@ -1,31 +1,35 @@
-"""HBM-resident load balance across GPUs (configs C3/C4).
+"""Streaming load balance across GPUs (configs C3/C4).
 
-The reference balances shards through the filesystem (lddl/dask/load_balance.py:41-369: MPI
-Allreduce of per-file counts, then read/concat/rewrite of parquet files) so that, per bin, every
-shard ends with N or N+1 samples (`Progress` targets, load_balance.py:161-169). When the samples
-are already in HBM on every GPU, the same contract is met with two collectives over RCCL/xGMI and
-no file traffic:
+The reference balances shards through the filesystem after preprocessing
+(lddl/dask/load_balance.py:41-369: MPI Allreduce of per-file counts, then read / concat /
+rewrite of parquet files) so that, per bin, every shard ends with N or N+1 samples (`Progress`
+targets, load_balance.py:161-169). Here the same contract is met batch by batch while the
+samples are in HBM, so a rank never holds more than one batch of pair tables, at any corpus size:
 
-  1. every rank orders its samples by bin (stable; `lddl_bin_stable`) and all-gathers its per-bin
-     counts (int64[world, nbins]) — the global bin-count all-gather of the north star;
-  2. all ranks compute the same plan (`plan_exchange`): bin b's samples in rank-major order are
-     cut into `num_shards` contiguous ranges of base or base+1 samples (the first total % S
-     shards get +1); shard s belongs to rank s * world // S, so each rank owns a contiguous run
-     of every bin and only the imbalance crosses ranks;
-  3. an all-to-all-v of the row metadata, then one per ragged column (token ids, masked
-     positions as bytes, labels), carries ONLY rows that change rank: rows that stay are never
-     packed or sent. The receiver's bin-major order interleaves its own rows with the received
-     ones in global order.
+  * the global order of bin b is batch after batch, rank after rank inside a batch, each rank's
+    rows in their stable bin order (`lddl_bin_stable`, binning.py:63-93 semantics);
+  * global row g of bin b goes to shard g % S (round-robin deal). Every prefix of a deal is
+    balanced, so after ANY number of batches each shard holds N or N+1 rows of every bin, the
+    first total % S shards the extra one — and a batch can be balanced, written and freed before
+    the next batch is built;
+  * per batch, each rank all-gathers its per-bin counts (int64[W, B], RCCL: the north star's
+    bin-count all-gather); with the totals of earlier batches every rank then knows the global
+    index of every row, and the rows of (source rank j, bin b, shard s) form one arithmetic run
+    of j's bin-b rows (`deal_runs`: first row (s - g0) mod S, stride S);
+  * shard s belongs to rank s * W // S. Rows of other ranks' shards cross in one all-to-all-v of
+    row metadata and one per ragged column (token ids, masked positions as bytes, labels);
+  * a rank's output is its shards' runs, bin-major, then shard, then source rank (= global order
+    inside a shard): a row order over [own table | received rows] built on the device
+    (`lddl_expand_segments`), materialised into one table (two-source ragged gathers) only when
+    rows arrived.
 
-Output (`BalancedBins`): when a rank received nothing (always at world size 1) the result is a
-row order over the rank's own table — no bytes move; otherwise the rank's rows are materialised
-once into a contiguous bin-major table (two ragged gathers: own rows, received rows).
+At world size 1 nothing moves: the result is a row order over the batch's own table. At W > 1
+(W - 1) / W of the rows cross ranks, the price of a balance that needs only the current batch.
 
-The algorithm is split into per-rank phases (`RankBalance`) so that the collective driver
-(`balance`, torch.distributed: RCCL on GPUs, gloo on CPUs) and the in-process driver over
-virtual ranks (`balance_virtual`, used by the tests to run W ranks on one GPU) execute the same
-plan, pack and regroup code. Data movement goes through `HipOps` (HIP kernels through the C ABI);
-there is no other implementation in the product.
+Every device step is a HIP kernel of liblddl_amd.so (`HipOps`); the plan is host integer math,
+replicated on every rank. The per-rank phases (`RankBalance`: bin, plan, pack, unpack, regroup)
+are shared by the collective driver (`StreamBalancer`, torch.distributed: RCCL on GPUs, gloo on
+CPUs) and the in-process driver over virtual ranks (`stream_virtual`, W ranks on one device).
 """
 import time
 from dataclasses import dataclass, field
@@ -46,31 +50,28 @@ def shard_owner(num_shards, world):
 
 
 def shard_targets(counts, num_shards):
-    """int64[S, B]: samples of bin b in shard s (N or N+1; the first total % S shards get +1,
-    the reference's Progress targets, load_balance.py:161-169)."""
-    total = np.asarray(counts, np.int64).sum(0)
+    """int64[S, B]: samples of bin b in shard s after dealing sum(counts) rows (N or N+1; the
+    first total % S shards get +1, the reference's Progress targets, load_balance.py:161-169)."""
+    total = np.asarray(counts, np.int64).reshape(-1, np.shape(counts)[-1]).sum(0)
     base, rem = total // num_shards, total % num_shards
     return base[None, :] + (np.arange(num_shards)[:, None] < rem[None, :]).astype(np.int64)
 
 
-def plan_exchange(counts, num_shards=None):
-    """counts int64[W, B] (rank j's samples in bin b) -> (target [W, B], send [W, W, B],
-    first [W, W, B]): rank j sends send[j, k, b] of its bin-b rows, starting at its local bin-b
-    row first[j, k, b], to rank k; rank k then holds target[k, b] bin-b samples (the sum of its
-    shards' targets). send[j, j, b] are the rows that stay on rank j."""
+def deal_runs(g0, counts, num_shards):
+    """Rows whose global indices are g0 .. g0 + counts - 1 (per bin), dealt to shard g % S:
+    returns (first, n), int64[..., B, S]: shard s gets the block's rows first + t * S, t < n."""
+    g0 = np.asarray(g0, np.int64)
+    c = np.asarray(counts, np.int64)[..., None]
+    first = (np.arange(num_shards, dtype=np.int64) - g0[..., None]) % num_shards
+    n = np.where(first < c, (c - 1 - first) // num_shards + 1, 0)
+    return first, n
+
+
+def batch_start(prior, counts):
+    """g0[j, b]: global index of rank j's first bin-b row of this batch (prior[b] rows of bin b in
+    earlier batches; ranks in order)."""
     counts = np.asarray(counts, np.int64)
-    W, B = counts.shape
-    S = W if num_shards is None else int(num_shards)
-    st = shard_targets(counts, S)
-    target = np.zeros((W, B), np.int64)
-    np.add.at(target, shard_owner(S, W), st)
-    src0 = np.cumsum(counts, 0) - counts
-    dst0 = np.cumsum(target, 0) - target
-    lo = np.maximum(src0[:, None, :], dst0[None, :, :])
-    hi = np.minimum((src0 + counts)[:, None, :], (dst0 + target)[None, :, :])
-    send = np.maximum(hi - lo, 0)
-    first = np.where(send > 0, lo - src0[:, None, :], 0)
-    return target, send, first
+    return np.asarray(prior, np.int64)[None, :] + np.cumsum(counts, 0) - counts
 
 
 def gather_counts(local_counts, group=None):
@@ -84,70 +85,95 @@ def gather_counts(local_counts, group=None):
 
 
 # ---- data-movement primitives ----------------------------------------------------------------
-class HipOps:
-    """The balance's device primitives: HIP kernels of liblddl_amd.so on torch's current stream."""
-
-    def __init__(self, ctx):
-        self.ctx = ctx
-
-    def bin_stable(self, num_tokens, bin_size, nbins):
-        """(perm int64[n], counts int64[nbins]): stable regroup of the rows by
-        bin_id = min((num_tokens - 1) // bin_size, nbins - 1) (binning.py:63-93)."""
-        from .output import bin_stable
-        perm, _, cnt = bin_stable(self.ctx, num_tokens, bin_size, nbins)
-        return perm, cnt
-
-    def scan(self, x):
-        out = torch.empty(x.numel() + 1, dtype=torch.int64, device=x.device)
-        check(lib.lddl_scan_i64(_stream(), _ptr(x), x.numel(), _ptr(out)))
-        return out
-
-    def gather_into(self, src, src_off, rows, dst_off, dst):
-        """dst[dst_off[i] ...] = src[src_off[rows[i]] .. src_off[rows[i] + 1])."""
-        if rows.numel() == 0:
-            return dst
-        check(lib.lddl_gather_ragged(_stream(), _ptr(src), _ptr(src_off), src.element_size(),
-                                     _ptr(rows), rows.numel(), _ptr(dst_off), _ptr(dst)))
-        return dst
-
-
 def _alloc(n, dtype, dev):
     return torch.empty(max(int(n), 1), dtype=dtype, device=dev)[:int(n)]
 
 
-def _expand(vec, starts, lens, dev):
-    """Concatenation of the slices vec[starts[i] : starts[i] + lens[i]] (one device gather)."""
-    total = int(sum(lens))
-    if total == 0:
-        return torch.zeros(0, dtype=vec.dtype, device=dev)
-    st = torch.tensor(starts, dtype=torch.int64, device=dev)
-    ln = torch.tensor(lens, dtype=torch.int64, device=dev)
-    first = torch.cumsum(ln, 0) - ln
-    idx = torch.repeat_interleave(st - first, ln, output_size=total) + torch.arange(
-        total, dtype=torch.int64, device=dev)
-    return vec.index_select(0, idx)
+class HipOps:
+    """The balance's device primitives: HIP kernels of liblddl_amd.so on torch's current stream.
+    Two-source row addressing: row r < n_a is row r of the first table, else row r - n_a of the
+    second (include/lddl_amd.h, row movement)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def bin_stable(self, pb, bin_size, nbins):
+        """(perm int64[n], counts int64[nbins]): stable regroup of the rows by
+        bin_id = min((num_tokens - 1) // bin_size, nbins - 1) (binning.py:63-93)."""
+        from .output import bin_stable
+        perm, _, cnt = bin_stable(self.ctx, tok_off=pb.tok_off, bin_size=bin_size, nbins=nbins,
+                                  with_bin_id=False)
+        return perm, cnt
+
+    def scan(self, x):
+        from .output import scan
+        return scan(self.ctx, x)
+
+    def expand(self, src, seg, seg_off, dev):
+        """int64 row list of the segment table seg[k] = (start, stride, direct) over outputs
+        seg_off[k] .. seg_off[k+1] (lddl_expand_segments)."""
+        total = int(seg_off[-1])
+        out = _alloc(total, torch.int64, dev)
+        if total:
+            d_seg = torch.from_numpy(np.ascontiguousarray(seg, np.int64)).to(dev)
+            d_off = torch.from_numpy(np.ascontiguousarray(seg_off, np.int64)).to(dev)
+            check(lib.lddl_expand_segments(_stream(), _ptr(src), _ptr(d_seg), _ptr(d_off),
+                                           len(seg), total, _ptr(out)))
+        return out
+
+    def take(self, a, n_a, b, rows, dtype=None):
+        out = _alloc(rows.numel(), a.dtype, a.device)
+        check(lib.lddl_take(_stream(), _ptr(a), int(n_a), _ptr(b), a.element_size(), _ptr(rows),
+                            rows.numel(), _ptr(out)))
+        return out
+
+    def ragged_offsets(self, off_a, n_a, off_b, rows):
+        out = torch.empty(rows.numel() + 1, dtype=torch.int64, device=off_a.device)
+        check(lib.lddl_ragged_offsets(self.ctx.handle, _stream(), _ptr(off_a), int(n_a),
+                                      _ptr(off_b), _ptr(rows), rows.numel(), _ptr(out)))
+        return out
+
+    def gather(self, a, off_a, n_a, b, off_b, rows, dst_off, total):
+        out = _alloc(total, a.dtype, a.device)
+        if rows.numel():
+            check(lib.lddl_gather_ragged(_stream(), _ptr(a), _ptr(off_a), int(n_a), _ptr(b),
+                                         _ptr(off_b), a.element_size(), _ptr(rows), rows.numel(),
+                                         _ptr(dst_off), _ptr(out)))
+        return out
+
+    def meta_pack(self, pb, rows):
+        out = _alloc(4 * rows.numel(), torch.int32, pb.tok_off.device)
+        check(lib.lddl_pairs_meta_pack(_stream(), _ptr(pb.tok_off), _ptr(pb.len_a),
+                                       _ptr(pb.is_random_next), _ptr(pb.pos_off), _ptr(rows),
+                                       rows.numel(), _ptr(out)))
+        return out
+
+    def meta_unpack(self, meta):
+        n = meta.numel() // 4
+        dev = meta.device
+        ntok, nmask = _alloc(n, torch.int64, dev), _alloc(n, torch.int64, dev)
+        len_a, is_rn = _alloc(n, torch.int32, dev), _alloc(n, torch.uint8, dev)
+        check(lib.lddl_pairs_meta_unpack(_stream(), _ptr(meta), n, _ptr(ntok), _ptr(len_a),
+                                         _ptr(is_rn), _ptr(nmask)))
+        return ntok, len_a, is_rn, nmask
 
 
-def _group_sums(v, sizes):
-    """Per-group sums of consecutive runs of `v` (host list); sizes = run lengths."""
-    if not len(sizes):
-        return []
-    c = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-    if v.numel() == 0:
-        return [0] * len(sizes)
-    s = torch.cat([torch.zeros(1, dtype=torch.int64, device=v.device), torch.cumsum(v, 0)])
-    return (s[torch.from_numpy(c[1:]).to(v.device)] -
-            s[torch.from_numpy(c[:-1]).to(v.device)]).cpu().tolist()
+def _host_at(ops, off, idx):
+    """off[idx] for a few host indices (one small device take + copy)."""
+    if not len(idx):
+        return np.zeros(0, np.int64)
+    i = torch.from_numpy(np.asarray(idx, np.int64)).to(off.device)
+    return ops.take(off, off.numel(), None, i).cpu().numpy()
 
 
 # ---- result ----------------------------------------------------------------------------------
 @dataclass
 class BalancedBins:
-    """One rank's share after the balance, bin-major.
+    """One rank's share of one batch after the balance, bin-major.
 
     Output row i is row `rows[i]` of `table` (rows None = identity, i.e. the table itself is
     bin-major). Bin b is output rows [bin_off[b], bin_off[b+1]); inside a bin the rank's shards
-    follow each other: shard shards[m] holds shard_counts[m, b] of them."""
+    follow each other: shard shards[m] holds shard_counts[m, b] of them, in global order."""
     table: PairBatch
     rows: torch.Tensor
     bin_off: np.ndarray
@@ -155,216 +181,194 @@ class BalancedBins:
     shard_counts: np.ndarray = None
     n_tokens: int = 0              # sum of len(A) + len(B) over the output rows
     moved_rows: int = 0            # rows received from other ranks
-    all_shard_counts: np.ndarray = None  # int64[S, B]: every shard's samples per bin (all ranks)
+    all_shard_counts: np.ndarray = None  # int64[S, B]: this batch's rows per shard and bin (all ranks)
 
     @property
     def n_rows(self):
         return int(self.bin_off[-1])
 
-    @property
-    def tokens(self):  # materialised token ids in output order (tests / diagnostics)
-        return self.materialize().table.tokens
-
-    def shard_rows(self, m):
-        """Output rows of this rank's m-th shard, bin after bin (host int64), and their bins."""
-        idx, bins = [], []
-        for b in range(len(self.bin_off) - 1):
-            a = int(self.bin_off[b] + self.shard_counts[:m, b].sum())
-            c = int(self.shard_counts[m, b])
-            idx.append(np.arange(a, a + c, dtype=np.int64))
-            bins.append(np.full(c, b, np.int64))
-        return np.concatenate(idx), np.concatenate(bins)
+    def shard_range(self, m, b):
+        """Output rows [r0, r1) of this rank's m-th shard in bin b."""
+        r0 = int(self.bin_off[b] + self.shard_counts[:m, b].sum())
+        return r0, r0 + int(self.shard_counts[m, b])
 
     def bin_ids(self):
-        """int64[n_rows] bin id of every output row (device)."""
-        dev = self.table.tok_off.device
-        nb = len(self.bin_off) - 1
-        return torch.repeat_interleave(torch.arange(nb, dtype=torch.int64, device=dev),
-                                       torch.from_numpy(np.diff(self.bin_off)).to(dev),
-                                       output_size=self.n_rows)
+        """int64[n_rows] bin id of every output row (host)."""
+        return np.repeat(np.arange(len(self.bin_off) - 1, dtype=np.int64), np.diff(self.bin_off))
 
-    def materialize(self, ops=None):
+    def materialize(self, ops):
         """The contiguous bin-major table (copies only if `rows` is not the identity)."""
         if self.rows is None:
             return self
-        ops = ops or HipOps(None)
-        t = _gather_table(ops, self.table, self.rows)
+        t = _gather_table(ops, self.table, None, self.rows)
         return BalancedBins(t, None, self.bin_off, self.shards, self.shard_counts, self.n_tokens,
                             self.moved_rows, self.all_shard_counts)
 
 
-def _gather_table(ops, pb, rows):
-    """Rows `rows` of PairBatch pb as a new contiguous PairBatch."""
-    dev = pb.tok_off.device
-    ntok = (pb.tok_off[1:] - pb.tok_off[:-1]).index_select(0, rows)
-    tok_off = ops.scan(ntok.contiguous())
-    n_tok = int(tok_off[-1].item())
-    tokens = ops.gather_into(pb.tokens, pb.tok_off, rows, tok_off, _alloc(n_tok, pb.tokens.dtype, dev))
-    out = PairBatch(tokens, tok_off, pb.len_a.index_select(0, rows),
-                    pb.is_random_next.index_select(0, rows))
-    if pb.pos is not None:
-        nm = (pb.pos_off[1:] - pb.pos_off[:-1]).index_select(0, rows)
-        pos_off = ops.scan(nm.contiguous())
-        n_m = int(pos_off[-1].item())
-        out.pos = ops.gather_into(pb.pos, pb.pos_off, rows, pos_off, _alloc(n_m, pb.pos.dtype, dev))
-        out.labels = ops.gather_into(pb.labels, pb.pos_off, rows, pos_off,
-                                     _alloc(n_m, pb.labels.dtype, dev))
-        out.pos_off = pos_off
+def _gather_table(ops, pa, pr, rows):
+    """Rows `rows` of the virtual concatenation [pa | pr] (pr may be None) as one contiguous
+    PairBatch: every output row copied once, from whichever table holds it."""
+    dev = pa.tok_off.device
+    na = pa.n_pairs
+
+    def col(xa, xr):
+        return ops.take(xa, na, xr, rows)
+
+    def ragged(xa, oa, xr, orr):
+        off = ops.ragged_offsets(oa, na, orr, rows)
+        n = int(off[-1].item())
+        return ops.gather(xa, oa, na, xr, orr, rows, off, n), off, n
+    pr_ = pr if pr is not None else PairBatch(None, None, None, None)
+    tokens, tok_off, _ = ragged(pa.tokens, pa.tok_off, pr_.tokens, pr_.tok_off)
+    out = PairBatch(tokens, tok_off, col(pa.len_a, pr_.len_a),
+                    col(pa.is_random_next, pr_.is_random_next))
+    if pa.pos is not None:
+        out.pos, out.pos_off, n_m = ragged(pa.pos, pa.pos_off, pr_.pos, pr_.pos_off)
+        out.labels = ops.gather(pa.labels, pa.pos_off, na, pr_.labels, pr_.pos_off, rows,
+                                out.pos_off, n_m)
         out.n_masked = n_m
+    assert out.tokens.device == dev
     return out
 
 
 # ---- per-rank phases -------------------------------------------------------------------------
 class RankBalance:
-    """One rank's part of the balance: bin (local), plan (replicated), pack / unpack around the
-    two exchange rounds (row metadata, then the ragged columns), regroup."""
+    """One rank's part of one batch: bin (local), plan (replicated), pack / unpack around the two
+    exchange rounds (row metadata, then the ragged columns), regroup."""
 
     def __init__(self, ops, pb, bin_size, nbins, rank, world, num_shards=None):
         self.ops, self.pb, self.nbins = ops, pb, nbins
         self.me, self.W = rank, world
         self.S = world if num_shards is None else int(num_shards)
         self.dev = pb.tok_off.device
-        self.ntok = pb.tok_off[1:] - pb.tok_off[:-1]
         self.masking = pb.pos is not None
-        self.nmask = (pb.pos_off[1:] - pb.pos_off[:-1]) if self.masking else None
-        self.perm, self.local_counts = ops.bin_stable((self.ntok + 3).to(torch.int32), bin_size,
-                                                      nbins)
+        if self.masking:
+            assert pb.pos.element_size() == 2 and pb.labels.element_size() == 4
+        assert pb.tokens.element_size() == 4
+        self.perm, self.local_counts = ops.bin_stable(pb, bin_size, nbins)
 
     # plan ----------------------------------------------------------------------------------
-    def set_plan(self, counts):
-        W, me, B = self.W, self.me, self.nbins
+    def set_plan(self, counts, prior):
+        """counts int64[W, B]: every rank's rows per bin in this batch; prior int64[B]: rows of
+        each bin in earlier batches (all ranks)."""
+        W, me, B, S = self.W, self.me, self.nbins, self.S
         self.counts = np.asarray(counts, np.int64)
-        self.target, self.send, self.first = plan_exchange(self.counts, self.S)
-        bin0 = np.concatenate([[0], np.cumsum(self.counts[me])])
-        starts, lens = [], []
+        first, n = deal_runs(batch_start(prior, self.counts), self.counts, S)  # [W, B, S]
+        owner = shard_owner(S, W)
+        self.shards = [int(s) for s in np.nonzero(owner == me)[0]]
+        mine = np.asarray(self.shards, np.int64)
+        bin0 = np.concatenate([[0], np.cumsum(self.counts[me])])[:-1]
+        # rows leaving this rank: destination-major, then bin, then shard (each run strided by S)
+        seg, lens = [], []
         self.send_rows_per_dst = [0] * W
-        for k in range(W):  # rows leaving this rank, destination-major then bin
+        for k in range(W):
             if k == me:
                 continue
+            ks = np.nonzero(owner == k)[0]
             for b in range(B):
-                c = int(self.send[me, k, b])
-                if c:
-                    starts.append(int(bin0[b] + self.first[me, k, b]))
-                    lens.append(c)
-                    self.send_rows_per_dst[k] += c
-        self.send_idx = _expand(self.perm, starts, lens, self.dev)
-        self.recv_rows_per_src = [0 if j == me else int(self.send[j, me].sum()) for j in range(W)]
+                for s in ks:
+                    c = int(n[me, b, s])
+                    if c:
+                        seg.append((int(bin0[b] + first[me, b, s]), S, 0))
+                        lens.append(c)
+                        self.send_rows_per_dst[k] += c
+        self._send_seg = (seg, lens)
+        self.n_send = sum(self.send_rows_per_dst)
+        # rows arriving from rank j: j's runs of (bin, my shard), in j's send order
+        self.recv_rows_per_src = [0 if j == me else int(n[j][:, mine].sum()) for j in range(W)]
         self.n_recv = sum(self.recv_rows_per_src)
-        # output order over the virtual source [local rows (via perm) | received rows]
+        recv0 = np.concatenate([[0], np.cumsum(self.recv_rows_per_src)])
+        # output order over [own rows (through perm) | received rows]: bin, my shard, source rank
         n_local = self.pb.n_pairs
-        src0 = np.concatenate([[0], np.cumsum(self.recv_rows_per_src)])
-        starts, lens = [], []
+        within = {}  # (j, b, s) -> offset of the run inside j's rows for me
+        for j in range(W):
+            if j == me:
+                continue
+            o = 0
+            for b in range(B):
+                for s in mine:
+                    within[(j, b, int(s))] = o
+                    o += int(n[j, b, s])
+        seg, lens = [], []
         for b in range(B):
-            for j in range(W):
-                c = int(self.send[j, me, b])
-                if not c:
-                    continue
-                if j == me:
-                    starts.append(int(bin0[b] + self.first[me, me, b]))
-                else:
-                    starts.append(int(n_local + src0[j] + self.send[j, me, :b].sum()))
-                lens.append(c)
-        self._order_src = (starts, lens)
-        self.bin_off = np.concatenate([[0], np.cumsum(self.target[me])]).astype(np.int64)
-        owner = shard_owner(self.S, W)
-        self.shards = [int(s) for s in np.nonzero(owner == me)[0]]
-        self.all_shard_counts = shard_targets(self.counts, self.S)
-        self.shard_counts = self.all_shard_counts[self.shards]
+            for s in mine:
+                for j in range(W):
+                    c = int(n[j, b, s])
+                    if not c:
+                        continue
+                    if j == me:
+                        seg.append((int(bin0[b] + first[me, b, s]), S, 0))
+                    else:
+                        seg.append((int(n_local + recv0[j] + within[(j, b, int(s))]), 1, 1))
+                    lens.append(c)
+        self._order_seg = (seg, lens)
+        per_bin = n[:, :, mine].sum(axis=(0, 2)) if len(mine) else np.zeros(B, np.int64)
+        self.bin_off = np.concatenate([[0], np.cumsum(per_bin)]).astype(np.int64)
+        self.batch_shard_counts = n.sum(0).T.copy()  # [S, B]
+        self.shard_counts = self.batch_shard_counts[mine] if len(mine) else np.zeros((0, B), np.int64)
+        self.send_idx = self._expand(self._send_seg)
+
+    def _expand(self, segs):
+        seg, lens = segs
+        seg_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        arr = np.asarray(seg, np.int64).reshape(-1, 3)
+        return self.ops.expand(self.perm, arr, seg_off, self.dev)
 
     # round 1: row metadata -----------------------------------------------------------------
     def pack_meta(self):
-        r = self.send_idx
-        cols = [self.ntok.index_select(0, r), self.pb.len_a.index_select(0, r).long(),
-                self.pb.is_random_next.index_select(0, r).long(),
-                self.nmask.index_select(0, r) if self.masking else torch.zeros_like(r)]
-        meta = torch.stack(cols, 1).reshape(-1) if r.numel() else torch.zeros(
-            0, dtype=torch.int64, device=self.dev)
+        meta = self.ops.meta_pack(self.pb, self.send_idx)
         return meta, [4 * x for x in self.send_rows_per_dst], [4 * x for x in self.recv_rows_per_src]
 
     def unpack_meta(self, rmeta):
-        self.rmeta = rmeta.view(-1, 4)
+        ntok, len_a, is_rn, nmask = self.ops.meta_unpack(rmeta)
+        self.rt = PairBatch(None, self.ops.scan(ntok), len_a, is_rn)
+        if self.masking:
+            self.rt.pos_off = self.ops.scan(nmask)
 
     # round 2: ragged columns ---------------------------------------------------------------
-    def _ragged(self, data, data_off, sizes, recv_sizes):
+    def _ragged(self, data, data_off, recv_off):
         r = self.send_idx
-        off = self.ops.scan(sizes.index_select(0, r).contiguous())
-        n = int(off[-1].item()) if r.numel() else 0
-        buf = self.ops.gather_into(data, data_off, r, off, _alloc(n, data.dtype, self.dev))
-        ss = _group_sums(sizes.index_select(0, r), self.send_rows_per_dst)
-        rs = _group_sums(recv_sizes, self.recv_rows_per_src)
+        off = self.ops.ragged_offsets(data_off, self.pb.n_pairs, None, r)
+        cut = np.concatenate([[0], np.cumsum(self.send_rows_per_dst)])
+        rcut = np.concatenate([[0], np.cumsum(self.recv_rows_per_src)])
+        sb = _host_at(self.ops, off, cut)
+        rb = _host_at(self.ops, recv_off, rcut)
+        buf = self.ops.gather(data, data_off, self.pb.n_pairs, None, None, r, off, int(sb[-1]))
+        ss, rs = np.diff(sb).tolist(), np.diff(rb).tolist()
         if buf.element_size() == 2:  # RCCL has no 16-bit integer type: move the bytes
-            return buf.view(torch.uint8), [2 * x for x in ss], [2 * x for x in rs]
+            b8 = buf.view(torch.uint8) if buf.numel() else torch.zeros(0, dtype=torch.uint8,
+                                                                       device=buf.device)
+            return b8, [2 * x for x in ss], [2 * x for x in rs]
         return buf, ss, rs
 
     def pack_data(self):
-        out = [self._ragged(self.pb.tokens, self.pb.tok_off, self.ntok, self.rmeta[:, 0])]
+        out = [self._ragged(self.pb.tokens, self.pb.tok_off, self.rt.tok_off)]
         if self.masking:
-            out.append(self._ragged(self.pb.pos, self.pb.pos_off, self.nmask, self.rmeta[:, 3]))
-            out.append(self._ragged(self.pb.labels, self.pb.pos_off, self.nmask, self.rmeta[:, 3]))
+            out.append(self._ragged(self.pb.pos, self.pb.pos_off, self.rt.pos_off))
+            out.append(self._ragged(self.pb.labels, self.pb.pos_off, self.rt.pos_off))
         return out
 
     # regroup -------------------------------------------------------------------------------
     def finish(self, recvs):
-        n_local = self.pb.n_pairs
-        if self.n_recv == 0 and sum(self.send_rows_per_dst) == 0:
-            # every row stays (always at world size 1): the output is the local bin order itself
-            return BalancedBins(self.pb, self.perm, self.bin_off, self.shards, self.shard_counts,
-                                int(self.pb.tokens.numel()), 0, self.all_shard_counts)
-        src = torch.cat([self.perm, torch.arange(n_local, n_local + self.n_recv, dtype=torch.int64,
-                                                  device=self.dev)])
-        order = _expand(src, *self._order_src, self.dev)
-        ntok_v = torch.cat([self.ntok, self.rmeta[:, 0]])
-        n_tokens = int(ntok_v.index_select(0, order).sum().item()) if order.numel() else 0
-        bb = BalancedBins(self.pb, order, self.bin_off, self.shards, self.shard_counts, n_tokens,
-                          self.n_recv, self.all_shard_counts)
+        order = self._expand(self._order_seg)
+        kw = dict(bin_off=self.bin_off, shards=self.shards, shard_counts=self.shard_counts,
+                  moved_rows=self.n_recv, all_shard_counts=self.batch_shard_counts)
         if self.n_recv == 0:
-            return bb  # nothing arrived: a row order over the rank's own table, no copy
-        # received rows as a PairBatch, then one materialisation of the two sources
-        rtok = recvs[0]
-        rt = PairBatch(rtok, self.ops.scan(self.rmeta[:, 0].contiguous()),
-                       self.rmeta[:, 1].to(torch.int32), self.rmeta[:, 2].to(torch.uint8))
+            # nothing arrived: a row order over the rank's own table, no copy
+            if self.n_send == 0:
+                n_tokens = int(self.pb.tokens.numel())
+            else:
+                n_tokens = int(_host_at(self.ops, self.ops.ragged_offsets(
+                    self.pb.tok_off, self.pb.n_pairs, None, order), [order.numel()])[0])
+            return BalancedBins(self.pb, order, n_tokens=n_tokens, **kw)
+        rt = self.rt
+        rt.tokens = recvs[0]
         if self.masking:
-            rt.pos = recvs[1].view(self.pb.pos.dtype)
-            rt.labels = recvs[2]
-            rt.pos_off = self.ops.scan(self.rmeta[:, 3].contiguous())
-        return BalancedBins(_gather_two(self.ops, self.pb, rt, order), None, self.bin_off,
-                            self.shards, self.shard_counts, n_tokens, self.n_recv,
-                            self.all_shard_counts)
-
-
-def _gather_two(ops, pa, pr, order):
-    """Rows `order` of the virtual concatenation [pa | pr] as one contiguous PairBatch: each
-    output row is copied once, from whichever table holds it."""
-    dev = pa.tok_off.device
-    na = pa.n_pairs
-    is_a = order < na
-    ia = torch.nonzero(is_a).reshape(-1)
-    ir = torch.nonzero(~is_a).reshape(-1)
-    ra, rr = order.index_select(0, ia), order.index_select(0, ir) - na
-
-    def per_row(xa, xr):
-        return torch.cat([xa, xr]).index_select(0, order)
-
-    ntok = per_row(pa.tok_off[1:] - pa.tok_off[:-1], pr.tok_off[1:] - pr.tok_off[:-1])
-    tok_off = ops.scan(ntok.contiguous())
-    tokens = _alloc(int(tok_off[-1].item()), pa.tokens.dtype, dev)
-    ops.gather_into(pa.tokens, pa.tok_off, ra, tok_off.index_select(0, ia), tokens)
-    ops.gather_into(pr.tokens, pr.tok_off, rr, tok_off.index_select(0, ir), tokens)
-    out = PairBatch(tokens, tok_off, per_row(pa.len_a, pr.len_a),
-                    per_row(pa.is_random_next, pr.is_random_next))
-    if pa.pos is not None:
-        nm = per_row(pa.pos_off[1:] - pa.pos_off[:-1], pr.pos_off[1:] - pr.pos_off[:-1])
-        pos_off = ops.scan(nm.contiguous())
-        n_m = int(pos_off[-1].item())
-        pos = _alloc(n_m, pa.pos.dtype, dev)
-        lab = _alloc(n_m, pa.labels.dtype, dev)
-        da, dr = pos_off.index_select(0, ia), pos_off.index_select(0, ir)
-        ops.gather_into(pa.pos, pa.pos_off, ra, da, pos)
-        ops.gather_into(pr.pos, pr.pos_off, rr, dr, pos)
-        ops.gather_into(pa.labels, pa.pos_off, ra, da, lab)
-        ops.gather_into(pr.labels, pr.pos_off, rr, dr, lab)
-        out.pos, out.labels, out.pos_off, out.n_masked = pos, lab, pos_off, n_m
-    return out
+            rt.pos = recvs[1].view(self.pb.pos.dtype) if recvs[1].numel() else torch.zeros(
+                0, dtype=self.pb.pos.dtype, device=self.dev)
+            rt.labels = recvs[2].view(self.pb.labels.dtype)
+        t = _gather_table(self.ops, self.pb, rt, order)
+        return BalancedBins(t, None, n_tokens=int(t.tokens.numel()), **kw)
 
 
 # ---- drivers ---------------------------------------------------------------------------------
@@ -376,33 +380,50 @@ def _a2a(payload, group):
     return recv
 
 
+class StreamBalancer:
+    """The balance of a stream of batches over every rank of `group` into `num_shards` (default:
+    world size) per-bin shards. Call `step(pb)` once per batch on every rank, in the same order
+    (a rank without rows passes an empty PairBatch); `all_shard_counts` is the layout so far
+    (every shard N or N+1 rows per bin after every step)."""
+
+    def __init__(self, ctx, bin_size, nbins, num_shards=None, group=None, ops=None):
+        self.multi = dist.is_initialized() and dist.get_world_size(group) > 1
+        self.W = dist.get_world_size(group) if self.multi else 1
+        self.me = dist.get_rank(group) if self.multi else 0
+        self.S = self.W if num_shards is None else int(num_shards)
+        self.bin_size, self.nbins, self.group = bin_size, nbins, group
+        self.ops = ops or HipOps(ctx)
+        self.prior = np.zeros(nbins, np.int64)
+        self.all_shard_counts = np.zeros((self.S, nbins), np.int64)
+
+    def step(self, pb, timings=None):
+        def mark(name):
+            if timings is not None:
+                if pb.tok_off.is_cuda:
+                    torch.cuda.synchronize()
+                timings[name] = time.perf_counter()
+        mark('start')
+        rb = RankBalance(self.ops, pb, self.bin_size, self.nbins, self.me, self.W, self.S)
+        mark('bin')
+        counts = gather_counts(rb.local_counts, self.group)
+        rb.set_plan(counts, self.prior)
+        mark('plan')
+        if self.multi:
+            rb.unpack_meta(_a2a(rb.pack_meta(), self.group))
+            recvs = [_a2a(p, self.group) for p in rb.pack_data()]
+        else:
+            recvs = []
+        mark('exchange')
+        out = rb.finish(recvs)
+        mark('regroup')
+        self.prior += counts.sum(0)
+        self.all_shard_counts += rb.batch_shard_counts
+        return out
+
+
 def balance(ctx, pb, bin_size, nbins, group=None, timings=None, num_shards=None, ops=None):
-    """Balance the PairBatch `pb` of every rank of `group` into `num_shards` (default: world
-    size) per-bin shards of N or N+1 samples; collective over torch.distributed (RCCL for cuda
-    tensors). timings: optional dict filled with synchronised per-phase wall times."""
-    def mark(name):
-        if timings is not None:
-            if pb.tok_off.is_cuda:
-                torch.cuda.synchronize()
-            timings[name] = time.perf_counter()
-    mark('start')
-    multi = dist.is_initialized() and dist.get_world_size(group) > 1
-    W = dist.get_world_size(group) if multi else 1
-    me = dist.get_rank(group) if multi else 0
-    rb = RankBalance(ops or HipOps(ctx), pb, bin_size, nbins, me, W, num_shards)
-    mark('bin')
-    rb.set_plan(gather_counts(rb.local_counts, group))
-    mark('counts')
-    if multi:
-        rb.unpack_meta(_a2a(rb.pack_meta(), group))
-        recvs = [_a2a(p, group) for p in rb.pack_data()]
-    else:
-        rb.unpack_meta(torch.zeros(0, dtype=torch.int64, device=rb.dev))
-        recvs = []
-    mark('exchange')
-    out = rb.finish(recvs)
-    mark('regroup')
-    return out
+    """Balance one batch `pb` of every rank of `group` (a one-step StreamBalancer)."""
+    return StreamBalancer(ctx, bin_size, nbins, num_shards, group, ops).step(pb, timings)
 
 
 def _local_a2a(payloads, k):
@@ -414,17 +435,29 @@ def _local_a2a(payloads, k):
     return torch.cat(pieces) if pieces else None
 
 
+def stream_virtual(ops, batches, bin_size, nbins, num_shards=None):
+    """The same balance over W virtual ranks held by one process: batches[t][r] = rank r's table
+    of batch t. Returns outs[t][r] (BalancedBins) — the plan, pack and regroup of StreamBalancer,
+    with the exchange done by slicing."""
+    W = len(batches[0])
+    S = W if num_shards is None else int(num_shards)
+    prior = np.zeros(nbins, np.int64)
+    outs = []
+    for pbs in batches:
+        rbs = [RankBalance(ops, pb, bin_size, nbins, r, W, S) for r, pb in enumerate(pbs)]
+        counts = np.stack([rb.local_counts.cpu().numpy() for rb in rbs])
+        for rb in rbs:
+            rb.set_plan(counts, prior)
+        metas = [rb.pack_meta() for rb in rbs]
+        for k, rb in enumerate(rbs):
+            rb.unpack_meta(_local_a2a(metas, k))
+        datas = [rb.pack_data() for rb in rbs]
+        outs.append([rb.finish([_local_a2a([d[c] for d in datas], k)
+                                for c in range(len(datas[k]))]) for k, rb in enumerate(rbs)])
+        prior += counts.sum(0)
+    return outs
+
+
 def balance_virtual(ops, pbs, bin_size, nbins, num_shards=None):
-    """The same balance over W virtual ranks held by one process (pbs[r] = rank r's table):
-    the plan, pack and regroup of `balance`, with the exchange done by slicing."""
-    W = len(pbs)
-    rbs = [RankBalance(ops, pb, bin_size, nbins, r, W, num_shards) for r, pb in enumerate(pbs)]
-    counts = np.stack([rb.local_counts.cpu().numpy() for rb in rbs])
-    for rb in rbs:
-        rb.set_plan(counts)
-    metas = [rb.pack_meta() for rb in rbs]
-    for k, rb in enumerate(rbs):
-        rb.unpack_meta(_local_a2a(metas, k))
-    datas = [rb.pack_data() for rb in rbs]
-    return [rb.finish([_local_a2a([d[c] for d in datas], k) for c in range(len(datas[k]))])
-            for k, rb in enumerate(rbs)]
+    """One batch over W virtual ranks (pbs[r] = rank r's table)."""
+    return stream_virtual(ops, [pbs], bin_size, nbins, num_shards)[0]

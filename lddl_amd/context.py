@@ -25,6 +25,28 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+# The library's temporaries come from PyTorch's caching allocator (lddl_ctx_set_allocator), so
+# one pool owns HBM: no second cache of hipMalloc blocks beside torch's. `user` carries the
+# device index. LDDL_ARENA=own keeps the library's own block cache instead (A/B only).
+_ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p)
+_FREE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)
+
+
+def _torch_alloc(nbytes, stream, user):
+    try:
+        return torch.cuda.caching_allocator_alloc(int(nbytes), device=int(user or 0),
+                                                  stream=int(stream or 0))
+    except Exception:  # out of memory: the library reports hipErrorOutOfMemory
+        return None
+
+
+def _torch_free(p, stream, user):
+    torch.cuda.caching_allocator_delete(int(p))
+
+
+_TORCH_ALLOC, _TORCH_FREE = _ALLOC_FN(_torch_alloc), _FREE_FN(_torch_free)
+
+
 class Context:
     """Tokenizer tables resident in HBM.
 
@@ -50,6 +72,9 @@ class Context:
         check(lib.lddl_ctx_create(self.device.index, table.ctypes.data, len(table), vocab,
                                   len(vocab), ctypes.byref(h)))
         self._h = h
+        if os.environ.get('LDDL_ARENA') != 'own':
+            check(lib.lddl_ctx_set_allocator(h, _TORCH_ALLOC, _TORCH_FREE,
+                                             ctypes.c_void_p(self.device.index)))
         vs = ctypes.c_int32()
         sp = (ctypes.c_int32 * 5)()
         mp = ctypes.c_int32()

@@ -19,15 +19,37 @@ namespace lddl {
 // waits on the event first). A batch-per-step workload therefore allocates only in its first
 // step. (The stream-ordered HIP pool that this replaces showed 0.4-2 s hipMallocAsync calls
 // once torch's caching allocator held a large share of HBM.)
+//
+// With an external allocator set (lddl_ctx_set_allocator: the host hands in its own device
+// allocator, e.g. PyTorch's caching allocator), blocks come from and go straight back to it and
+// nothing is cached here, so one pool owns HBM.
 class DevArena {
  public:
+  typedef void* (*AllocFn)(size_t bytes, void* stream, void* user);
+  typedef void (*FreeFn)(void* p, void* stream, void* user);
   struct Block {
     void* p = nullptr;
     size_t size = 0;
     hipEvent_t ev = nullptr;
     hipStream_t st = nullptr;
+    bool ext = false;  // from the external allocator
   };
+  void set_external(AllocFn a, FreeFn f, void* user) {
+    trim();
+    std::lock_guard<std::mutex> g(mu_);
+    alloc_ = a;
+    free_fn_ = f;
+    user_ = user;
+  }
   hipError_t take(size_t bytes, hipStream_t st, Block& out) {
+    if (alloc_) {
+      out = Block{};
+      out.size = bytes ? bytes : 16;
+      out.p = alloc_(out.size, (void*)st, user_);
+      out.ext = true;
+      out.st = st;
+      return out.p ? hipSuccess : hipErrorOutOfMemory;
+    }
     const size_t want = round_up(bytes);
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -56,6 +78,10 @@ class DevArena {
   }
   void give(Block b, hipStream_t st) {
     if (!b.p) return;
+    if (b.ext) {  // stream-ordered external pool: reusable by later work on `st`
+      if (free_fn_) free_fn_(b.p, (void*)st, user_);
+      return;
+    }
     if (!b.ev) (void)hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
     if (b.ev) (void)hipEventRecord(b.ev, st);
     b.st = st;
@@ -83,6 +109,21 @@ class DevArena {
   }
   std::mutex mu_;
   std::vector<Block> free_;
+  AllocFn alloc_ = nullptr;
+  FreeFn free_fn_ = nullptr;
+  void* user_ = nullptr;
+};
+
+// A temporary from the arena for the duration of one C-ABI call (returned on `st`).
+struct ArenaTmp {
+  DevArena* a;
+  hipStream_t st;
+  DevArena::Block b{};
+  ArenaTmp(DevArena* arena, hipStream_t stream) : a(arena), st(stream) {}
+  hipError_t take(size_t bytes) { return a->take(bytes, st, b); }
+  template <typename T>
+  T* as() const { return static_cast<T*>(b.p); }
+  ~ArenaTmp() { a->give(b, st); }
 };
 }  // namespace lddl
 

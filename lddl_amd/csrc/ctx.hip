@@ -211,3 +211,12 @@ extern "C" int lddl_ctx_render_table(const lddl_ctx* c, const uint8_t** d_bytes,
   *d_off = c->d_render_off;
   return 0;
 }
+
+extern "C" int lddl_ctx_set_allocator(lddl_ctx* c, lddl_alloc_fn alloc_fn, lddl_free_fn free_fn,
+                                      void* user) {
+  if (!c) LDDL_FAIL(-1, "null ctx");
+  if ((alloc_fn == nullptr) != (free_fn == nullptr))
+    LDDL_FAIL(-1, "set both allocator callbacks or neither");
+  c->arena.set_external(alloc_fn, free_fn, user);
+  return 0;
+}

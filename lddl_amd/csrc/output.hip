@@ -105,7 +105,16 @@ __global__ void __launch_bounds__(kBinThreads) bin_partitions_kernel(
 // ---- stable sort by bin of one large segment: tiles of kBinTile rows, one wavefront each ----
 constexpr int kBinTile = 2048;
 
-__global__ void __launch_bounds__(64) bin_tile_hist_kernel(const int32_t* __restrict__ num_tokens,
+// num_tokens of row r: an int32 column, or (tok_off given) the pair's token count + 3
+struct NumTok {
+  const int32_t* nt;
+  const int64_t* tok_off;
+  __device__ int32_t operator[](int64_t r) const {
+    return nt ? nt[r] : (int32_t)(tok_off[r + 1] - tok_off[r] + 3);
+  }
+};
+
+__global__ void __launch_bounds__(64) bin_tile_hist_kernel(NumTok num_tokens,
                                                            int64_t n, int32_t bin_size,
                                                            int32_t nbins, int64_t n_tiles,
                                                            int64_t* __restrict__ tile_counts) {
@@ -121,7 +130,7 @@ __global__ void __launch_bounds__(64) bin_tile_hist_kernel(const int32_t* __rest
 }
 
 __global__ void __launch_bounds__(64) bin_tile_scatter_kernel(
-    const int32_t* __restrict__ num_tokens, int64_t n, int32_t bin_size, int32_t nbins,
+    NumTok num_tokens, int64_t n, int32_t bin_size, int32_t nbins,
     int32_t nbits, int64_t n_tiles, const int64_t* __restrict__ tile_base,
     int64_t* __restrict__ perm, int64_t* __restrict__ bin_id) {
   __shared__ int64_t s_run[kMaxBinsLds];
@@ -146,7 +155,7 @@ __global__ void __launch_bounds__(64) bin_tile_scatter_kernel(
     if (in) {
       const int64_t dst = base + (int)popc_below(match);
       perm[dst] = r;
-      bin_id[dst] = b;
+      if (bin_id) bin_id[dst] = b;
       if ((match & below) == 0) s_run[b] = base + __popcll(match);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -209,7 +218,9 @@ __device__ void joined_write(const RenderArgs& R, const int32_t* ids, int64_t n,
 
 __global__ void __launch_bounds__(256) render_lengths_kernel(RenderArgs R, int64_t* a_len,
                                                              int64_t* b_len, int64_t* l_len,
-                                                             int64_t* n_pos) {
+                                                             int64_t* n_pos, const uint8_t* is_rn,
+                                                             uint16_t* num_tokens_out,
+                                                             uint8_t* is_rn_out) {
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R.n_rows) return;
   const int64_t q = R.rows ? R.rows[row] : row;
@@ -228,6 +239,9 @@ __global__ void __launch_bounds__(256) render_lengths_kernel(RenderArgs R, int64
     b_len[row] = lb;
     if (l_len) l_len[row] = ll;
     if (n_pos) n_pos[row] = 128 + 2 * np;
+    // the row's num_tokens / is_random_next columns in output order
+    if (num_tokens_out) num_tokens_out[row] = (uint16_t)(t1 - t0 + 3);
+    if (is_rn_out) is_rn_out[row] = is_rn[q];
   }
 }
 
@@ -274,10 +288,19 @@ __global__ void __launch_bounds__(256) render_write_kernel(RenderArgs R, const i
   }
 }
 
-// ---- ragged row gather (sample exchange packing) ---------------------------------------------
+// ---- row movement of the load balance (lddl_amd/balance.py) ----------------------------------
+// Rows are addressed over two sources: row r < n_a is row r of source A, else row r - n_a of
+// source B (a rank's own table and the rows it received), so the exchange never concatenates.
 template <typename T>
-__global__ void __launch_bounds__(256) gather_ragged_kernel(const T* __restrict__ src,
-                                                            const int64_t* __restrict__ src_off,
+struct Src2 {
+  const T* a;
+  const T* b;
+  int64_t n_a;
+  __device__ const T* at(int64_t r) const { return r < n_a ? a + r : b + (r - n_a); }
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) gather_ragged_kernel(Src2<T> src, Src2<int64_t> off,
                                                             const int64_t* __restrict__ rows,
                                                             int64_t n_rows,
                                                             const int64_t* __restrict__ dst_off,
@@ -285,8 +308,61 @@ __global__ void __launch_bounds__(256) gather_ragged_kernel(const T* __restrict_
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n_rows) return;
   const int64_t r = rows ? rows[i] : i;
-  const int64_t a = src_off[r], n = src_off[r + 1] - a, o = dst_off[i];
-  for (int64_t j = lane_id(); j < n; j += 64) dst[o + j] = src[a + j];
+  const int64_t* o2 = off.at(r);
+  const int64_t a = o2[0], n = o2[1] - a, o = dst_off[i];
+  const T* s = r < src.n_a ? src.a : src.b;  // offsets are relative to the row's own source
+  for (int64_t j = lane_id(); j < n; j += 64) dst[o + j] = s[a + j];
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) take_kernel(Src2<T> src, const int64_t* __restrict__ rows,
+                                                   int64_t n_rows, T* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n_rows) dst[i] = *src.at(rows ? rows[i] : i);
+}
+
+// Segmented index expansion: segment k covers outputs [seg_off[k], seg_off[k+1]); its element t
+// is v = start + t * stride, written as v (mode 1) or src[v] (mode 0). One thread per output;
+// the segment is found by binary search over the (L2-resident) segment offsets.
+__global__ void __launch_bounds__(256) expand_segments_kernel(const int64_t* __restrict__ src,
+                                                              const int64_t* __restrict__ seg,
+                                                              const int64_t* __restrict__ seg_off,
+                                                              int64_t n_seg, int64_t total,
+                                                              int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  int64_t lo = 0, hi = n_seg;  // seg_off[lo] <= i < seg_off[hi]
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (seg_off[mid] <= i) lo = mid;
+    else hi = mid;
+  }
+  const int64_t v = seg[3 * lo] + (i - seg_off[lo]) * seg[3 * lo + 1];
+  out[i] = seg[3 * lo + 2] ? v : src[v];
+}
+
+// Per-row metadata of the exchange: {len(A) + len(B), len(A), is_random_next, masks} as int32[4]
+__global__ void __launch_bounds__(256) pairs_meta_pack_kernel(
+    const int64_t* __restrict__ tok_off, const int32_t* __restrict__ len_a,
+    const uint8_t* __restrict__ is_rn, const int64_t* __restrict__ pos_off,
+    const int64_t* __restrict__ rows, int64_t n, int4* __restrict__ meta) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows ? rows[i] : i;
+  meta[i] = make_int4((int32_t)(tok_off[r + 1] - tok_off[r]), len_a[r], (int32_t)is_rn[r],
+                      pos_off ? (int32_t)(pos_off[r + 1] - pos_off[r]) : 0);
+}
+
+__global__ void __launch_bounds__(256) pairs_meta_unpack_kernel(
+    const int4* __restrict__ meta, int64_t n, int64_t* __restrict__ ntok,
+    int32_t* __restrict__ len_a, uint8_t* __restrict__ is_rn, int64_t* __restrict__ nmask) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int4 m = meta[i];
+  ntok[i] = m.x;
+  len_a[i] = m.y;
+  is_rn[i] = (uint8_t)m.z;
+  if (nmask) nmask[i] = m.w;
 }
 
 }  // namespace
@@ -294,33 +370,117 @@ __global__ void __launch_bounds__(256) gather_ragged_kernel(const T* __restrict_
 
 using namespace lddl;
 
-extern "C" int lddl_gather_ragged(void* stream, const void* d_src, const int64_t* d_src_off,
+template <typename T>
+static void launch_gather(const void* a, const int64_t* oa, int64_t n_a, const void* b,
+                          const int64_t* ob, const int64_t* rows, int64_t n, const int64_t* dst_off,
+                          void* dst, hipStream_t st) {
+  hipLaunchKernelGGL(gather_ragged_kernel<T>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st,
+                     Src2<T>{(const T*)a, (const T*)b, n_a}, Src2<int64_t>{oa, ob, n_a}, rows, n,
+                     dst_off, (T*)dst);
+}
+
+extern "C" int lddl_gather_ragged(void* stream, const void* d_src_a, const int64_t* d_off_a,
+                                  int64_t n_a, const void* d_src_b, const int64_t* d_off_b,
                                   int32_t elem_bytes, const int64_t* d_rows, int64_t n_rows,
                                   const int64_t* d_dst_off, void* d_dst) {
-  if (n_rows < 0) LDDL_FAIL(-1, "bad size");
+  if (n_rows < 0 || n_a < 0) LDDL_FAIL(-1, "bad size");
   if (n_rows == 0) return 0;
-  const dim3 grid((unsigned)((n_rows + 3) / 4)), block(256);
+  if (!d_rows && n_rows > n_a) LDDL_FAIL(-1, "n_rows > n_a without a row index");
   hipStream_t st = as_stream(stream);
   switch (elem_bytes) {
-    case 1:
-      hipLaunchKernelGGL(gather_ragged_kernel<uint8_t>, grid, block, 0, st,
-                         (const uint8_t*)d_src, d_src_off, d_rows, n_rows, d_dst_off, (uint8_t*)d_dst);
-      break;
-    case 2:
-      hipLaunchKernelGGL(gather_ragged_kernel<uint16_t>, grid, block, 0, st,
-                         (const uint16_t*)d_src, d_src_off, d_rows, n_rows, d_dst_off, (uint16_t*)d_dst);
-      break;
-    case 4:
-      hipLaunchKernelGGL(gather_ragged_kernel<uint32_t>, grid, block, 0, st,
-                         (const uint32_t*)d_src, d_src_off, d_rows, n_rows, d_dst_off, (uint32_t*)d_dst);
-      break;
-    case 8:
-      hipLaunchKernelGGL(gather_ragged_kernel<uint64_t>, grid, block, 0, st,
-                         (const uint64_t*)d_src, d_src_off, d_rows, n_rows, d_dst_off, (uint64_t*)d_dst);
-      break;
-    default:
-      LDDL_FAIL(-1, "elem_bytes %d unsupported", elem_bytes);
+    case 1: launch_gather<uint8_t>(d_src_a, d_off_a, n_a, d_src_b, d_off_b, d_rows, n_rows, d_dst_off, d_dst, st); break;
+    case 2: launch_gather<uint16_t>(d_src_a, d_off_a, n_a, d_src_b, d_off_b, d_rows, n_rows, d_dst_off, d_dst, st); break;
+    case 4: launch_gather<uint32_t>(d_src_a, d_off_a, n_a, d_src_b, d_off_b, d_rows, n_rows, d_dst_off, d_dst, st); break;
+    case 8: launch_gather<uint64_t>(d_src_a, d_off_a, n_a, d_src_b, d_off_b, d_rows, n_rows, d_dst_off, d_dst, st); break;
+    default: LDDL_FAIL(-1, "elem_bytes %d unsupported", elem_bytes);
   }
+  LDDL_HIP(hipGetLastError());
+  return 0;
+}
+
+template <typename T>
+static void launch_take(const void* a, int64_t n_a, const void* b, const int64_t* rows, int64_t n,
+                        void* dst, hipStream_t st) {
+  hipLaunchKernelGGL(take_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     Src2<T>{(const T*)a, (const T*)b, n_a}, rows, n, (T*)dst);
+}
+
+extern "C" int lddl_take(void* stream, const void* d_a, int64_t n_a, const void* d_b,
+                         int32_t elem_bytes, const int64_t* d_rows, int64_t n_rows, void* d_dst) {
+  if (n_rows < 0 || n_a < 0) LDDL_FAIL(-1, "bad size");
+  if (n_rows == 0) return 0;
+  if (!d_rows && n_rows > n_a) LDDL_FAIL(-1, "n_rows > n_a without a row index");
+  hipStream_t st = as_stream(stream);
+  switch (elem_bytes) {
+    case 1: launch_take<uint8_t>(d_a, n_a, d_b, d_rows, n_rows, d_dst, st); break;
+    case 2: launch_take<uint16_t>(d_a, n_a, d_b, d_rows, n_rows, d_dst, st); break;
+    case 4: launch_take<uint32_t>(d_a, n_a, d_b, d_rows, n_rows, d_dst, st); break;
+    case 8: launch_take<uint64_t>(d_a, n_a, d_b, d_rows, n_rows, d_dst, st); break;
+    default: LDDL_FAIL(-1, "elem_bytes %d unsupported", elem_bytes);
+  }
+  LDDL_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int lddl_expand_segments(void* stream, const int64_t* d_src, const int64_t* d_seg,
+                                    const int64_t* d_seg_off, int64_t n_seg, int64_t total,
+                                    int64_t* d_out) {
+  if (n_seg < 0 || total < 0) LDDL_FAIL(-1, "bad size");
+  if (total == 0) return 0;
+  if (n_seg == 0) LDDL_FAIL(-1, "no segments for %lld outputs", (long long)total);
+  hipLaunchKernelGGL(expand_segments_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), d_src, d_seg, d_seg_off, n_seg, total, d_out);
+  LDDL_HIP(hipGetLastError());
+  return 0;
+}
+
+namespace lddl {
+namespace {
+struct RowSize {
+  Src2<int64_t> off;
+  const int64_t* rows;
+  __device__ int64_t operator()(int64_t i) const {
+    const int64_t* o = off.at(rows ? rows[i] : i);
+    return o[1] - o[0];
+  }
+};
+}  // namespace
+}  // namespace lddl
+
+extern "C" int lddl_ragged_offsets(lddl_ctx* c, void* stream, const int64_t* d_off_a, int64_t n_a,
+                                   const int64_t* d_off_b, const int64_t* d_rows, int64_t n_rows,
+                                   int64_t* d_out) {
+  if (!c) LDDL_FAIL(-1, "null ctx");
+  if (n_rows < 0 || n_a < 0) LDDL_FAIL(-1, "bad size");
+  if (!d_rows && n_rows > n_a) LDDL_FAIL(-1, "n_rows > n_a without a row index");
+  hipStream_t st = as_stream(stream);
+  ArenaTmp scratch(&c->arena, st);
+  LDDL_HIP(scratch.take(sizeof(int64_t) * scan_scratch_elems(n_rows)));
+  LDDL_HIP(scan_exclusive(RowSize{Src2<int64_t>{d_off_a, d_off_b, n_a}, d_rows}, n_rows, d_out,
+                          scratch.as<int64_t>(), st));
+  return 0;
+}
+
+extern "C" int lddl_pairs_meta_pack(void* stream, const int64_t* d_tok_off, const int32_t* d_len_a,
+                                    const uint8_t* d_is_rn, const int64_t* d_pos_off,
+                                    const int64_t* d_rows, int64_t n, int32_t* d_meta) {
+  if (n < 0) LDDL_FAIL(-1, "bad size");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(pairs_meta_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), d_tok_off, d_len_a, d_is_rn, d_pos_off, d_rows, n,
+                     reinterpret_cast<int4*>(d_meta));
+  LDDL_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int lddl_pairs_meta_unpack(void* stream, const int32_t* d_meta, int64_t n,
+                                      int64_t* d_ntok, int32_t* d_len_a, uint8_t* d_is_rn,
+                                      int64_t* d_nmask) {
+  if (n < 0) LDDL_FAIL(-1, "bad size");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(pairs_meta_unpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), reinterpret_cast<const int4*>(d_meta), n, d_ntok, d_len_a,
+                     d_is_rn, d_nmask);
   LDDL_HIP(hipGetLastError());
   return 0;
 }
@@ -344,39 +504,39 @@ extern "C" int lddl_bin_partitions(lddl_ctx* c, void* stream, const int32_t* d_n
 }
 
 extern "C" int lddl_bin_stable(lddl_ctx* c, void* stream, const int32_t* d_num_tokens,
-                               int64_t n_rows, int32_t bin_size, int32_t nbins, int64_t* d_perm,
-                               int64_t* d_bin_id, int64_t* d_counts) {
-  (void)c;
+                               const int64_t* d_tok_off, int64_t n_rows, int32_t bin_size,
+                               int32_t nbins, int64_t* d_perm, int64_t* d_bin_id, int64_t* d_counts) {
+  if (!c) LDDL_FAIL(-1, "null ctx");
   if (bin_size < 1 || nbins < 1) LDDL_FAIL(-1, "bin_size and nbins must be >= 1");
   if (nbins > kMaxBinsLds) LDDL_FAIL(-1, "nbins %d > %d unsupported", nbins, kMaxBinsLds);
   if (n_rows < 0) LDDL_FAIL(-1, "bad sizes");
+  if (!d_num_tokens && !d_tok_off && n_rows) LDDL_FAIL(-1, "need num_tokens or tok_off");
   hipStream_t st = as_stream(stream);
   if (n_rows == 0) {
     LDDL_HIP(hipMemsetAsync(d_counts, 0, sizeof(int64_t) * nbins, st));
     return 0;
   }
+  const NumTok nt{d_num_tokens, d_tok_off};
   int nbits = 0;
   while ((1 << nbits) < nbins) ++nbits;
   const int64_t n_tiles = (n_rows + kBinTile - 1) / kBinTile;
   const int64_t m = n_tiles * nbins;
-  int64_t *tc, *scratch;
-  LDDL_HIP(hipMallocAsync((void**)&tc, sizeof(int64_t) * (2 * m + 1), st));
-  LDDL_HIP(hipMallocAsync((void**)&scratch, sizeof(int64_t) * scan_scratch_elems(m), st));
+  ArenaTmp tcb(&c->arena, st), scb(&c->arena, st);
+  LDDL_HIP(tcb.take(sizeof(int64_t) * (2 * m + 1)));
+  LDDL_HIP(scb.take(sizeof(int64_t) * scan_scratch_elems(m)));
+  int64_t* tc = tcb.as<int64_t>();
   int64_t* base = tc + m;
-  hipLaunchKernelGGL(bin_tile_hist_kernel, dim3((unsigned)n_tiles), dim3(64), 0, st, d_num_tokens,
+  hipLaunchKernelGGL(bin_tile_hist_kernel, dim3((unsigned)n_tiles), dim3(64), 0, st, nt,
                      n_rows, bin_size, nbins, n_tiles, tc);
   struct In {
     const int64_t* v;
     __device__ int64_t operator()(int64_t i) const { return v[i]; }
   };
-  const hipError_t e = scan_exclusive(In{tc}, m, base, scratch, st);
+  LDDL_HIP(scan_exclusive(In{tc}, m, base, scb.as<int64_t>(), st));
   hipLaunchKernelGGL(bin_tile_scatter_kernel, dim3((unsigned)n_tiles), dim3(64), 0, st,
-                     d_num_tokens, n_rows, bin_size, nbins, nbits, n_tiles, base, d_perm, d_bin_id);
+                     nt, n_rows, bin_size, nbins, nbits, n_tiles, base, d_perm, d_bin_id);
   hipLaunchKernelGGL(bin_totals_kernel, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, st,
                      base, n_tiles, nbins, d_counts);
-  LDDL_HIP(hipFreeAsync(scratch, st));
-  LDDL_HIP(hipFreeAsync(tc, st));
-  LDDL_HIP(e);
   LDDL_HIP(hipGetLastError());
   return 0;
 }
@@ -392,13 +552,17 @@ extern "C" int lddl_render_lengths(lddl_ctx* c, void* stream, const int32_t* d_t
                                    const int64_t* d_tok_off, const int32_t* d_len_a,
                                    const int32_t* d_lab, const int64_t* d_pos_off,
                                    const int64_t* d_rows, int64_t n_rows, int64_t* d_a_len,
-                                   int64_t* d_b_len, int64_t* d_l_len, int64_t* d_npy_len) {
+                                   int64_t* d_b_len, int64_t* d_l_len, int64_t* d_npy_len,
+                                   const uint8_t* d_is_rn, uint16_t* d_num_tokens_out,
+                                   uint8_t* d_is_rn_out) {
   if (!c) LDDL_FAIL(-1, "null ctx");
   if (n_rows <= 0) return 0;
+  if (d_is_rn_out && !d_is_rn) LDDL_FAIL(-1, "is_random_next output without input");
   const RenderArgs R = make_render(c, d_tokens, d_tok_off, d_len_a, nullptr, d_lab, d_pos_off,
                                    d_rows, n_rows);
   hipLaunchKernelGGL(render_lengths_kernel, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0,
-                     as_stream(stream), R, d_a_len, d_b_len, d_l_len, d_npy_len);
+                     as_stream(stream), R, d_a_len, d_b_len, d_l_len, d_npy_len, d_is_rn,
+                     d_num_tokens_out, d_is_rn_out);
   LDDL_HIP(hipGetLastError());
   return 0;
 }
@@ -422,17 +586,17 @@ extern "C" int lddl_render_write(lddl_ctx* c, void* stream, const int32_t* d_tok
   return 0;
 }
 
-extern "C" int lddl_scan_i64(void* stream, const int64_t* d_in, int64_t n, int64_t* d_out) {
+extern "C" int lddl_scan_i64(lddl_ctx* c, void* stream, const int64_t* d_in, int64_t n,
+                             int64_t* d_out) {
+  if (!c) LDDL_FAIL(-1, "null ctx");
   if (n < 0) LDDL_FAIL(-1, "bad size");
   hipStream_t st = as_stream(stream);
-  int64_t* scratch;
-  LDDL_HIP(hipMallocAsync((void**)&scratch, sizeof(int64_t) * scan_scratch_elems(n), st));
+  ArenaTmp scratch(&c->arena, st);
+  LDDL_HIP(scratch.take(sizeof(int64_t) * scan_scratch_elems(n)));
   struct In {
     const int64_t* v;
     __device__ int64_t operator()(int64_t i) const { return v[i]; }
   };
-  const hipError_t e = scan_exclusive(In{d_in}, n, d_out, scratch, st);
-  LDDL_HIP(hipFreeAsync(scratch, st));
-  LDDL_HIP(e);
+  LDDL_HIP(scan_exclusive(In{d_in}, n, d_out, scratch.as<int64_t>(), st));
   return 0;
 }

@@ -5,9 +5,9 @@ Pipeline (reference call stack in SURVEY.md §3.1):
   read `*.txt` sources into blocks (readers.py)            -> lddl_amd.dask.readers (host; each
                                                               rank reads only its own blocks)
   random shuffle of documents over partitions (100-111)    -> seeded shuffle of the documents of
-                                                              each GPU batch of partitions (host;
-                                                              the reference's is global and
-                                                              unseeded)
+                                                              each shuffle group of partitions
+                                                              (host; the reference's is global
+                                                              and unseeded)
   split_id_text (readers.py:131-136)                       -> host, per line
   sent_tokenize + strip + drop empty (86-88)               -> lddl_segment_* (HIP Punkt; nltk on
                                                               the host with --sentence-splitter host)
@@ -27,11 +27,14 @@ partitions p with p % world_size == r (partitions are independent) 
 those blocks.
 
 `--num-shards S` (lddl_amd; the reference runs `balance_dask_output` as a second job over the
-files): the pair tables stay in HBM, are binned per rank and balanced across ranks in one pass
-(lddl_amd/balance.py: RCCL all-gather of the per-bin counts, all-to-all-v of the rows that
-change rank), and the output is the balancer's layout directly: `shard-<k>.parquet_<b>` (or
-`shard-<k>.parquet` unbinned) with N or N+1 samples per bin, plus `.num_samples.json`
-(lddl/dask/load_balance.py:90-92, 372-378) — what get_bert_pretrain_data_loader consumes.
+files) writes the balancer's layout directly: `shard-<k>.parquet_<b>` (or `shard-<k>.parquet`
+unbinned) with N or N+1 samples per bin, plus `.num_samples.json` (lddl/dask/load_balance.py:
+90-92, 372-378) — what get_bert_pretrain_data_loader consumes. `--balance-plan stream` (default)
+balances every GPU batch in HBM as it is produced (lddl_amd/balance.py: RCCL all-gather of the
+batch's per-bin counts, round-robin deal of each bin's rows over the shards, all-to-all-v of the
+rows owned by other ranks), so HBM holds one batch at any corpus size and each shard file grows
+by one row group per batch; `--balance-plan reference` writes the part files and runs the
+drop-in balance_dask_output over them (the reference's exact shard contents).
 """
 import argparse
 import functools
@@ -85,32 +88,47 @@ def plan_partitions(args):
     return blocks
 
 
-def iter_batches(args, rank=0, world=1, blocks=None, as_bytes=False):
-    """This rank's partitions in GPU batches of <= --gpu-batch-bytes of input, read lazily:
-    yields [(p, lines)] per batch, the documents shuffled over the batch's partitions (each keeps
-    its document count) by Random(partition_seed(seed, -1 - first partition of the batch)).
-    as_bytes: lines as UTF-8 bytes (the GPU segmenter's input) instead of str."""
-    blocks = plan_partitions(args) if blocks is None else blocks
-    mine = [p for p in range(len(blocks)) if p % world == rank]
-    cur, size = [], 0
-    groups = []
-    for p in mine:
-        b = blocks[p].nbytes
-        if cur and size + b > args.gpu_batch_bytes:
-            groups.append(cur)
+def _greedy(items, size_of, cap):
+    """Consecutive runs of `items` of at most `cap` total size (at least one item each)."""
+    out, cur, size = [], [], 0
+    for it in items:
+        b = size_of(it)
+        if cur and size + b > cap:
+            out.append(cur)
             cur, size = [], 0
-        cur.append(p)
+        cur.append(it)
         size += b
     if cur:
-        groups.append(cur)
-    for g in groups:
-        parts = [(p, readers.read_block(blocks[p], as_bytes=as_bytes)) for p in g]
-        docs = [d for _, lines in parts for d in lines]
-        random.Random(partition_seed(args.seed, -1 - g[0])).shuffle(docs)
-        out, k = [], 0
-        for p, lines in parts:
-            out.append((p, docs[k:k + len(lines)]))
-            k += len(lines)
+        out.append(cur)
+    return out
+
+
+def rank_batches(args, blocks, rank=0, world=1):
+    """This rank's partitions (p % world == rank) as GPU batches: lists of shuffle groups, each a
+    list of partitions. Shuffle groups are runs of ~--shuffle-group-bytes of input and do not
+    depend on --gpu-batch-bytes; a batch is a run of whole groups of <= --gpu-batch-bytes."""
+    mine = [p for p in range(len(blocks)) if p % world == rank]
+    groups = _greedy(mine, lambda p: blocks[p].nbytes, args.shuffle_group_bytes)
+    return _greedy(groups, lambda g: sum(blocks[p].nbytes for p in g), args.gpu_batch_bytes)
+
+
+def iter_batches(args, rank=0, world=1, blocks=None, as_bytes=False):
+    """This rank's partitions in GPU batches, read lazily: yields [(p, lines)] per batch. The
+    documents of each shuffle group are shuffled over the group's partitions (each keeps its
+    document count) by Random(partition_seed(seed, -1 - first partition of the group)), so the
+    output does not depend on the GPU batch size. as_bytes: lines as UTF-8 bytes (the GPU
+    segmenter's input) instead of str."""
+    blocks = plan_partitions(args) if blocks is None else blocks
+    for batch in rank_batches(args, blocks, rank, world):
+        out = []
+        for g in batch:
+            parts = [(p, readers.read_block(blocks[p], as_bytes=as_bytes)) for p in g]
+            docs = [d for _, lines in parts for d in lines]
+            random.Random(partition_seed(args.seed, -1 - g[0])).shuffle(docs)
+            k = 0
+            for p, lines in parts:
+                out.append((p, docs[k:k + len(lines)]))
+                k += len(lines)
         yield out
 
 
@@ -302,44 +320,95 @@ def write_txt(outdir, rd, part_rows, index, masking, nbins, counts, n_part):
     return paths
 
 
-def write_balanced(ctx, args, bb, outdir, binned, executor=None, futures=None):
-    """This rank's balanced shards: `shard-<k>.parquet_<b>` per bin (binned) or
-    `shard-<k>.parquet`, the load balancer's names (load_balance.py:90-92)."""
-    import torch
-    from ... import output
-    dev = ctx.device
-    nbins = len(bb.bin_off) - 1
-    paths = []
-    for m, s in enumerate(bb.shards):
-        idx, bins = bb.shard_rows(m)
-        rows = torch.from_numpy(idx).to(dev)
-        if bb.rows is not None:
-            rows = bb.rows.index_select(0, rows)
-        rd = output.render(ctx, bb.table, rows, torch.from_numpy(bins).to(dev) if binned else None)
-        r0 = 0
-        for b in range(nbins):
-            r1 = r0 + int(bb.shard_counts[m, b])
-            fn = os.path.join(outdir, 'shard-{}.parquet{}'.format(s, '_{}'.format(b) if binned
-                                                                 else ''))
-            if executor is None:
-                output.write_table(rd, r0, r1, args.masking, binned, fn)
-            else:
-                futures.append(executor.submit(output.write_table, rd, r0, r1, args.masking,
-                                               binned, fn))
-            paths.append(fn)
-            r0 = r1
-    return paths
+class ShardWriters:
+    """This rank's balanced shards, written as the batches stream through: one parquet file per
+    (shard, bin) named like the load balancer's (`shard-<k>.parquet_<b>`, or `shard-<k>.parquet`
+    unbinned, load_balance.py:90-92), one row group per batch in batch order. Each batch's
+    writes run on the thread pool while the next batch is on the GPU; a writer is never
+    appended from two threads (a batch's writes finish before the next batch's start)."""
+
+    def __init__(self, outdir, nbins, binned, masking, pool):
+        self.outdir, self.nbins, self.binned, self.masking, self.pool = (outdir, nbins, binned,
+                                                                         masking, pool)
+        self.writers, self.pending, self.shards = {}, [], set()
+
+    def name(self, s, b):
+        return os.path.join(self.outdir, 'shard-{}.parquet{}'.format(
+            s, '_{}'.format(b) if self.binned else ''))
+
+    def _append(self, key, rd, r0, r1):
+        import pyarrow.parquet as pq
+        from ... import output
+        t = output.table(rd, r0, r1, self.masking, self.binned)
+        w = self.writers.get(key)
+        if w is None:
+            w = self.writers[key] = pq.ParquetWriter(self.name(*key), t.schema,
+                                                     compression=output.DEFAULT_COMPRESSION)
+        w.write_table(t)
+
+    def add(self, ctx, bb):
+        """Render this batch's rows of the rank's shards (GPU) and queue their writes."""
+        from ... import output
+        self.shards.update(bb.shards)
+        for f in self.pending:
+            f.result()
+        self.pending = []
+        if bb.n_rows == 0:
+            return
+        rd = output.render(ctx, bb.table, bb.rows, bb.bin_ids() if self.binned else None)
+        for m, s in enumerate(bb.shards):
+            for b in range(self.nbins):
+                r0, r1 = bb.shard_range(m, b)
+                if r1 > r0:
+                    self.pending.append(self.pool.submit(self._append, (s, b), rd, r0, r1))
+
+    def close(self):
+        """Finish the writes; shards of a bin that received no rows get an empty file (every bin
+        has all shards, as the loader requires)."""
+        import pyarrow.parquet as pq
+        from ... import output
+        for f in self.pending:
+            f.result()
+        self.pending = []
+        paths = []
+        for s in sorted(self.shards):
+            for b in range(self.nbins):
+                w = self.writers.pop((s, b), None)
+                if w is not None:
+                    w.close()
+                else:
+                    pq.write_table(output.schema(self.masking, self.binned).empty_table(),
+                                   self.name(s, b), compression=output.DEFAULT_COMPRESSION)
+                paths.append(self.name(s, b))
+        return paths
 
 
-def num_samples_of_shards(bb, binned):
-    """`.num_samples.json` content of the balanced layout (load_balance.py:372-378)."""
+def num_samples_of_shards(shard_counts, binned):
+    """`.num_samples.json` content of the balanced layout (load_balance.py:372-378) from the
+    int64[S, B] shard counts."""
     out = {}
-    S, B = bb.all_shard_counts.shape
+    S, B = shard_counts.shape
     for b in range(B):
         for s in range(S):
             out['shard-{}.parquet{}'.format(s, '_{}'.format(b) if binned else '')] = int(
-                bb.all_shard_counts[s, b])
+                shard_counts[s, b])
     return out
+
+
+def _empty_pairs(ctx, masking):
+    """A PairBatch without rows (a rank with fewer batches still takes part in the collectives)."""
+    import torch
+    from ...pairs import PairBatch
+    dev = ctx.device
+    e64 = torch.zeros(1, dtype=torch.int64, device=dev)
+    pb = PairBatch(torch.zeros(0, dtype=torch.int32, device=dev), e64,
+                   torch.zeros(0, dtype=torch.int32, device=dev),
+                   torch.zeros(0, dtype=torch.uint8, device=dev))
+    if masking:
+        pb.pos = torch.zeros(0, dtype=torch.int16, device=dev)
+        pb.labels = torch.zeros(0, dtype=torch.int32, device=dev)
+        pb.pos_off = e64.clone()
+    return pb
 
 
 def _prefetch(gen, depth=1):
@@ -400,6 +469,8 @@ def main(args):
         raise ValueError('Format {} not supported!'.format(args.output_format))
     if args.num_shards is not None and args.output_format != 'parquet':
         raise ValueError('--num-shards writes balanced parquet shards only')
+    if args.num_shards is not None and args.num_shards < 1:
+        raise ValueError('--num-shards must be >= 1')
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -432,11 +503,21 @@ def main(args):
         batches = _prefetch(batches)
     timer.mark()
     n_files = 0
-    kept = []
     pending = []  # writes of the previous batch (at most two batches of rendered rows in memory)
+    stream = writers = None
+    if args.num_shards is not None and args.balance_plan == 'stream':
+        from ...balance import StreamBalancer
+        binned = args.bin_size is not None
+        bin_size = args.bin_size if binned else args.target_seq_length
+        nbins = args.target_seq_length // bin_size
+        stream = StreamBalancer(ctx, bin_size, nbins, num_shards=args.num_shards)
+        writers = ShardWriters(outdir, nbins, binned, args.masking, pool)
+        # every rank steps the balancer once per batch of the rank with the most batches
+        n_steps = max(len(rank_batches(args, blocks, r, world)) for r in range(world))
+    k = 0
     for batch, corpus in batches:
         timer('read')
-        if args.num_shards is None:
+        if stream is None:
             futs = []
             n_files += len(process_batch(ctx, args, batch, corpus, outdir, timer, pool, futs))
             for f in pending:
@@ -444,48 +525,40 @@ def main(args):
             pending = futs
             timer('write_wait')
         else:
-            kept.append(make_batch_pairs(ctx, args, batch, corpus, timer))
+            bb = stream.step(make_batch_pairs(ctx, args, batch, corpus, timer))
+            timer('balance')
+            writers.add(ctx, bb)
+            del bb
+            timer('render')
+            k += 1
         timer.mark()
     for f in pending:
         f.result()
     timer('write_wait')
-    if args.num_shards is not None:
-        from ...balance import balance
-        from ...pairs import cat_pair_batches, PairBatch
-        timer.mark()
-        if kept:
-            pb = cat_pair_batches(kept)
-        else:  # a rank without partitions still takes part in the collectives
-            e64 = torch.zeros(1, dtype=torch.int64, device=ctx.device)
-            pb = PairBatch(torch.zeros(0, dtype=torch.int32, device=ctx.device), e64,
-                           torch.zeros(0, dtype=torch.int32, device=ctx.device),
-                           torch.zeros(0, dtype=torch.uint8, device=ctx.device))
-            if args.masking:
-                pb.pos = torch.zeros(0, dtype=torch.int16, device=ctx.device)
-                pb.labels = torch.zeros(0, dtype=torch.int32, device=ctx.device)
-                pb.pos_off = e64.clone()
-        del kept
-        binned = args.bin_size is not None
-        bin_size = args.bin_size if binned else args.target_seq_length
-        nbins = args.target_seq_length // bin_size
-        bb = balance(ctx, pb, bin_size, nbins, num_shards=args.num_shards)
-        timer('balance')
-        futs = []
-        n_files += len(write_balanced(ctx, args, bb, outdir, binned, pool, futs))
-        for f in futs:
-            f.result()
-        timer('render+write')
+    if stream is not None:
+        for _ in range(k, n_steps):
+            writers.add(ctx, stream.step(_empty_pairs(ctx, args.masking)))
+        n_files += len(writers.close())
+        timer('write_wait')
         if rank == 0:
             with open(os.path.join(outdir, '.num_samples.json'), 'w') as f:
-                json.dump(num_samples_of_shards(bb, binned), f)
+                json.dump(num_samples_of_shards(stream.all_shard_counts, binned), f)
     pool.shutdown()
     if world > 1:
         dist.barrier()
-    if rank == 0 and args.num_shards is None and args.output_format == 'parquet':
+    if rank == 0 and stream is None and args.output_format == 'parquet':
         from ... import output
         output.write_dataset_metadata(outdir, len(blocks),
                                       None if args.bin_size is None else
                                       args.target_seq_length // args.bin_size)
+    if args.num_shards is not None and args.balance_plan == 'reference':
+        # the reference's second job over the part files: balance_dask_output in place
+        # (load_balance.py:381-418), its exact shard layout, originals deleted
+        from .. import load_balance as LB
+        if world > 1:
+            dist.barrier()
+        LB.main(LB.attach_args().parse_args(['--indir', outdir, '--num-shards',
+                                             str(args.num_shards)]))
     if rank == 0:
         print('Running the dask pipeline took {} s'.format(time.perf_counter() - tic))
         if args.profile_stages:
@@ -542,8 +615,12 @@ def attach_args(parser=None):
                     'masking in the data loader)')
     parser.add_argument('--masked-lm-ratio', type=float, default=0.15, help='Default: 0.15')
     parser.add_argument('--gpu-batch-bytes', type=int, default=1 << 30,
-                        help='lddl_amd: input text bytes per GPU batch of partitions (documents '
-                             'are shuffled within a batch)')
+                        help='lddl_amd: input text bytes per GPU batch of partitions (whole '
+                             'shuffle groups; bounds HBM use, does not change the output)')
+    parser.add_argument('--shuffle-group-bytes', type=int, default=1 << 30,
+                        help='lddl_amd: documents are shuffled across the partitions of runs of '
+                             'this many input bytes (the reference shuffles globally, '
+                             'pretrain.py:100-111; INTEGRATION.md)')
     parser.add_argument('--sentence-splitter', choices=['gpu', 'host'], default='gpu',
                         help='gpu: Punkt on the GPU (exact nltk PunktSentenceTokenizer); host: '
                              "nltk's sent_tokenize in host processes (requires nltk)")
@@ -557,9 +634,15 @@ def attach_args(parser=None):
                              "'native' draws the same distributions from Philox counter streams "
                              "keyed by --seed (documents and pairs in parallel)")
     parser.add_argument('--num-shards', type=int, default=None,
-                        help='lddl_amd: balance in HBM across all ranks (RCCL) and write the '
-                             "load balancer's layout (shard-<k>.parquet[_<b>] with N or N+1 "
-                             'samples per bin + .num_samples.json) instead of part.* files')
+                        help="lddl_amd: write the load balancer's layout (shard-<k>.parquet[_<b>] "
+                             'with N or N+1 samples per bin + .num_samples.json) instead of '
+                             'part.* files (see --balance-plan)')
+    parser.add_argument('--balance-plan', choices=['stream', 'reference'], default='stream',
+                        help="lddl_amd, with --num-shards: 'stream' balances each GPU batch in "
+                             "HBM as it is produced (round-robin deal of every bin's rows over "
+                             "the shards, RCCL exchange; one batch resident); 'reference' writes "
+                             "the part files and runs balance_dask_output over them, the "
+                             "reference's exact shard layout")
     parser.add_argument('--write-threads', type=int, default=min(os.cpu_count() or 1, 16),
                         help='lddl_amd: parquet files written concurrently (threads). Default: '
                              'min(cpus, 16)')

@@ -139,7 +139,13 @@ def read_block(blk, as_bytes=False):
         return lines
     r = random.Random()
     r.setstate(blk.state)
-    return [x for x in lines if r.random() < blk.ratio]
+    kept = []
+    for x in lines:
+        if r.random() < blk.ratio:
+            kept.append(x)
+        elif as_bytes:  # dask's read_text decodes every line strictly, sampled out or not; the
+            x.decode('utf-8')  # kept ones are checked on the GPU (lddl_utf8_check)
+    return kept
 
 
 def read_blocks(files, blocksize=None):

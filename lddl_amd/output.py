@@ -46,22 +46,24 @@ def bin_partitions(ctx, num_tokens, part_off, bin_size, nbins):
     return perm, bin_id, counts.view(n_part, nbins)
 
 
-def bin_stable(ctx, num_tokens, bin_size, nbins):
-    """One segment (all rows): (perm, bin_id, counts[nbins]) — the tiled multi-workgroup regroup
-    used before the load-balance exchange."""
-    n = num_tokens.numel()
-    dev = num_tokens.device
+def bin_stable(ctx, num_tokens=None, bin_size=8, nbins=1, tok_off=None, with_bin_id=True):
+    """One segment (all rows): (perm, bin_id or None, counts[nbins]) — the tiled multi-workgroup
+    regroup used before the load-balance exchange. Rows are given by num_tokens (int32 cuda) or
+    by a pair table's tok_off (num_tokens = len(A) + len(B) + 3)."""
+    n = num_tokens.numel() if num_tokens is not None else tok_off.numel() - 1
+    dev = ctx.device
     perm = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
-    bin_id = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
+    bin_id = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n] if with_bin_id else None
     counts = torch.empty(nbins, dtype=torch.int64, device=dev)
-    check(lib.lddl_bin_stable(ctx.handle, _stream(), _ptr(num_tokens), n, bin_size, nbins,
-                              _ptr(perm), _ptr(bin_id), _ptr(counts)))
+    check(lib.lddl_bin_stable(ctx.handle, _stream(), _ptr(num_tokens), _ptr(tok_off), n, bin_size,
+                              nbins, _ptr(perm), _ptr(bin_id), _ptr(counts)))
     return perm, bin_id, counts
 
 
-def _scan(x):
+def scan(ctx, x):
+    """Exclusive prefix sum of int64 cuda x -> int64[n + 1] (HIP, lddl_scan_i64)."""
     out = torch.empty(x.numel() + 1, dtype=torch.int64, device=x.device)
-    check(lib.lddl_scan_i64(_stream(), _ptr(x), x.numel(), _ptr(out)))
+    check(lib.lddl_scan_i64(ctx.handle, _stream(), _ptr(x), x.numel(), _ptr(out)))
     return out
 
 
@@ -112,12 +114,15 @@ def render(ctx, pb, rows=None, bin_id=None):
     npy_len = torch.empty_like(a_len) if masking else None
     lab = pb.labels if masking else None
     pos_off = pb.pos_off if masking else None
+    num_tokens = torch.empty(max(n, 1), dtype=torch.int16, device=dev)[:n]  # uint16 storage
+    is_rn = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)[:n]
     check(lib.lddl_render_lengths(ctx.handle, st, _ptr(pb.tokens), _ptr(pb.tok_off), _ptr(pb.len_a),
                                   _ptr(lab), _ptr(pos_off), _ptr(rows), n, _ptr(a_len), _ptr(b_len),
-                                  _ptr(l_len), _ptr(npy_len)))
-    a_off, b_off = _scan(a_len), _scan(b_len)
-    l_off = _scan(l_len) if masking else None
-    npy_off = _scan(npy_len) if masking else None
+                                  _ptr(l_len), _ptr(npy_len), _ptr(pb.is_random_next),
+                                  _ptr(num_tokens), _ptr(is_rn)))
+    a_off, b_off = scan(ctx, a_len), scan(ctx, b_len)
+    l_off = scan(ctx, l_len) if masking else None
+    npy_off = scan(ctx, npy_len) if masking else None
     tot = [int(x[-1].item()) if x is not None else 0 for x in (a_off, b_off, l_off, npy_off)]
     bufs = [torch.empty(max(t, 1), dtype=torch.uint8, device=dev) for t in tot]
     check(lib.lddl_render_write(ctx.handle, st, _ptr(pb.tokens), _ptr(pb.tok_off), _ptr(pb.len_a),
@@ -126,9 +131,6 @@ def render(ctx, pb, rows=None, bin_id=None):
                                 _ptr(npy_off), _ptr(bufs[0]), _ptr(bufs[1]),
                                 _ptr(bufs[2]) if masking else None,
                                 _ptr(bufs[3]) if masking else None))
-    sel = (lambda x: x) if rows is None else (lambda x: x.index_select(0, rows))
-    num_tokens = sel((pb.tok_off[1:] - pb.tok_off[:-1]) + 3)
-    is_rn = sel(pb.is_random_next)
 
     def host(t, k):  # pinned staging (torch's caching host allocator): full-rate D2H
         h = torch.empty(max(k, 1), dtype=t.dtype, pin_memory=True)[:k]
@@ -137,12 +139,13 @@ def render(ctx, pb, rows=None, bin_id=None):
 
     out = Rendered(a_off.cpu().numpy(), host(bufs[0], tot[0]), b_off.cpu().numpy(),
                    host(bufs[1], tot[1]), is_rn.cpu().numpy().astype(bool),
-                   num_tokens.cpu().numpy().astype(np.uint16))
+                   num_tokens.cpu().numpy().view(np.uint16))
     if masking:
         out.l_off, out.l_bytes = l_off.cpu().numpy(), host(bufs[2], tot[2])
         out.npy_off, out.npy_bytes = npy_off.cpu().numpy(), host(bufs[3], tot[3])
-    if bin_id is not None:
-        out.bin_id = bin_id.cpu().numpy().astype(np.int64)
+    if bin_id is not None:  # host int64[n] (or a device tensor)
+        out.bin_id = (bin_id.cpu().numpy() if torch.is_tensor(bin_id) else
+                      np.asarray(bin_id)).astype(np.int64)
     return out
 
 

@@ -54,27 +54,6 @@ class PairBatch:
         return out
 
 
-def cat_pair_batches(pbs):
-    """One PairBatch of the rows of `pbs` in order (device concatenation, offsets rebased)."""
-    if len(pbs) == 1:
-        return pbs[0]
-    tok0 = np.cumsum([0] + [int(p.tokens.numel()) for p in pbs[:-1]])
-    toks = torch.cat([p.tokens for p in pbs])
-    tok_off = torch.cat([pbs[0].tok_off[:1]] + [p.tok_off[1:] + int(o) for p, o in zip(pbs, tok0)])
-    out = PairBatch(toks, tok_off, torch.cat([p.len_a for p in pbs]),
-                    torch.cat([p.is_random_next for p in pbs]))
-    if pbs[0].pos is not None:
-        m0 = np.cumsum([0] + [int(p.pos.numel()) for p in pbs[:-1]])
-        out.pos = torch.cat([p.pos for p in pbs])
-        out.labels = torch.cat([p.labels for p in pbs])
-        out.pos_off = torch.cat([pbs[0].pos_off[:1]] +
-                                [p.pos_off[1:] + int(o) for p, o in zip(pbs, m0)])
-        out.n_masked = int(out.pos.numel())
-    out.n_kept_sentences = sum(p.n_kept_sentences for p in pbs)
-    out.n_kept_documents = sum(p.n_kept_documents for p in pbs)
-    return out
-
-
 def make_pairs(ctx, sent_off, ids, sent_len, doc_sent_off, part_doc_off, part_seed, seq=128,
                dup=5, masking=False, short_seq_prob=0.1, masked_lm_ratio=0.15, rng='replay',
                native_seed=12345):

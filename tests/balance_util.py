@@ -5,33 +5,86 @@ TorchCpuOps is test infrastructure: the product always uses balance.HipOps (HIP 
 import numpy as np
 import torch
 
-from lddl_amd.balance import plan_exchange, shard_owner, shard_targets
+from lddl_amd.balance import shard_owner, shard_targets
 from lddl_amd.pairs import PairBatch
 
 
+def _np(t):
+    return None if t is None else t.numpy()
+
+
 class TorchCpuOps:
-    def bin_stable(self, num_tokens, bin_size, nbins):
-        b = torch.clamp((num_tokens.long() - 1) // bin_size, max=nbins - 1)
-        perm = torch.from_numpy(np.argsort(b.numpy(), kind='stable').astype(np.int64))
-        return perm, torch.bincount(b, minlength=nbins).long()
+    """numpy restatement of HipOps on CPU tensors (two-source row addressing: row r < n_a is
+    row r of the first table, else row r - n_a of the second)."""
+
+    def bin_stable(self, pb, bin_size, nbins):
+        nt = np.diff(pb.tok_off.numpy()) + 3
+        b = np.minimum((nt - 1) // bin_size, nbins - 1)
+        return (torch.from_numpy(np.argsort(b, kind='stable').astype(np.int64)),
+                torch.from_numpy(np.bincount(b, minlength=nbins).astype(np.int64)))
 
     def scan(self, x):
         return torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(x.long(), 0)])
 
-    def gather_into(self, src, src_off, rows, dst_off, dst):
-        so, do = src_off.tolist(), dst_off.tolist()
-        for i, r in enumerate(rows.tolist()):
-            n = so[r + 1] - so[r]
-            dst[do[i]:do[i] + n] = src[so[r]:so[r + 1]]
-        return dst
+    def expand(self, src, seg, seg_off, dev):
+        out = [np.zeros(0, np.int64)]
+        for (st, sd, direct), a, z in zip(np.asarray(seg).reshape(-1, 3), seg_off[:-1], seg_off[1:]):
+            v = st + np.arange(z - a, dtype=np.int64) * sd
+            out.append(v if direct else src.numpy()[v])
+        return torch.from_numpy(np.concatenate(out))
+
+    @staticmethod
+    def _pick(a, n_a, b, r):
+        out = np.empty(len(r), a.dtype)
+        m = r < n_a
+        out[m] = a[r[m]]
+        if (~m).any():
+            out[~m] = b[r[~m] - n_a]
+        return out
+
+    def take(self, a, n_a, b, rows):
+        return torch.from_numpy(self._pick(a.numpy(), n_a, _np(b), rows.numpy()))
+
+    def _spans(self, off_a, n_a, off_b, rows):
+        r = rows.numpy()
+        oa, ob = off_a.numpy(), _np(off_b)
+        lo = self._pick(oa[:-1], n_a, None if ob is None else ob[:-1], r)
+        hi = self._pick(oa[1:], n_a, None if ob is None else ob[1:], r)
+        return r, lo, hi
+
+    def ragged_offsets(self, off_a, n_a, off_b, rows):
+        _, lo, hi = self._spans(off_a, n_a, off_b, rows)
+        return torch.from_numpy(np.concatenate([[0], np.cumsum(hi - lo)]).astype(np.int64))
+
+    def gather(self, a, off_a, n_a, b, off_b, rows, dst_off, total):
+        r, lo, hi = self._spans(off_a, n_a, off_b, rows)
+        A, B = a.numpy(), _np(b)
+        parts = [(A if q < n_a else B)[x:y] for q, x, y in zip(r, lo, hi)]
+        out = np.concatenate(parts) if parts else np.zeros(0, A.dtype)
+        assert len(out) == total
+        return torch.from_numpy(out.astype(A.dtype))
+
+    def meta_pack(self, pb, rows):
+        r = rows.numpy()
+        to = pb.tok_off.numpy()
+        po = pb.pos_off.numpy() if pb.pos_off is not None else None
+        m = np.stack([to[r + 1] - to[r], pb.len_a.numpy()[r], pb.is_random_next.numpy()[r],
+                      (po[r + 1] - po[r]) if po is not None else np.zeros(len(r), np.int64)], 1)
+        return torch.from_numpy(m.astype(np.int32).reshape(-1))
+
+    def meta_unpack(self, meta):
+        m = meta.numpy().reshape(-1, 4)
+        return (torch.from_numpy(m[:, 0].astype(np.int64)), torch.from_numpy(m[:, 1].copy()),
+                torch.from_numpy(m[:, 2].astype(np.uint8)), torch.from_numpy(m[:, 3].astype(np.int64)))
 
 
-def random_table(rng, n, seq, rank, masking=True, device='cpu'):
-    """A PairBatch of n rows whose token ids encode (rank, row, k) so that moves are traceable."""
+def random_table(rng, n, seq, rank, masking=True, device='cpu', tag=0):
+    """A PairBatch of n rows whose token ids encode (tag, rank, row, k) so moves are traceable."""
     ntok = rng.integers(2, seq - 2, n).astype(np.int64)
     tok_off = np.concatenate([[0], np.cumsum(ntok)]).astype(np.int64)
-    tokens = np.concatenate([np.full(c, rank * 1_000_000 + r * 100, np.int64) + np.arange(c)
-                             for r, c in enumerate(ntok)] or [np.zeros(0, np.int64)]) % (1 << 31)
+    tokens = np.concatenate([np.full(c, tag * 50_000_000 + rank * 1_000_000 + r * 100, np.int64) +
+                             np.arange(c) for r, c in enumerate(ntok)] or [np.zeros(0, np.int64)]
+                            ) % (1 << 31)
     len_a = np.array([rng.integers(1, c) for c in ntok], np.int32)
     is_rn = rng.integers(0, 2, n).astype(np.uint8)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
@@ -60,35 +113,43 @@ def host_rows(h):
     return out
 
 
-def check_balanced(inputs, outputs, bin_size, nbins, num_shards):
-    """inputs[r]: rank r's to_host() table before; outputs[r]: (host dict of the materialised
-    output table, bin_off, shards, shard_counts). Checks the north-star / reference invariants:
-    per bin every shard holds N or N+1 samples, each rank's table is bin-major, and the
-    concatenation over ranks of bin b equals the global stable bin order (rank-major input)."""
-    W = len(inputs)
-    counts = []
-    glob = [[] for _ in range(nbins)]
-    for h in inputs:
-        nt = np.diff(h['tok_off']) + 3
-        bins = np.minimum((nt - 1) // bin_size, nbins - 1)
-        counts.append(np.bincount(bins, minlength=nbins))
-        rows = host_rows(h)
-        for q in np.argsort(bins, kind='stable'):
-            glob[bins[q]].append(rows[q])
-    counts = np.asarray(counts, np.int64)
-    target, _, _ = plan_exchange(counts, num_shards)
-    st = shard_targets(counts, num_shards)
-    assert (st.max(0) - st.min(0) <= 1).all()
-    owner = shard_owner(num_shards, W)
-    got = [[] for _ in range(nbins)]
-    for k, (h, bin_off, shards, shard_counts) in enumerate(outputs):
-        np.testing.assert_array_equal(np.diff(bin_off), target[k])
-        assert list(shards) == [s for s in range(num_shards) if owner[s] == k]
-        np.testing.assert_array_equal(shard_counts, st[shards])
-        np.testing.assert_array_equal(np.asarray(shard_counts).sum(0), target[k])
-        rows = host_rows(h)
-        assert len(rows) == bin_off[-1]
+def check_stream(inputs, outputs, bin_size, nbins, num_shards):
+    """inputs[t][r]: rank r's to_host() table of batch t; outputs[t][r]: (host dict of the
+    materialised output table, bin_off, shards, shard_counts). Checks the deal contract: the
+    global order of bin b is batch-major, then rank-major, then each rank's stable bin order;
+    global row g of bin b belongs to shard g % S, shard s to rank s * W // S; each rank's output
+    of a batch is bin-major, then its shards ascending, rows in global order; and after every
+    batch each shard holds N or N+1 rows of every bin (the reference's Progress targets).
+    Returns the cumulative int64[S, B] shard counts."""
+    W, S = len(inputs[0]), num_shards
+    owner = shard_owner(S, W)
+    prior = np.zeros(nbins, np.int64)
+    cum = np.zeros((S, nbins), np.int64)
+    for t in range(len(inputs)):
+        glob = [[] for _ in range(nbins)]
+        for h in inputs[t]:
+            nt = np.diff(h['tok_off']) + 3
+            bins = np.minimum((nt - 1) // bin_size, nbins - 1)
+            rows = host_rows(h)
+            for q in np.argsort(bins, kind='stable'):
+                glob[bins[q]].append(rows[q])
+        per_shard = [[[] for _ in range(nbins)] for _ in range(S)]
         for b in range(nbins):
-            got[b] += rows[bin_off[b]:bin_off[b + 1]]
-    for b in range(nbins):
-        assert got[b] == glob[b], 'bin {} differs from the global stable order'.format(b)
+            for i, row in enumerate(glob[b]):
+                per_shard[(prior[b] + i) % S][b].append(row)
+            prior[b] += len(glob[b])
+        for k, (h, bin_off, shards, shard_counts) in enumerate(outputs[t]):
+            assert list(shards) == [s for s in range(S) if owner[s] == k]
+            rows = host_rows(h)
+            assert len(rows) == bin_off[-1]
+            for b in range(nbins):
+                exp = [x for s in shards for x in per_shard[s][b]]
+                assert rows[bin_off[b]:bin_off[b + 1]] == exp, \
+                    'batch {} rank {} bin {} differs from the dealt global order'.format(t, k, b)
+                for m, s in enumerate(shards):
+                    assert shard_counts[m][b] == len(per_shard[s][b])
+        for s in range(S):
+            for b in range(nbins):
+                cum[s, b] += len(per_shard[s][b])
+        np.testing.assert_array_equal(cum, shard_targets(prior[None, :], S))
+    return cum

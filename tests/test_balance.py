@@ -1,13 +1,12 @@
-"""HBM load balance across ranks (lddl_amd/balance.py).
+"""Streaming load balance across ranks (lddl_amd/balance.py).
 
-* the plan (pure host) for random count matrices and shard counts;
-* `balance_virtual` (W ranks in one process) and `balance` under gloo at world size 2 on the
-  CPU, both running the product's plan / pack / regroup code with CPU data-movement
-  primitives (tests/balance_util.py);
-* on the GPU: `balance_virtual` over W = 1, 2, 4, 8 virtual ranks with the HIP kernels, on real
-  pair tables, against the oracle's stable bin order (oracle.bin_samples).
+* the deal plan (pure host): `deal_runs` against a brute-force deal, N / N+1 after every prefix;
+* `stream_virtual` (W ranks in one process, several batches) and `StreamBalancer` under gloo at
+  world size 2 on the CPU, both running the product's plan / pack / regroup code with CPU
+  data-movement primitives (tests/balance_util.py);
+* on the GPU: `stream_virtual` over W = 1 .. 8 virtual ranks with the HIP kernels, on real pair
+  tables split into batches, against the contract and the oracle's stable bin order.
 Invariants follow lddl/dask/load_balance.py:321-378 (per bin, N or N+1 samples per shard)."""
-import os
 import socket
 
 import numpy as np
@@ -16,43 +15,37 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from balance_util import TorchCpuOps, check_balanced, random_table
-from lddl_amd.balance import balance, balance_virtual, plan_exchange, shard_targets
+from balance_util import TorchCpuOps, check_stream, random_table
+from lddl_amd.balance import (StreamBalancer, balance, batch_start, deal_runs, shard_targets,
+                              stream_virtual)
 
 
-def _check_plan(counts, S=None):
-    W, B = counts.shape
-    target, send, first = plan_exchange(counts, S)
-    assert (target.sum(0) == counts.sum(0)).all()
-    st = shard_targets(counts, W if S is None else S)
-    assert (st.max(0) - st.min(0) <= 1).all()
-    assert (send.sum(1) == counts).all() and (send.sum(0) == target).all()
-    for b in range(B):  # global (rank-major) order is preserved: receivers get contiguous runs
-        gid = np.concatenate([[0], np.cumsum(counts[:, b])])
-        got = []
-        for k in range(W):
-            for j in range(W):
-                n = send[j, k, b]
-                if n:
-                    got += list(range(gid[j] + first[j, k, b], gid[j] + first[j, k, b] + n))
-        assert got == list(range(counts[:, b].sum()))
-
-
-def test_plan_exchange_cases():
+def test_deal_runs_brute_force():
     rng = np.random.default_rng(0)
-    for W, B in ((1, 4), (2, 64), (3, 5), (8, 64)):
-        for S in (None, W, 2 * W + 1, 64):
-            for _ in range(10):
-                c = rng.integers(0, 50, (W, B))
-                c[:, 0] = 0
-                _check_plan(c, S)
+    for _ in range(200):
+        S = int(rng.integers(1, 20))
+        g0 = int(rng.integers(0, 100))
+        c = int(rng.integers(0, 60))
+        first, n = deal_runs(np.array([g0]), np.array([c]), S)
+        for s in range(S):
+            rows = [i for i in range(c) if (g0 + i) % S == s]
+            assert n[0, s] == len(rows)
+            if rows:
+                assert rows == list(range(first[0, s], c, S))
 
 
-def test_plan_balanced_input_moves_nothing():
-    c = np.full((4, 8), 10, np.int64)
-    _, send, _ = plan_exchange(c)
-    assert (send[np.arange(4), np.arange(4)] == c).all()
-    assert send.sum() == c.sum()  # everything stays home
+def test_deal_prefixes_balanced():
+    """Any sequence of batches of any sizes leaves every shard within one row (N or N+1)."""
+    rng = np.random.default_rng(1)
+    for W, S, B in ((1, 1, 3), (2, 5, 4), (4, 4, 8), (8, 24, 64), (3, 2, 5)):
+        prior = np.zeros(B, np.int64)
+        tot = np.zeros((S, B), np.int64)
+        for _ in range(6):
+            counts = rng.integers(0, 40, (W, B))
+            _, n = deal_runs(batch_start(prior, counts), counts, S)
+            tot += n.sum(0).T
+            prior += counts.sum(0)
+            np.testing.assert_array_equal(tot, shard_targets(prior[None, :], S))
 
 
 def _to_host_out(bb, ops):
@@ -60,16 +53,19 @@ def _to_host_out(bb, ops):
     return (m.table.to_host(), bb.bin_off, bb.shards, bb.shard_counts)
 
 
-@pytest.mark.parametrize('W,S,masking', [(1, 1, True), (1, 3, False), (2, 2, True), (3, 7, True),
-                                         (4, 4, False), (8, 8, True), (8, 20, True)])
-def test_balance_virtual_cpu(W, S, masking):
-    rng = np.random.default_rng(W * 100 + S)
+@pytest.mark.parametrize('W,S,masking,T', [(1, 1, True, 1), (1, 3, False, 3), (2, 2, True, 2),
+                                           (3, 7, True, 3), (4, 4, False, 1), (8, 8, True, 2),
+                                           (8, 20, True, 1), (2, 1, True, 2)])
+def test_stream_virtual_cpu(W, S, masking, T):
+    rng = np.random.default_rng(W * 100 + S + T)
     ops = TorchCpuOps()
-    pbs = [random_table(rng, int(rng.integers(0, 120)), 64, r, masking) for r in range(W)]
-    outs = balance_virtual(ops, pbs, 8, 8, num_shards=S)
-    check_balanced([pb.to_host() for pb in pbs], [_to_host_out(o, ops) for o in outs], 8, 8, S)
+    batches = [[random_table(rng, int(rng.integers(0, 120)), 64, r, masking, tag=t)
+                for r in range(W)] for t in range(T)]
+    outs = stream_virtual(ops, batches, 8, 8, num_shards=S)
+    check_stream([[pb.to_host() for pb in pbs] for pbs in batches],
+                 [[_to_host_out(o, ops) for o in os_] for os_ in outs], 8, 8, S)
     if W == 1:
-        assert outs[0].moved_rows == 0 and outs[0].rows is not None  # no copy at world size 1
+        assert all(o[0].moved_rows == 0 and o[0].rows is not None for o in outs)  # no copy
 
 
 def _free_port():
@@ -85,20 +81,28 @@ def _worker(rank, world, port, S, out):
                             world_size=world)
     rng = np.random.default_rng(1000 + rank)
     ops = TorchCpuOps()
-    pb = random_table(rng, [150, 40][rank], 64, rank, True)
-    bb = balance(None, pb, 8, 8, num_shards=S, ops=ops)
-    out[rank] = (pb.to_host(), _to_host_out(bb, ops), bb.moved_rows)
+    sb = StreamBalancer(None, 8, 8, num_shards=S, ops=ops)
+    res = []
+    for t, n in enumerate([[150, 40], [0, 70], [33, 33]]):  # an empty batch on rank 0 too
+        pb = random_table(rng, n[rank], 64, rank, True, tag=t)
+        bb = sb.step(pb)
+        res.append((pb.to_host(), _to_host_out(bb, ops), bb.moved_rows))
+    out[rank] = (res, sb.all_shard_counts)
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize('S', [2, 5])
-def test_balance_gloo_world2(S):
+def test_stream_gloo_world2(S):
     with mp.Manager() as m:
         out = m.dict()
         mp.spawn(_worker, args=(2, _free_port(), S, out), nprocs=2, join=True)
         res = dict(out)
-    check_balanced([res[0][0], res[1][0]], [res[0][1], res[1][1]], 8, 8, S)
-    assert res[1][2] > 0  # the lighter rank received rows over the exchange
+    T = len(res[0][0])
+    cum = check_stream([[res[r][0][t][0] for r in range(2)] for t in range(T)],
+                       [[res[r][0][t][1] for r in range(2)] for t in range(T)], 8, 8, S)
+    for r in range(2):  # every rank's running layout is the same, and the one checked
+        np.testing.assert_array_equal(res[r][1], cum)
+    assert res[1][0][0][2] > 0 and res[0][0][0][2] > 0  # rows crossed in both directions
 
 
 # ---- GPU ------------------------------------------------------------------------------------
@@ -121,7 +125,7 @@ def gpu_tables():
 
 
 def _split_rows(pb, cuts):
-    """Row ranges of one PairBatch as separate PairBatches (one per virtual rank)."""
+    """Row ranges of one PairBatch as separate PairBatches."""
     from lddl_amd.pairs import PairBatch
     out = []
     for a, z in zip(cuts[:-1], cuts[1:]):
@@ -135,34 +139,38 @@ def _split_rows(pb, cuts):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('W,S', [(1, 1), (2, 2), (4, 4), (8, 8), (8, 24), (3, 5)])
-def test_balance_virtual_gpu(gpu_tables, W, S):
-    """W virtual ranks on one GPU, HIP kernels: uneven row splits (skewed so that rows must
-    move), checked against the invariants and, for the concatenated order, the oracle."""
+@pytest.mark.parametrize('W,S,T', [(1, 1, 1), (1, 8, 3), (2, 2, 2), (4, 4, 1), (8, 8, 2),
+                                   (8, 24, 1), (3, 5, 3)])
+def test_stream_virtual_gpu(gpu_tables, W, S, T):
+    """W virtual ranks x T batches on one GPU, HIP kernels: skewed row splits (rows must move),
+    checked against the deal contract; bin totals against the oracle's stable bin order."""
     from oracle import oracle as O
     from lddl_amd.balance import HipOps
     ctx, pb = gpu_tables
     n = pb.n_pairs
-    w = np.arange(1, W + 1, dtype=np.float64) ** 2
+    w = np.tile(np.arange(1, W + 1, dtype=np.float64) ** 2, T)
     cuts = np.concatenate([[0], np.round(np.cumsum(w) / w.sum() * n)]).astype(np.int64)
-    pbs = _split_rows(pb, cuts)
+    parts = _split_rows(pb, cuts)
+    batches = [parts[t * W:(t + 1) * W] for t in range(T)]
     ops = HipOps(ctx)
-    outs = balance_virtual(ops, pbs, 8, 64, num_shards=S)
-    hosts = [p.to_host() for p in pbs]
-    check_balanced(hosts, [_to_host_out(o, ops) for o in outs], 8, 64, S)
-    # the oracle's stable bin order of the whole (rank-major) table is what the ranks hold
+    outs = stream_virtual(ops, batches, 8, 64, num_shards=S)
+    check_stream([[p.to_host() for p in pbs] for pbs in batches],
+                 [[_to_host_out(o, ops) for o in os_] for os_ in outs], 8, 64, S)
     nt = np.diff(pb.tok_off.cpu().numpy()) + 3
     eb, eo, ec = O.bin_samples(nt.astype(np.int32), 8, 64)
-    assert sum(o.n_rows for o in outs) == n
-    np.testing.assert_array_equal(sum(np.diff(o.bin_off) for o in outs), ec)
+    assert sum(o.n_rows for os_ in outs for o in os_) == n
+    np.testing.assert_array_equal(sum(np.diff(o.bin_off) for os_ in outs for o in os_), ec)
+    for os_ in outs:
+        for o in os_:
+            assert o.n_tokens == int(_to_host_out(o, ops)[0]['tok_off'][-1])
     if W > 1:
-        assert sum(o.moved_rows for o in outs) > 0
+        assert sum(o.moved_rows for os_ in outs for o in os_) > 0
 
 
 @pytest.mark.gpu
 def test_balance_world1_no_copy(gpu_tables):
-    """World size 1 (collective driver without a process group): a row order over the table,
-    nothing packed or moved; equal to the oracle's stable bin order."""
+    """World size 1, one shard (collective driver without a process group): a row order over the
+    table, nothing packed or moved; equal to the oracle's stable bin order."""
     from oracle import oracle as O
     ctx, pb = gpu_tables
     bb = balance(ctx, pb, 8, 64)
@@ -171,5 +179,5 @@ def test_balance_world1_no_copy(gpu_tables):
     eb, eo, ec = O.bin_samples(nt.astype(np.int32), 8, 64)
     np.testing.assert_array_equal(bb.rows.cpu().numpy(), eo)
     np.testing.assert_array_equal(np.diff(bb.bin_off), ec)
-    np.testing.assert_array_equal(bb.bin_ids().cpu().numpy(), eb[eo])
+    np.testing.assert_array_equal(bb.bin_ids(), eb[eo])
     assert bb.n_tokens == int(pb.tokens.numel())

@@ -168,3 +168,63 @@ def test_pack_token_counts_match_str_split():
         b = _canon(s)
         assert b.split() == [t.encode('utf-8') for t in s.split()], repr(s)
         assert _ntok(b) == len(s.split()), repr(s)
+
+
+def test_sampled_out_malformed_line_still_raises(tmp_path):
+    """dask.bag.read_text decodes the whole block strictly, so a malformed line raises even when
+    random_sample would drop it: the GPU path's bytes reader decodes the lines it
+    samples out on the host (the kept ones go to lddl_utf8_check)."""
+    f = tmp_path / 'a.txt'
+    lines = [b'wiki-%d good text %d' % (i, i) for i in range(200)]
+    bad = 57
+    lines[bad] = b'wiki-57 bad \xff\xfe text'
+    f.write_bytes(b'\n'.join(lines) + b'\n')
+    for seed in range(100):  # a seed whose sample drops the malformed line
+        blocks = R.plan_blocks(str(tmp_path), None, sample_ratio=0.5, sample_seed=seed)
+        r = __import__('random').Random()
+        r.setstate(blocks[0].state)
+        if [r.random() < 0.5 for _ in lines][bad] is False:
+            break
+    with pytest.raises(UnicodeDecodeError):
+        R.read_block(blocks[0], as_bytes=False)
+    with pytest.raises(UnicodeDecodeError):
+        R.read_block(blocks[0], as_bytes=True)
+
+
+def test_txt_output_matches_reference_writer(tmp_path):
+    """--output-format txt: the CLI's writer (pretrain.write_txt / _txt_line) against the files the
+    REFERENCE's own `_save_txt` wrote (pretrain.py:501-531; to_textfiles / to_textfiles_binned,
+    binning.py:439-509) for the same rows (tests/golden/make_txt_golden.py): names and bytes."""
+    import base64
+    import json
+    from conftest import GOLDEN
+    from lddl_amd.dask.bert import pretrain as P
+
+    class Rows:  # the Rendered.row() interface write_txt reads
+        def __init__(self, rows):
+            self.rows = rows
+
+        def row(self, r):
+            return self.rows[r]
+    with open(os.path.join(GOLDEN, 'txt_output.json')) as f:
+        cases = json.load(f)
+    for c in cases:
+        nbins = c['seq'] // c['bin_size'] if c['bin_size'] else None
+        rows, part_rows, counts = [], [0], []
+        for prows in c['partitions']:
+            prows = [dict(r, masked_lm_positions=base64.b64decode(r['masked_lm_positions']))
+                     if 'masked_lm_positions' in r else r for r in prows]
+            if nbins:  # the GPU path hands write_txt each partition's rows bin after bin (stable)
+                b = np.minimum((np.asarray([r['num_tokens'] for r in prows], np.int64) - 1) //
+                               c['bin_size'], nbins - 1)
+                prows = [prows[i] for i in np.argsort(b, kind='stable')]
+                counts.append(np.bincount(b, minlength=nbins))
+            rows += prows
+            part_rows.append(len(rows))
+        out = tmp_path / c['name']
+        out.mkdir()
+        n_part = len(c['partitions'])
+        P.write_txt(str(out), Rows(rows), np.asarray(part_rows), list(range(n_part)), c['masking'],
+                    nbins, np.asarray(counts) if nbins else None, n_part)
+        got = {fn: (out / fn).read_text() for fn in sorted(os.listdir(out))}
+        assert got == c['files'], c['name']

@@ -280,41 +280,63 @@ def test_pretrain_cli_txt_output(tmp_path, binned):
 
 @pytest.mark.parametrize('binned,masking', [(True, True), (False, False)])
 def test_pretrain_cli_num_shards_balanced(tmp_path, binned, masking):
-    """--num-shards: the balancer's layout straight from HBM (shard-<k>.parquet[_<b>], N or N+1
-    samples per bin, .num_samples.json) holding exactly the rows of the part.* output of the
-    same run; then get_bert_pretrain_data_loader consumes it."""
+    """--num-shards (stream plan): shard s of bin b holds exactly the rows g = s (mod S) of bin
+    b's global order — the part.* rows of the same run, partitions in order — in that order, N or
+    N+1 per shard, with .num_samples.json; the files are identical when the corpus streams
+    through the GPU in four batches; then get_bert_pretrain_data_loader consumes them."""
     import logging
-    from collections import Counter
     from lddl_amd.torch import get_bert_pretrain_data_loader
-    extra = ['--bin-size', '32'] if binned else []
     from lddl_amd.dask.bert import pretrain as P
+    extra = (['--bin-size', '32'] if binned else []) + ['--shuffle-group-bytes', '1']
     args = _cli(tmp_path, tmp_path / 'parts', extra, masking=masking)
     _cli(tmp_path, tmp_path / 'shards', extra + ['--num-shards', '4'], masking=masking)
+    _cli(tmp_path, tmp_path / 'shards_b', extra + ['--num-shards', '4', '--gpu-batch-bytes', '1'],
+         masking=masking)
     nb = 4 if binned else 1
+    n_part = len(P.plan_partitions(args))
+    assert len(P.rank_batches(P.attach_args().parse_args(
+        ['--sink', 'x', '--gpu-batch-bytes', '1', '--shuffle-group-bytes', '1']),
+        P.plan_partitions(args))) == n_part  # one batch per partition in shards_b
     ns = json.loads((tmp_path / 'shards' / '.num_samples.json').read_text())
-    want_rows, got_rows = Counter(), Counter()
-    for p in range(len(P.plan_partitions(args))):
-        for b in range(nb):
-            fn = 'part.{}.parquet{}'.format(p, '_{}'.format(b) if binned else '')
-            for r in pq.read_table(tmp_path / 'parts' / fn).to_pylist():
-                want_rows[tuple(sorted(r.items()))] += 1
+    assert ns == json.loads((tmp_path / 'shards_b' / '.num_samples.json').read_text())
+    assert len(ns) == 4 * nb
     for b in range(nb):
+        sfx = '_{}'.format(b) if binned else ''
+        glob = [r for p in range(n_part)
+                for r in pq.read_table(tmp_path / 'parts' / 'part.{}.parquet{}'.format(p, sfx)).to_pylist()]
         counts = []
         for s in range(4):
-            fn = 'shard-{}.parquet{}'.format(s, '_{}'.format(b) if binned else '')
+            fn = 'shard-{}.parquet{}'.format(s, sfx)
             t = pq.read_table(tmp_path / 'shards' / fn)
             assert ns[fn] == t.num_rows
+            assert t.to_pylist() == glob[s::4]
+            assert pq.read_table(tmp_path / 'shards_b' / fn).to_pylist() == glob[s::4]
             counts.append(t.num_rows)
-            for r in t.to_pylist():
-                if binned:
-                    assert r['bin_id'] == b
-                got_rows[tuple(sorted(r.items()))] += 1
         assert max(counts) - min(counts) <= 1
-    assert got_rows == want_rows
-    assert len(ns) == 4 * nb
     dl = get_bert_pretrain_data_loader(
         str(tmp_path / 'shards'), vocab_file=VOCAB_UNCASED,
         data_loader_kwargs={'batch_size': 16, 'num_workers': 2}, log_level=logging.WARNING)
     n = sum(batch['input_ids'].size(0) for batch in dl)
     # the loader evens out files to the smallest count per bin (lost-samples rule)
     assert sum(ns.values()) - 4 * nb <= n <= sum(ns.values())
+
+
+def test_pretrain_cli_num_shards_reference_plan(tmp_path):
+    """--balance-plan reference: the part files balanced by balance_dask_output in place — the
+    reference's shard layout (its plans are pinned by tests/golden/balance.json)."""
+    import shutil
+    from lddl_amd.dask import load_balance as LB
+    extra = ['--bin-size', '32']
+    _cli(tmp_path, tmp_path / 'parts', extra)
+    ref = tmp_path / 'ref'
+    shutil.copytree(tmp_path / 'parts', ref)
+    LB.main(LB.attach_args().parse_args(['--indir', str(ref), '--num-shards', '3']))
+    got = tmp_path / 'got'
+    _cli(tmp_path, got, extra + ['--num-shards', '3', '--balance-plan', 'reference'])
+    names = sorted(os.listdir(ref))
+    assert names == sorted(os.listdir(got))
+    assert not any(n.startswith('part.') for n in names)
+    for n in names:
+        if '.parquet' in n:
+            assert pq.read_table(got / n).to_pylist() == pq.read_table(ref / n).to_pylist()
+    assert (got / '.num_samples.json').read_text() == (ref / '.num_samples.json').read_text()
