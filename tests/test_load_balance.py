@@ -109,3 +109,47 @@ def test_generate_num_samples_cache(tmp_path):
     LB.generate_num_samples_cache(['--indir', str(tmp_path)])
     with open(tmp_path / '.num_samples.json') as f:
         assert json.load(f) == {'part.0.parquet_0': 3, 'part.1.parquet_0': 4}
+
+
+# ---- world size 2 (gloo): rank-striped footer reads + all_reduce, shard k written by rank k % 2
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _lb_worker(rank, world, port, indir, outdir, S):
+    os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    import torch.distributed as dist
+    LB.main(LB.attach_args().parse_args(['--indir', indir, '--outdir', outdir, '--num-shards',
+                                         str(S), '--keep-orig']))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('case', [c for c in _cases() if c['status'] == 'ok'],
+                         ids=lambda c: '{}-{}'.format(c['counts'], c['num_shards']))
+def test_cli_world2_matches_reference_plan(tmp_path, case):
+    """balance_dask_output under two gloo ranks writes the shards of the reference's plan
+    (tests/golden/balance.json, generated by the reference's _balance) with the rows in the
+    reference's order, whichever rank wrote them."""
+    import torch.multiprocessing as mp
+    counts, S = case['counts'], case['num_shards']
+    d, out = tmp_path / 'data', tmp_path / 'out'
+    d.mkdir()
+    uid = 0
+    for i, c in enumerate(counts):
+        pq.write_table(pa.table({'A': pa.array(['a{}'.format(u) for u in range(uid, uid + c)],
+                                               pa.string()),
+                                 'uid': pa.array(range(uid, uid + c), pa.int64())}),
+                       d / 'part.{}.parquet_0'.format(i))
+        uid += c
+    mp.spawn(_lb_worker, args=(2, _free_port(), str(d), str(out), S), nprocs=2, join=True)
+    with open(out / '.num_samples.json') as f:
+        js = json.load(f)
+    got = {k: pq.read_table(out / k).column('uid').to_pylist() for k in js}
+    assert got == case['shards']
+    assert js == {k: len(v) for k, v in case['shards'].items()}
