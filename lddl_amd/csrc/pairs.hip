@@ -110,6 +110,7 @@ __global__ void part_offsets_kernel(const int64_t* part_doc_off, int64_t n_part,
 // flow); only parallel phases (twist, temper, speculative shuffle draws) use the lanes.
 // ---------------------------------------------------------------------------------------------
 constexpr int kN = 624, kM = 397;
+constexpr int kLook = 64;  // MT words of look-ahead past the block (WaveRng)
 constexpr int64_t kPoolChunk = 4096;  // mask pool entries reserved per atomic
 
 __device__ inline int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -124,43 +125,16 @@ __device__ inline uint32_t temper(uint32_t y) {
   return y;
 }
 
-// kFyGuess.m[s0]: the expected rejection pattern of a 64-word Fisher-Yates window whose first
-// word is drawn for step s0 (fy_draws' starting point), built by walking the window with the
-// expected rejection rate 1 - u / 2^bit_length(u) of each bound u and rejecting a word whenever
-// the running expectation passes the next half integer. Only a starting guess: any pattern
-// converges to the same draws.
-constexpr int kFyGuessN = 512;
-struct FyGuess {
-  uint64_t m[kFyGuessN];
-};
-constexpr FyGuess make_fy_guess() {
-  FyGuess g{};
-  for (int s0 = 0; s0 < kFyGuessN; ++s0) {
-    uint64_t m = 0;
-    double r = 0.0;
-    int R = 0;
-    for (int t = 0; t < 64; ++t) {
-      const int u = s0 + 1 - t + R;
-      if (u <= 1) break;
-      int k = 0;
-      while ((1 << k) <= u) ++k;
-      r += 1.0 - (double)u / (double)(1 << k);
-      if (r >= R + 0.5) {
-        m |= 1ull << t;
-        ++R;
-      }
-    }
-    g.m[s0] = m;
-  }
-  return g;
-}
-__constant__ FyGuess kFyGuess = make_fy_guess();
 struct WaveRng {
-  uint32_t* mt;  // LDS raw state [624]
-  uint32_t* tw;  // unused (a tempered copy of the block in LDS cut occupancy: 7 KB -> 5 waves/SIMD)
-  int mti;       // next word of the block (uniform)
-  int wbase;     // window base (uniform)
-  int wend;      // min(wbase + 64, kN) while the window is valid, 0 when stale (uniform)
+  // LDS: the raw 624-word block followed by kLook words of look-ahead, the next block's first
+  // words (next[i] = twist1(cur[i], cur[i+1], cur[i+397]) for i < 227 depends on the current
+  // block alone). mti indexes that extended stream: a window starting at mti < 624 may read up to
+  // kLook words past it without a block check, and the twist runs when a window or a register
+  // refill starts at mti >= 624 (mti -= 624 afterwards).
+  uint32_t* mt;
+  int mti;       // next word (uniform), < kN + kLook
+  int wbase;     // register window base (uniform)
+  int wend;      // wbase + 64 while the register window is valid, 0 when stale (uniform)
   uint32_t win;  // this lane's tempered word temper(mt[wbase + lane])
 #ifdef LDDL_STAMPS
   uint64_t n_pass = 0, n_win = 0;  // diagnostics: Jacobi passes / Fisher-Yates windows
@@ -171,7 +145,7 @@ struct WaveRng {
     return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
   }
 
-  // regenerate + temper the block with all 64 lanes: three dependency-free phases
+  // regenerate the block with all 64 lanes (three dependency-free phases), then the look-ahead
   __device__ void twist() {
     const int l = threadIdx.x;
     for (int i = l; i < kN - kM; i += 64) {  // [0,227): old[i], old[i+1], old[i+397]
@@ -191,10 +165,14 @@ struct WaveRng {
     __syncthreads();
     if (l == 0) mt[kN - 1] = twist1(mt[kN - 1], mt[0], mt[kM - 1]);
     __syncthreads();
-    mti = 0;
-    wbase = 0;
-    wend = 64;
-    win = temper(mt[l]);
+    if (l < kLook) mt[kN + l] = twist1(mt[l], mt[l + 1], mt[l + kM]);
+    __syncthreads();
+    mti -= kN;
+    wbase = -1024;
+    wend = 0;
+  }
+  __device__ void ensure() {
+    if (mti >= kN) twist();
   }
 
   __device__ void seed_i64(int64_t seed) {  // random.seed(int): init_by_array(abs(seed) limbs)
@@ -229,19 +207,17 @@ struct WaveRng {
       mt[0] = 0x80000000u;
     }
     __syncthreads();
-    twist();  // CPython leaves index = N after seeding: the first draw twists
+    mti = kN;  // CPython leaves index = N after seeding: the first draw twists
+    wbase = -1024;
+    wend = 0;
   }
 
   // out of line: runs once per 64 draws (window load) or per 624 draws (twist)
   __device__ void refill() {
-    if (mti >= kN) {
-      twist();
-    } else {
-      wbase = uni(mti);
-      wend = uni(min(mti + 64, kN));
-      const int k = mti + (int)threadIdx.x;
-      win = k < kN ? temper(mt[k]) : 0u;
-    }
+    ensure();
+    wbase = mti;
+    wend = mti + 64;
+    win = temper(mt[mti + (int)threadIdx.x]);
   }
   __device__ uint32_t u32() {
     if (mti >= wend) refill();  // one scalar compare per draw
@@ -255,91 +231,65 @@ struct WaveRng {
   // rejected iff (w_t >> (32 - bit_length(i_t + 1))) > i_t, i.e. with u = i + 1 (the draw's
   // bound) iff (w_t >> clz(u)) >= u. R is the fixed point of R_t = #{v < t : rejected under
   // R_v}, found by Jacobi iteration on ballots: the recurrence is causal, so every pass fixes at
-  // least the first wrong word. The iteration starts from kFyGuess[s0], the rejection pattern a
-  // window starting at step s0 has when every word is rejected with its expected rate (fewer
-  // passes than starting from "no rejection"); any guess converges to the same fixed point.
-  // The pass is kept to one VALU compare + one scalar compare-and-branch: for s0 >= 64 every
-  // bound in the window is >= 2; a tail window clamps its bounds below 2 to "never rejected".
+  // least the first wrong word. Words past the last step (u <= 1) come after every valid word
+  // and do not affect their R; they are held "accepted" (a verdict that followed their R would
+  // keep changing and cost passes: 11.7 instead of ~5 per window), and the first of them ends
+  // the shuffle. The window's bookkeeping is vector work on wave-uniform values plus two
+  // scalar branches per pass, so the scalar unit (the binding pipe of this kernel) carries
+  // little of it.
   template <typename Sink>
-  __device__ void fy_draws(int64_t n, Sink sink) {
+  __device__ void fy_draws(int32_t n, Sink sink) {
     const int lane = threadIdx.x;
-    int32_t s0 = (int32_t)(n - 1);  // next step (uniform); n < 2^30 (host-checked)
+    int32_t s0 = n - 1;  // next step (uniform); n < 2^30 (host-checked)
     while (s0 >= 1) {
-      if (mti >= kN) twist();
-      const int L = min(64, kN - mti);
-      // lanes past the block end hold w = 0: x = 0 never reaches a bound >= 1
-      const uint32_t w = lane < L ? temper(mt[mti + lane]) : 0u;
+      ensure();
+      const uint32_t w = temper(mt[mti + lane]);
       const int32_t u1 = s0 + 1 - lane;
-      uint64_t rej = s0 < kFyGuessN ? kFyGuess.m[s0] : 0ull;
-      if (L < 64) rej &= (1ull << L) - 1;
-      int32_t R = (int32_t)popc_below(rej);
+      int32_t R = 0;
       uint32_t x;
-      if (s0 >= 64) {
-#ifndef LDDL_FY_NOASM
-        // the pass as 4 VALU + one scalar compare-and-branch (the compiler's form adds a
-        // select, an exec AND and a second branch per pass)
-        int32_t u;
-        asm volatile(
-            "s_branch 2f\n"
-            "1:\n\t"
-            "s_mov_b64 %[rej], vcc\n\t"
-            "v_mbcnt_lo_u32_b32 %[R], vcc_lo, 0\n\t"
-            "v_mbcnt_hi_u32_b32 %[R], vcc_hi, %[R]\n"
-            "2:\n\t"
-            "v_add_u32 %[u], %[u1], %[R]\n\t"
-            "v_ffbh_u32 %[x], %[u]\n\t"
-            "v_lshrrev_b32 %[x], %[x], %[w]\n\t"
-            "v_cmp_ge_u32 vcc, %[x], %[u]\n\t"
-            "s_cmp_eq_u64 vcc, %[rej]\n\t"
-            "s_cbranch_scc0 1b\n"
-            : [rej] "+s"(rej), [R] "+v"(R), [x] "=&v"(x), [u] "=&v"(u)
-            : [u1] "v"(u1), [w] "v"(w)
-            : "vcc", "scc");
-#else
+      uint64_t rej;
+      if (s0 >= 64) {  // every word of the window has a step
         while (true) {
           const int32_t u = u1 + R;  // >= 2
           x = w >> __clz((uint32_t)u);
-          const uint64_t bm = __builtin_amdgcn_uicmp(x, (uint32_t)u, 35 /* uge */);
+          rej = ballot(x >= (uint32_t)u);
+          const int32_t R2 = (int32_t)popc_below(rej);
 #ifdef LDDL_STAMPS
           ++n_pass;
 #endif
-          if (bm == rej) break;
-          rej = bm;
-          R = (int32_t)popc_below(rej);
+          if (ballot(R2 != R) == 0) break;
+          R = R2;
         }
-#endif
-      } else {
+      } else {  // words past the last step (u <= 1) are held "accepted", so they settle at once
         while (true) {
           const int32_t u = u1 + R;
-          // u <= 1 (past the last step): shift 31 keeps x <= 1 < the 0xFFFFFFFF threshold
-          const uint32_t sh = u > 1 ? (uint32_t)__clz((uint32_t)u) : 31u;
-          x = w >> sh;
-          const uint32_t thr = u > 1 ? (uint32_t)u : 0xFFFFFFFFu;
-          const uint64_t bm = __builtin_amdgcn_uicmp(x, thr, 35 /* uge */);
+          x = w >> (__clz((uint32_t)u) & 31);
+          rej = ballot(u > 1 && x >= (uint32_t)u);
+          const int32_t R2 = (int32_t)popc_below(rej);
 #ifdef LDDL_STAMPS
           ++n_pass;
 #endif
-          if (bm == rej) break;
-          rej = bm;
-          R = (int32_t)popc_below(rej);
+          if (ballot(R2 != R) == 0) break;
+          R = R2;
         }
       }
 #ifdef LDDL_STAMPS
       ++n_win;
 #endif
       const int32_t i = u1 + R - 1;
-      // words consumed: up to the first word past the last step (i < 1) or the window end
-      int E = L;
-      if (s0 < 64) {
-        const uint64_t fin = __builtin_amdgcn_sicmp(i, 1, 40 /* slt */) & (L >= 64 ? ~0ull : ((1ull << L) - 1));
-        if (fin) E = __ffsll((unsigned long long)fin) - 1;
+      const uint64_t fin = ballot(i < 1);
+      const bool acc = !((rej >> lane) & 1ull);
+      if (fin == 0) {  // every word of the window drawn for a step
+        if (acc) sink(i, x);
+        s0 -= 64 - __popcll(rej);
+        mti += 64;
+      } else {  // the shuffle ends in this window, at word E
+        const int E = __ffsll((unsigned long long)fin) - 1;
+        if (acc && lane < E) sink(i, x);
+        mti += E;
+        s0 = 0;
       }
-      if (lane < E && !((rej >> lane) & 1ull)) sink((int64_t)i, x);
-      const int nrej = __popcll(rej & (E >= 64 ? ~0ull : ((1ull << E) - 1)));
-      mti = uni(mti + E);
-      s0 = uni(s0 - (E - nrej));
     }
-    __syncthreads();
     wbase = -1024;
     wend = 0;  // the register window is stale
   }
@@ -347,28 +297,16 @@ struct WaveRng {
   // iff A is the longer side at that point, which has a closed form: with d = na - nb the first
   // |d| trims hit the longer side, then B and A alternate starting with B (ties trim B). Each
   // trim is from the front iff random() < 0.5, i.e. iff the first of its two words is < 2^31, so
-  // 64 trims resolve per wave pass with two ballots.
+  // 32 trims (64 words, the look-ahead) resolve per wave pass with two ballots.
   __device__ void trunc_draws(int32_t& na, int32_t& nb, int32_t max_num, int32_t& a_front,
                               int32_t& b_front) {
     const int32_t T = na + nb - max_num;
     if (T <= 0) return;
     const int32_t d = na - nb, ad = d < 0 ? -d : d;
     const int lane = threadIdx.x;
-    int32_t done = 0;
-    while (done < T) {
-      if (mti >= kN) twist();
-      const int pairs = (kN - mti) >> 1;
-      if (pairs == 0) {  // the trim's two words straddle the block end
-        wbase = -1024;
-        wend = 0;
-        const int32_t front = below_half() ? 1 : 0;
-        const bool sa = done < d || (done >= ad && ((done - ad) & 1));
-        if (sa) a_front += front;
-        else b_front += front;
-        ++done;
-        continue;
-      }
-      const int cnt = min(min(T - done, pairs), 64);
+    for (int32_t done = 0; done < T;) {
+      ensure();
+      const int32_t cnt = min(T - done, 32);
       const int32_t t = done + lane;
       const bool front = lane < cnt && temper(mt[mti + 2 * lane]) < 0x80000000u;
       const bool sa = t < d || (t >= ad && ((t - ad) & 1));
@@ -386,10 +324,10 @@ struct WaveRng {
 
   // Decisions of create_masked_lm_predictions (pretrain.py:208-221) for cnt masked tokens:
   // random() < 0.8 -> [MASK]; else random() < 0.5 -> keep; else vocab_words[randint(0, V-1)].
-  // Lane t tabulates the decision and word count of a token whose first word is mti + t; the
-  // chain of decision starts p_0 = 0, p_{k+1} = p_k + len[p_k] is then resolved for every k at
-  // once by pointer doubling (ds_bpermute), so lane k learns where decision k starts. A table
-  // entry that would read past the MT block is left empty and that token is drawn the scalar way.
+  // Lane t tabulates the decision and word count of a token whose first word is mti + t (only
+  // decisions whose words lie in the 64-word look-ahead); the chain of decision starts p_0 = 0,
+  // p_{k+1} = p_k + len[p_k] is then resolved for every k at once by pointer doubling
+  // (ds_bpermute), so lane k learns where decision k starts (a window holds <= 32 decisions).
   // cnt <= 64; returns decision `lane` in each lane < cnt.
   __device__ int32_t mask_decisions(int cnt, uint64_t lt08, int32_t V, int32_t mask_id) {
     const int lane = threadIdx.x;
@@ -397,70 +335,62 @@ struct WaveRng {
     int32_t res = 0;
     int c = 0;
     while (c < cnt) {
-      if (mti >= kN) twist();
-      const int avail = kN - mti;
-      int len = 0;
-      int32_t tok = 0;
-      {
-        // mask / keep decided for every lane without branches (words past the block are read
-        // from the LDS after it and never used); only the random-token lanes loop
-        const uint32_t w0 = temper(mt[mti + lane]), w1 = temper(mt[mti + lane + 1]),
-                       w2 = temper(mt[mti + lane + 2]);
-        const uint64_t N = ((uint64_t)(w0 >> 5) << 26) | (w1 >> 6);
-        const bool is_mask = lane + 1 < avail && N < lt08;
-        const bool v3 = lane + 3 < avail;
-        const bool is_keep = !is_mask && v3 && w2 < 0x80000000u;
-        len = is_mask ? 2 : is_keep ? 4 : 0;
-        tok = is_mask ? mask_id : kKeep;
-        if (v3 && !is_mask && !is_keep) {
-          for (int j = lane + 4; j < avail; ++j) {
-            const uint32_t r = temper(mt[mti + j]) >> (32 - kV);
-            if (r < (uint32_t)V) {
-              len = j + 1 - lane;
-              tok = (int32_t)r;
-              break;
-            }
+      ensure();
+      const uint32_t* wp = mt + mti + lane;  // (lane 63's third word is one past the look-ahead)
+      const uint32_t w0 = temper(wp[0]), w1 = temper(wp[1]), w2 = temper(wp[2]);
+      const uint64_t N = ((uint64_t)(w0 >> 5) << 26) | (w1 >> 6);
+      const bool is_mask = lane + 2 <= kLook && N < lt08;
+      const bool v3 = lane + 4 <= kLook;
+      const bool is_keep = !is_mask && v3 && w2 < 0x80000000u;
+      int len = is_mask ? 2 : is_keep ? 4 : 0;
+      int32_t tok = is_mask ? mask_id : kKeep;
+      if (v3 && !is_mask && !is_keep) {  // the random-token lanes scan for randint's word
+        for (int j = 4; lane + j < kLook; ++j) {
+          const uint32_t r = temper(wp[j]) >> (32 - kV);
+          if (r < (uint32_t)V) {
+            len = j + 1;
+            tok = (int32_t)r;
+            break;
           }
         }
       }
       // J_b[t] = start after 2^b decisions from t (64: stop, absorbing)
-      int Jd[6];
+      int Jd[5];
       Jd[0] = len ? min(lane + len, 64) : 64;
 #pragma unroll
-      for (int b = 1; b < 6; ++b) {
+      for (int b = 1; b < 5; ++b) {
         const int y = __shfl(Jd[b - 1], Jd[b - 1] & 63, 64);
         Jd[b] = Jd[b - 1] >= 64 ? 64 : y;
       }
-      int p = 0;  // start of decision `lane`
+      int p = 0;  // start of decision `lane` (lanes < 32)
 #pragma unroll
-      for (int b = 0; b < 6; ++b) {
+      for (int b = 0; b < 5; ++b) {
         const int t = __shfl(Jd[b], p & 63, 64);
         if ((lane >> b) & 1) p = p >= 64 ? 64 : t;
       }
       const int lp = __shfl(len, p & 63, 64);
       const int32_t tp = __shfl(tok, p & 63, 64);
-      const uint64_t okm = ballot(p < 64 && lp > 0);  // a prefix of the lanes
-      int take = okm == ~0ull ? 64 : __ffsll((unsigned long long)~okm) - 1;
+      const uint64_t okm = ballot(lane < 32 && p < 64 && lp > 0);  // a prefix of the lanes
+      int take = __ffsll((unsigned long long)~okm) - 1;
       if (take > cnt - c) take = cnt - c;
       const int32_t tk = __shfl(tp, (lane - c) & 63, 64);  // decision k goes to lane c + k
       if (lane >= c && lane < c + take) res = tk;
-      int pos = 0;
-      if (take > 0) pos = (int)rdlane((uint32_t)p, take - 1) + (int)rdlane((uint32_t)lp, take - 1);
-      mti = uni(mti + pos);
-      c += take;
-      wbase = -1024;
-      wend = 0;
-      if (c < cnt && pos < 64) {  // the next decision's words straddle the block end
+      if (take > 0) {
+        mti = uni(mti + (int)rdlane((uint32_t)p, take - 1) + (int)rdlane((uint32_t)lp, take - 1));
+        c += take;
+      } else {  // the first decision needs words past the look-ahead: draw it word by word
+        wbase = -1024;
+        wend = 0;
         int32_t t2;
         if (rand53() < lt08) t2 = mask_id;
         else if (below_half()) t2 = kKeep;
         else t2 = (int32_t)randint(0, V - 1);
         if (lane == c) res = t2;
         ++c;
-        wbase = -1024;
-        wend = 0;
       }
     }
+    wbase = -1024;
+    wend = 0;
     return res;
   }
 
@@ -648,8 +578,7 @@ __device__ inline void densify_group(int64_t k0, const int64_t* __restrict__ ks_
 __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* s_mt = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* s_tw = nullptr;
-  int32_t* s_doc = reinterpret_cast<int32_t*>(s_mt + kN);  // [kDocLds + 1]
+  int32_t* s_doc = reinterpret_cast<int32_t*>(s_mt + kN + kLook);  // [kDocLds + 1]
   const int p = blockIdx.x;
   const int lane = threadIdx.x;
   const bool leader = lane == 0;
@@ -669,7 +598,7 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
 #ifdef LDDL_STAMPS
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  WaveRng rng{s_mt, s_tw, 0, 0, 0u
+  WaveRng rng{s_mt, 0, 0, 0, 0u
 #ifdef LDDL_STAMPS
               , 0, 0
 #endif
@@ -1939,7 +1868,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   A.tl = d_tl;
 #endif
   if (prm->seq > 512) TRY((set_error("replay planner supports target_seq_length <= 512"), -1));
-  const size_t lds = 4 * kN + 4 * (kDocLds + 4) + 16;  // ~4.5 KB: 8 waves/SIMD fit the CU's LDS
+  const size_t lds = 4 * (kN + kLook) + 4 * (kDocLds + 4) + 16;  // ~4.8 KB: 7 waves/SIMD fit
   A.joff = joff;
   A.ncand = ncand;
   // pools: decisions (int32, shuffled order) and shuffle draws (uint16), sized from the kept
