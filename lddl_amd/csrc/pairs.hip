@@ -336,16 +336,24 @@ struct WaveRng {
     int c = 0;
     while (c < cnt) {
       ensure();
-      const uint32_t* wp = mt + mti + lane;  // (lane 63's third word is one past the look-ahead)
-      const uint32_t w0 = temper(wp[0]), w1 = temper(wp[1]), w2 = temper(wp[2]);
+      // word t + j of the window reaches lane t by j whole-wave DPP shifts (one LDS read and one
+      // temper per lane); only words inside the look-ahead are used
+      const uint32_t* wp = mt + mti + lane;
+      const uint32_t w0 = temper(wp[0]);
+      const uint32_t w1 = (uint32_t)wave_next((int)w0), w2 = (uint32_t)wave_next((int)w1),
+                     w3 = (uint32_t)wave_next((int)w2), w4 = (uint32_t)wave_next((int)w3);
+      (void)w3;
       const uint64_t N = ((uint64_t)(w0 >> 5) << 26) | (w1 >> 6);
       const bool is_mask = lane + 2 <= kLook && N < lt08;
       const bool v3 = lane + 4 <= kLook;
       const bool is_keep = !is_mask && v3 && w2 < 0x80000000u;
-      int len = is_mask ? 2 : is_keep ? 4 : 0;
-      int32_t tok = is_mask ? mask_id : kKeep;
-      if (v3 && !is_mask && !is_keep) {  // the random-token lanes scan for randint's word
-        for (int j = 4; lane + j < kLook; ++j) {
+      const bool is_rand = v3 && !is_mask && !is_keep;
+      const uint32_t r4 = w4 >> (32 - kV);
+      const bool rand4 = is_rand && lane + 5 <= kLook && r4 < (uint32_t)V;  // randint's 1st word
+      int len = is_mask ? 2 : is_keep ? 4 : rand4 ? 5 : 0;
+      int32_t tok = is_mask ? mask_id : rand4 ? (int32_t)r4 : kKeep;
+      if (is_rand && !rand4) {  // randint rejected its first word: scan on (rare)
+        for (int j = 5; lane + j < kLook; ++j) {
           const uint32_t r = temper(wp[j]) >> (32 - kV);
           if (r < (uint32_t)V) {
             len = j + 1;
