@@ -720,7 +720,7 @@ def main():
         torch.cuda.synchronize()
         tok_ms = e0.elapsed_time(e1)
         sent_len = [sl]
-    pieces = sum(int((sl & ((1 << 30) - 1)).sum()) for sl in sent_len)
+    pieces = sum(int((sl.cpu().numpy() & ((1 << 30) - 1)).sum(dtype=np.int64)) for sl in sent_len)
     bal_ms = None
     if stream:  # one more, untimed step with the balance phases timed (summed over sub-batches)
         diag['balance'] = {}

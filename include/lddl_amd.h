@@ -51,6 +51,30 @@ int64_t lddl_synth_doc_text(uint64_t seed, int64_t doc_begin, int64_t target_byt
                             int64_t doc_cap, int64_t* n_doc_out, int n_threads);
 
 /* ---------------------------------------------------------------------------------------------
+ * Host reader of the preprocessor input (host-only, no GPU): replaces the per-line Python of
+ * dask.bag.read_text + random_sample (lddl/dask/readers.py:60-71), split_id_text (readers.py
+ * :131-136) and the document shuffle (lddl/dask/bert/pretrain.py:100-111, here per shuffle group
+ * with CPython's Random(seed).shuffle) for a batch of blocks, in threads.
+ * lddl_read_groups: block i = bytes [starts[i], ends[i]) of file paths[i]; mt_states (may be NULL:
+ *   no sampling) holds 625 words per block (the 624-word random_sample state + its index); a line
+ *   (block split on '\n', str.strip()ed, empty dropped) is kept iff random() < ratio. Blocks are
+ *   grouped into shuffle groups by group_off[n_groups+1]; group g's documents are shuffled by
+ *   random.Random(s).shuffle with abs(s) = group_seed_abs[g] and dealt back over its blocks (each
+ *   keeps its count). Every block must be valid UTF-8 (dask decodes blocks strictly): else
+ *   returns -2 with bad[0] = block, bad[1] = byte offset in the block. On success *n_docs
+ *   documents of *n_text bytes (the text after each line's id) are held by *out.
+ * lddl_read_fill: text[n_text], doc_off[n_docs+1], block_ndocs[n_blocks] (may be NULL), in block
+ *   order. lddl_read_free releases the handle.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct lddl_reader lddl_reader;
+int lddl_read_groups(int64_t n_blocks, const char* const* paths, const int64_t* starts,
+                     const int64_t* ends, const uint32_t* mt_states, double ratio, int64_t n_groups,
+                     const int64_t* group_off, const uint64_t* group_seed_abs, int n_threads,
+                     lddl_reader** out, int64_t* n_docs, int64_t* n_text, int64_t* bad);
+int lddl_read_fill(lddl_reader* reader, uint8_t* text, int64_t* doc_off, int64_t* block_ndocs);
+int lddl_read_free(lddl_reader* reader);
+
+/* ---------------------------------------------------------------------------------------------
  * Context = device-resident tokenizer tables.
  * Replaces `transformers.BertTokenizerFast(vocab_file)` (lddl/dask/bert/pretrain.py:584-587,
  * lddl/torch/bert.py:343-346). `norm_table` is lddl_amd/assets/bert_norm_{uncased,cased}.bin

@@ -25,6 +25,10 @@ SIGNATURES = {
     'lddl_version': (ctypes.c_int, []),
     'lddl_synth_corpus': (c_i64, [c_u64, c_i64, c_i64, c_dbl, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                                   c_i64p, c_i64p, ctypes.c_int]),
+    'lddl_read_groups': (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_dbl, c_i64, c_vp, c_vp,
+                                        ctypes.c_int, ctypes.POINTER(c_vp), c_i64p, c_i64p, c_vp]),
+    'lddl_read_fill': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
+    'lddl_read_free': (ctypes.c_int, [c_vp]),
     'lddl_ctx_create': (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_vp, c_i64,
                                        ctypes.POINTER(c_vp)]),
     'lddl_ctx_destroy': (ctypes.c_int, [c_vp]),

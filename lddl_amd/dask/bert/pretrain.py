@@ -112,6 +112,16 @@ def rank_batches(args, blocks, rank=0, world=1):
     return _greedy(groups, lambda g: sum(blocks[p].nbytes for p in g), args.gpu_batch_bytes)
 
 
+def n_gpu_batches(args, blocks, rank=0, world=1):
+    """GPU batches of `rank` (iter_doc_batches / iter_batches): the read batches of whole
+    shuffle groups, the GPU path's cut into runs of <= --gpu-batch-bytes of input."""
+    rb = rank_batches(args, blocks, rank, world)
+    if args.sentence_splitter == 'host':
+        return len(rb)
+    return sum(len(_greedy([p for g in b for p in g], lambda p: blocks[p].nbytes,
+                           args.gpu_batch_bytes)) for b in rb)
+
+
 def iter_batches(args, rank=0, world=1, blocks=None, as_bytes=False):
     """This rank's partitions in GPU batches, read lazily: yields [(p, lines)] per batch. The
     documents of each shuffle group are shuffled over the group's partitions (each keeps its
@@ -130,6 +140,31 @@ def iter_batches(args, rank=0, world=1, blocks=None, as_bytes=False):
                 out.append((p, docs[k:k + len(lines)]))
                 k += len(lines)
         yield out
+
+
+def iter_doc_batches(args, rank=0, world=1, blocks=None):
+    """The GPU-segmentation path's input: this rank's partitions as (partitions, corpus) GPU
+    batches, corpus = build_doc_corpus's ('documents', text, doc_off, part_doc_off). Whole shuffle
+    groups are read by the library's host reader (readers.read_groups_native: the same lines,
+    sampling, per-group document shuffle and split_id_text as iter_batches + build_doc_corpus, in
+    C++ threads), then cut into GPU batches of <= --gpu-batch-bytes of input (whole partitions),
+    so the GPU work, the rendering and the file writes of consecutive batches overlap."""
+    blocks = plan_partitions(args) if blocks is None else blocks
+    for batch in rank_batches(args, blocks, rank, world):
+        text, doc_off, nd = readers.read_groups_native(
+            [[blocks[p] for p in g] for g in batch],
+            [partition_seed(args.seed, -1 - g[0]) for g in batch],
+            threads=getattr(args, 'read_threads', 16))
+        parts = [p for g in batch for p in g]
+        pdo = np.zeros(len(parts) + 1, np.int64)
+        np.cumsum(nd, out=pdo[1:])
+        for sub in _greedy(list(range(len(parts))), lambda i: blocks[parts[i]].nbytes,
+                           args.gpu_batch_bytes):
+            i0, i1 = sub[0], sub[-1] + 1
+            d0, d1 = int(pdo[i0]), int(pdo[i1])
+            t0, t1 = int(doc_off[d0]), int(doc_off[d1])
+            yield ([(parts[i], None) for i in range(i0, i1)],
+                   ('documents', text[t0:t1], doc_off[d0:d1 + 1] - t0, pdo[i0:i1 + 1] - d0))
 
 
 def get_partitions(args, rank=0, world=1):
@@ -246,33 +281,68 @@ def make_batch_pairs(ctx, args, partitions, corpus, timer=None):
     return pb
 
 
-def process_batch(ctx, args, partitions, corpus, outdir, timer=None, executor=None, futures=None):
+def process_batch(ctx, args, partitions, corpus, outdir, timer=None, executor=None, futures=None,
+                  copier=None):
     """Run the GPU hot path over a group of partitions and write their files (concurrently on
-    `executor` when given: the futures go to `futures`)."""
+    `executor` when given: the futures go to `futures`). With a `copier` (one host thread), the
+    rendered columns are copied to the host and handed to the writers there, so this batch's
+    copy and writes overlap the next batch's GPU work; the returned future yields the paths."""
     from ... import output
     tm = timer or (lambda name: None)
+    index = [p for p, _ in partitions]
+    _trace('gpu_start', index[0])
     pb = make_batch_pairs(ctx, args, partitions, corpus, timer)
     part_rows = pb.part_off.cpu().numpy()
-    index = [p for p, _ in partitions]
     if args.bin_size is not None:
         import torch
         nbins = args.target_seq_length // args.bin_size
         nt = ((pb.tok_off[1:] - pb.tok_off[:-1]) + 3).to(torch.int32)
         perm, bin_id, counts = output.bin_partitions(ctx, nt, pb.part_off, args.bin_size, nbins)
-        rd = output.render(ctx, pb, perm, bin_id)
+        drd = output.render_device(ctx, pb, perm, bin_id)
         counts = counts.cpu().numpy()
     else:
         nbins, counts = None, None
-        rd = output.render(ctx, pb)
+        drd = output.render_device(ctx, pb)
+    del pb
     tm('render')
-    if args.output_format == 'parquet':
-        paths = output.write_parquet(outdir, rd, part_rows, index, args.masking, nbins, counts,
-                                     executor=executor, futures=futures)
-    else:
-        paths = write_txt(outdir, rd, part_rows, index, args.masking, nbins, counts,
-                          getattr(args, 'n_partitions', len(part_rows) - 1))
+
+    _trace('render_device', index[0])
+
+    def finish(stream=None):
+        _trace('d2h_start', index[0])
+        rd = drd.to_host(stream)
+        _trace('d2h_end', index[0])
+        if args.output_format == 'parquet':
+            return output.write_parquet(outdir, rd, part_rows, index, args.masking, nbins,
+                                        counts, executor=executor, futures=futures)
+        return write_txt(outdir, rd, part_rows, index, args.masking, nbins, counts,
+                         getattr(args, 'n_partitions', len(part_rows) - 1))
+    if copier is not None and args.output_format == 'parquet':
+        return copier.submit(finish, _copy_stream(ctx))
+    paths = finish()
     tm('write')
     return paths
+
+
+_T0 = time.perf_counter()
+_TRACE = os.environ.get('LDDL_TRACE_PIPELINE')
+
+
+def _trace(what, batch):
+    """LDDL_TRACE_PIPELINE=1: host timeline of the CLI pipeline on stderr (diagnostics)."""
+    if _TRACE:
+        import threading
+        sys.stderr.write('[pipe] %8.3f %-14s batch@%s %s\n' % (time.perf_counter() - _T0, what,
+                                                               batch,
+                                                               threading.current_thread().name))
+
+
+def _copy_stream(ctx):
+    import torch
+    s = getattr(ctx, '_copy_stream', None)
+    if s is None:
+        s = ctx._copy_stream = torch.cuda.Stream(device=ctx.device)
+    return s
 
 
 def _txt_line(row, masking):
@@ -330,7 +400,7 @@ class ShardWriters:
     def __init__(self, outdir, nbins, binned, masking, pool):
         self.outdir, self.nbins, self.binned, self.masking, self.pool = (outdir, nbins, binned,
                                                                          masking, pool)
-        self.writers, self.pending, self.shards = {}, [], set()
+        self.writers, self.pending, self.shards, self.jobs = {}, [], set(), []
 
     def name(self, s, b):
         return os.path.join(self.outdir, 'shard-{}.parquet{}'.format(
@@ -346,27 +416,40 @@ class ShardWriters:
                                                      compression=output.DEFAULT_COMPRESSION)
         w.write_table(t)
 
-    def add(self, ctx, bb):
-        """Render this batch's rows of the rank's shards (GPU) and queue their writes."""
+    def add(self, ctx, bb, copier=None):
+        """Render this batch's rows of the rank's shards (GPU) and queue their writes. With a
+        `copier` thread, the host copy and the queueing run there (in batch order: a batch's
+        appends are queued after the previous batch's have finished), overlapping the next
+        batch's GPU work."""
         from ... import output
         self.shards.update(bb.shards)
-        for f in self.pending:
-            f.result()
-        self.pending = []
         if bb.n_rows == 0:
             return
-        rd = output.render(ctx, bb.table, bb.rows, bb.bin_ids() if self.binned else None)
-        for m, s in enumerate(bb.shards):
-            for b in range(self.nbins):
-                r0, r1 = bb.shard_range(m, b)
-                if r1 > r0:
-                    self.pending.append(self.pool.submit(self._append, (s, b), rd, r0, r1))
+        drd = output.render_device(ctx, bb.table, bb.rows, bb.bin_ids() if self.binned else None)
+        ranges = [(s, b) + tuple(bb.shard_range(m, b)) for m, s in enumerate(bb.shards)
+                  for b in range(self.nbins)]
+
+        def job(stream=None):
+            rd = drd.to_host(stream)
+            for f in self.pending:
+                f.result()
+            self.pending = [self.pool.submit(self._append, (s, b), rd, r0, r1)
+                            for s, b, r0, r1 in ranges if r1 > r0]
+        if copier is None:
+            job()
+            return
+        while len(self.jobs) >= 2:
+            self.jobs.pop(0).result()
+        self.jobs.append(copier.submit(job, _copy_stream(ctx)))
 
     def close(self):
         """Finish the writes; shards of a bin that received no rows get an empty file (every bin
         has all shards, as the loader requires)."""
         import pyarrow.parquet as pq
         from ... import output
+        for j in self.jobs:
+            j.result()
+        self.jobs = []
         for f in self.pending:
             f.result()
         self.pending = []
@@ -447,7 +530,7 @@ class _StageTimer:
         if not self.enabled:
             return
         import torch
-        torch.cuda.synchronize()
+        torch.cuda.current_stream().synchronize()  # (not the copy stream: it overlaps)
         now = time.perf_counter()
         if self.t is not None:
             self.acc[name] = self.acc.get(name, 0.0) + now - self.t
@@ -479,12 +562,12 @@ def main(args):
     outdir = expand_outdir_and_mkdir(args.sink)
     blocks = plan_partitions(args)
     args.n_partitions = len(blocks)
-    batches = iter_batches(args, rank, world, blocks, as_bytes=args.sentence_splitter == 'gpu')
     if args.sentence_splitter == 'host':
         # host segmentation first: its process pool forks before this process touches the GPU
-        batches = [(b, ('sentences',) + build_corpus(b, args.local_n_workers)) for b in batches]
+        batches = [(b, ('sentences',) + build_corpus(b, args.local_n_workers))
+                   for b in iter_batches(args, rank, world, blocks)]
     else:
-        batches = ((b, build_doc_corpus(b)) for b in batches)
+        batches = iter_doc_batches(args, rank, world, blocks)
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -512,37 +595,51 @@ def main(args):
         nbins = args.target_seq_length // bin_size
         stream = StreamBalancer(ctx, bin_size, nbins, num_shards=args.num_shards)
         writers = ShardWriters(outdir, nbins, binned, args.masking, pool)
-        # every rank steps the balancer once per batch of the rank with the most batches
-        n_steps = max(len(rank_batches(args, blocks, r, world)) for r in range(world))
+        # every rank steps the balancer once per GPU batch of the rank with the most of them
+        n_steps = max(n_gpu_batches(args, blocks, r, world) for r in range(world))
     k = 0
+    copier = ThreadPoolExecutor(max_workers=1)  # device -> host copies of rendered batches
+    inflight = []  # (copy future, write futures) of the batches not yet written
     for batch, corpus in batches:
         timer('read')
         if stream is None:
             futs = []
-            n_files += len(process_batch(ctx, args, batch, corpus, outdir, timer, pool, futs))
-            for f in pending:
-                f.result()
-            pending = futs
+            job = process_batch(ctx, args, batch, corpus, outdir, timer, pool, futs, copier)
+            if isinstance(job, list):
+                n_files += len(job)
+            inflight.append((job, futs))
+            while len(inflight) > 2:  # at most two rendered batches in memory besides this one
+                j, fs = inflight.pop(0)
+                if not isinstance(j, list):
+                    n_files += len(j.result())
+                for f in fs:
+                    f.result()
             timer('write_wait')
         else:
             bb = stream.step(make_batch_pairs(ctx, args, batch, corpus, timer))
             timer('balance')
-            writers.add(ctx, bb)
+            writers.add(ctx, bb, copier)
             del bb
             timer('render')
             k += 1
         timer.mark()
     for f in pending:
         f.result()
+    for j, fs in inflight:
+        if not isinstance(j, list):
+            n_files += len(j.result())
+        for f in fs:
+            f.result()
     timer('write_wait')
     if stream is not None:
         for _ in range(k, n_steps):
-            writers.add(ctx, stream.step(_empty_pairs(ctx, args.masking)))
+            writers.add(ctx, stream.step(_empty_pairs(ctx, args.masking)), copier)
         n_files += len(writers.close())
         timer('write_wait')
         if rank == 0:
             with open(os.path.join(outdir, '.num_samples.json'), 'w') as f:
                 json.dump(num_samples_of_shards(stream.all_shard_counts, binned), f)
+    copier.shutdown()
     pool.shutdown()
     if world > 1:
         dist.barrier()
@@ -614,9 +711,13 @@ def attach_args(parser=None):
                     help_str='static masking in the preprocessor (default: off = dynamic '
                     'masking in the data loader)')
     parser.add_argument('--masked-lm-ratio', type=float, default=0.15, help='Default: 0.15')
-    parser.add_argument('--gpu-batch-bytes', type=int, default=1 << 30,
-                        help='lddl_amd: input text bytes per GPU batch of partitions (whole '
-                             'shuffle groups; bounds HBM use, does not change the output)')
+    parser.add_argument('--gpu-batch-bytes', type=int, default=256 << 20,
+                        help='lddl_amd: input text bytes per GPU batch of partitions (bounds HBM '
+                             'use; consecutive batches overlap their GPU work, rendering and file '
+                             'writes; does not change the part.* output). Default: 256 MiB')
+    parser.add_argument('--read-threads', type=int, default=min(os.cpu_count() or 1, 16),
+                        help='lddl_amd: host threads of the input reader (GPU segmentation path). '
+                             'Default: min(cpus, 16)')
     parser.add_argument('--shuffle-group-bytes', type=int, default=1 << 30,
                         help='lddl_amd: documents are shuffled across the partitions of runs of '
                              'this many input bytes (the reference shuffles globally, '

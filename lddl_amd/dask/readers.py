@@ -224,3 +224,63 @@ def split_id_text_bytes(raw):
         return raw[:i], raw[i + 1:]
     a, b = split_id_text(raw.decode('utf-8'))
     return a.encode('utf-8'), b.encode('utf-8')
+
+
+def read_groups_native(groups, group_seeds, threads=16):
+    """The documents of shuffle groups of blocks, read by the library's host reader
+    (lddl_read_groups: C++ threads, no per-line Python): for every group, its blocks' lines as
+    read_block(as_bytes=True) gives them, shuffled by random.Random(seed).shuffle over the group
+    (pretrain.py:100-111 per group) and dealt back (each block keeps its count), each reduced to the
+    text after its id (split_id_text_bytes). Returns (text uint8, doc_off int64[n_docs + 1],
+    block_ndocs int64[n_blocks]) in block order. Malformed UTF-8 anywhere in a block raises
+    UnicodeDecodeError, as dask's strict decode of the block does."""
+    import ctypes
+    import numpy as np
+    from .._native import lib, check
+    blocks = [b for g in groups for b in g]
+    n = len(blocks)
+    paths = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(b.path) for b in blocks])
+    starts = np.asarray([b.start for b in blocks], np.int64)
+    ends = np.asarray([max(b.end, b.start) for b in blocks], np.int64)
+    ratios = {b.ratio for b in blocks if b.state is not None}
+    if any(b.state is None for b in blocks) and ratios:
+        raise ValueError('blocks mix sampled and unsampled reads')
+    if len(ratios) > 1:
+        raise ValueError('blocks with different sample ratios')
+    states = None
+    if ratios:
+        states = np.empty((n, 625), np.uint32)
+        for i, b in enumerate(blocks):
+            assert b.state[0] == 3 and len(b.state[1]) == 625
+            states[i] = b.state[1]
+    goff = np.zeros(len(groups) + 1, np.int64)
+    np.cumsum([len(g) for g in groups], out=goff[1:])
+    seeds = [abs(int(x)) for x in group_seeds]
+    if any(x >= 1 << 64 for x in seeds):
+        raise ValueError('shuffle seeds must be below 2**64 in magnitude')
+    seeds = np.asarray(seeds, np.uint64)
+    h = ctypes.c_void_p()
+    n_docs, n_text = ctypes.c_int64(), ctypes.c_int64()
+    bad = np.zeros(2, np.int64)
+    st = lib.lddl_read_groups(n, paths, starts.ctypes.data, ends.ctypes.data,
+                              None if states is None else states.ctypes.data,
+                              float(ratios.pop()) if ratios else 1.0, len(groups),
+                              goff.ctypes.data, seeds.ctypes.data, int(threads), ctypes.byref(h),
+                              ctypes.byref(n_docs), ctypes.byref(n_text), bad.ctypes.data)
+    if st == -2:
+        b = blocks[int(bad[0])]
+        off = b.start + int(bad[1])
+        with open(b.path, 'rb') as f:
+            f.seek(max(off - 8, b.start))
+            ctx = f.read(16)
+        raise UnicodeDecodeError('utf-8', ctx, min(8, off - b.start), min(8, off - b.start) + 1,
+                                 'invalid UTF-8 at byte {} of {}'.format(off, b.path))
+    check(st)
+    try:
+        text = np.empty(n_text.value, np.uint8)
+        doc_off = np.empty(n_docs.value + 1, np.int64)
+        ndocs = np.empty(max(n, 1), np.int64)[:n]
+        check(lib.lddl_read_fill(h, text.ctypes.data, doc_off.ctypes.data, ndocs.ctypes.data))
+    finally:
+        lib.lddl_read_free(h)
+    return text, doc_off, ndocs

@@ -104,6 +104,52 @@ class Rendered:
 def render(ctx, pb, rows=None, bin_id=None):
     """Render the parquet columns of PairBatch `pb` for output rows `rows` (int64 cuda tensor of
     pair indices, None = all pairs in order). Returns a host `Rendered`."""
+    return render_device(ctx, pb, rows, bin_id).to_host()
+
+
+@dataclass
+class DeviceRendered:
+    """render()'s columns still in HBM (device tensors), with the stream event after which they
+    are complete: to_host() copies them to pinned host memory on a stream of its own, so the
+    copy of one batch overlaps the GPU work of the next (any thread may call it)."""
+    cols: dict
+    tot: list
+    masking: bool
+    event: object = None
+
+    def to_host(self, stream=None):
+        st = stream if stream is not None else torch.cuda.current_stream()
+        if self.event is not None:
+            st.wait_event(self.event)
+        out = {}
+        with torch.cuda.stream(st):
+            for k, t in self.cols.items():
+                if t is None:
+                    out[k] = None
+                    continue
+                if _PAGEABLE:  # (A/B diagnostics) pageable host buffers
+                    h = torch.empty(max(t.numel(), 1), dtype=t.dtype)[:t.numel()]
+                    h.copy_(t)
+                else:
+                    h = torch.empty(max(t.numel(), 1), dtype=t.dtype, pin_memory=True)[:t.numel()]
+                    h.copy_(t, non_blocking=True)
+                t.record_stream(st)
+                out[k] = h
+        st.synchronize()
+        n = {k: (v.numpy() if v is not None else None) for k, v in out.items()}
+        rd = Rendered(n['a_off'], n['a_bytes'], n['b_off'], n['b_bytes'],
+                      n['is_rn'].astype(bool), n['num_tokens'].view(np.uint16))
+        if self.masking:
+            rd.l_off, rd.l_bytes = n['l_off'], n['l_bytes']
+            rd.npy_off, rd.npy_bytes = n['npy_off'], n['npy_bytes']
+        if n.get('bin_id') is not None:
+            rd.bin_id = n['bin_id'].astype(np.int64)
+        self.cols = None
+        return rd
+
+
+def render_device(ctx, pb, rows=None, bin_id=None):
+    """The GPU half of render(): kernels only (one host sync for the byte totals)."""
     dev = ctx.device
     n = pb.n_pairs if rows is None else rows.numel()
     masking = pb.pos is not None
@@ -132,21 +178,17 @@ def render(ctx, pb, rows=None, bin_id=None):
                                 _ptr(bufs[2]) if masking else None,
                                 _ptr(bufs[3]) if masking else None))
 
-    def host(t, k):  # pinned staging (torch's caching host allocator): full-rate D2H
-        h = torch.empty(max(k, 1), dtype=t.dtype, pin_memory=True)[:k]
-        h.copy_(t[:k])
-        return h.numpy()
-
-    out = Rendered(a_off.cpu().numpy(), host(bufs[0], tot[0]), b_off.cpu().numpy(),
-                   host(bufs[1], tot[1]), is_rn.cpu().numpy().astype(bool),
-                   num_tokens.cpu().numpy().view(np.uint16))
+    cols = {'a_off': a_off, 'a_bytes': bufs[0][:tot[0]], 'b_off': b_off,
+            'b_bytes': bufs[1][:tot[1]], 'is_rn': is_rn, 'num_tokens': num_tokens}
     if masking:
-        out.l_off, out.l_bytes = l_off.cpu().numpy(), host(bufs[2], tot[2])
-        out.npy_off, out.npy_bytes = npy_off.cpu().numpy(), host(bufs[3], tot[3])
-    if bin_id is not None:  # host int64[n] (or a device tensor)
-        out.bin_id = (bin_id.cpu().numpy() if torch.is_tensor(bin_id) else
-                      np.asarray(bin_id)).astype(np.int64)
-    return out
+        cols.update(l_off=l_off, l_bytes=bufs[2][:tot[2]], npy_off=npy_off,
+                    npy_bytes=bufs[3][:tot[3]])
+    if bin_id is not None:  # a device tensor (or host int64[n])
+        cols['bin_id'] = bin_id if torch.is_tensor(bin_id) else torch.from_numpy(
+            np.asarray(bin_id, np.int64)).to(dev)
+    ev = torch.cuda.Event()
+    ev.record()
+    return DeviceRendered(cols, tot, masking, ev)
 
 
 def schema(masking, binned):
@@ -184,9 +226,21 @@ def table(rd, r0, r1, masking, binned):
     return pa.Table.from_arrays(cols, schema=schema(masking, binned))
 
 
+_TRACE = os.environ.get('LDDL_TRACE_PIPELINE')
+_PAGEABLE = os.environ.get('LDDL_D2H_PAGEABLE')
+
+
 def write_table(rd, r0, r1, masking, binned, path, compression=DEFAULT_COMPRESSION):
     """Rows [r0, r1) of a Rendered as one parquet file."""
+    if _TRACE:
+        import sys
+        import time
+        t0 = time.perf_counter()
     pq.write_table(table(rd, r0, r1, masking, binned), path, compression=compression)
+    if _TRACE:
+        sys.stderr.write('[write] %s %.1f MB %.2f ms at %.3f\n' % (
+            os.path.basename(path), (rd.a_off[r1] - rd.a_off[r0]) * 2e-6,
+            (time.perf_counter() - t0) * 1e3, time.perf_counter()))
     return path
 
 

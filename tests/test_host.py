@@ -228,3 +228,62 @@ def test_txt_output_matches_reference_writer(tmp_path):
                     nbins, np.asarray(counts) if nbins else None, n_part)
         got = {fn: (out / fn).read_text() for fn in sorted(os.listdir(out))}
         assert got == c['files'], c['name']
+
+
+def _ws_corpus(d, n_files=3, n_lines=300, seed=5):
+    import random
+    rng = random.Random(seed)
+    ws = ['\t', ' ', '\x1c', ' ', '　', ' ', '\x85', ' \r', '\x0b']
+    words = ['abc', 'déjà', 'x', '中文', '[CLS]', 'q r', '', '\U0001f600']
+    for f in range(n_files):
+        lines = []
+        for i in range(n_lines):
+            parts = [rng.choice(words) for _ in range(rng.randint(0, 6))]
+            line = (rng.choice(ws) * rng.randint(0, 2) + 'id{}'.format(i) + rng.choice(ws) +
+                    ' '.join(parts) + rng.choice(ws) * rng.randint(0, 2))
+            lines.append('' if rng.random() < 0.1 else line)
+        with open(os.path.join(d, 'f{}.txt'.format(f)), 'w', encoding='utf-8') as fh:
+            fh.write('\n'.join(lines) + '\n')
+
+
+@pytest.mark.parametrize('ratio,bs', [(1.0, None), (1.0, 2500), (0.7, None), (0.6, 1700)])
+def test_native_reader_matches_python(tmp_path, ratio, bs):
+    """lddl_read_groups (C++ threads) == the per-line Python path: read_block(as_bytes=True)
+    lines (strip with str.isspace at both ends, empty dropped, random_sample), the per-group
+    Random(seed).shuffle of pretrain.iter_batches and split_id_text_bytes."""
+    import random
+    _ws_corpus(str(tmp_path))
+    blocks = R.plan_blocks(str(tmp_path), bs, ratio, 99)
+    groups = [blocks[i:i + 3] for i in range(0, len(blocks), 3)]
+    seeds = [12345 * 1000003 - 1 - 3 * i for i in range(len(groups))] + [-7]
+    if len(groups) > 1:
+        seeds[1] = -(1 << 40) - 3  # negative and two-limb seeds
+    seeds = seeds[:len(groups)]
+    text, doc_off, nd = R.read_groups_native(groups, seeds, threads=4)
+    exp, nde = [], []
+    for g, sd in zip(groups, seeds):
+        parts = [R.read_block(b, as_bytes=True) for b in g]
+        docs = [x for lines in parts for x in lines]
+        random.Random(sd).shuffle(docs)
+        k = 0
+        for lines in parts:
+            nde.append(len(lines))
+            exp += [R.split_id_text_bytes(x)[1] for x in docs[k:k + len(lines)]]
+            k += len(lines)
+    got = [bytes(text[doc_off[i]:doc_off[i + 1]]) for i in range(len(doc_off) - 1)]
+    assert got == exp
+    assert list(nd) == nde
+
+
+def test_native_reader_rejects_malformed_utf8(tmp_path):
+    """A malformed line raises even when random_sample would drop it (dask decodes whole
+    blocks strictly); overlong / surrogate / > U+10FFFF sequences are malformed as in Python."""
+    for bad in (b'\xc0\xaf', b'\xed\xa0\x80', b'\xf4\x90\x80\x80', b'\xe2\x82', b'\x80'):
+        p = tmp_path / 'x{}'.format(bad.hex())
+        p.mkdir()
+        with pytest.raises(UnicodeDecodeError):
+            bad.decode('utf-8')
+        (p / 'a.txt').write_bytes(b'id0 good line\nid1 bad ' + bad + b' here\nid2 ok\n')
+        blocks = R.plan_blocks(str(p), None, 0.01, 3)
+        with pytest.raises(UnicodeDecodeError):
+            R.read_groups_native([blocks], [1])
