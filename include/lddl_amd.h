@@ -72,7 +72,17 @@ int lddl_read_groups(int64_t n_blocks, const char* const* paths, const int64_t* 
                      const int64_t* group_off, const uint64_t* group_seed_abs, int n_threads,
                      lddl_reader** out, int64_t* n_docs, int64_t* n_text, int64_t* bad);
 int lddl_read_fill(lddl_reader* reader, uint8_t* text, int64_t* doc_off, int64_t* block_ndocs);
+/* block_ndocs[n_blocks] and doc_len[n_docs] (text bytes per document), either may be NULL; then
+ * lddl_read_fill_range copies documents [d0, d1) only: text[sum of their lengths],
+ * doc_off[d1 - d0 + 1] relative to text (a GPU batch at a time). */
+int lddl_read_counts(const lddl_reader* reader, int64_t* block_ndocs, int64_t* doc_len);
+int lddl_read_fill_range(lddl_reader* reader, int64_t d0, int64_t d1, uint8_t* text,
+                         int64_t* doc_off);
 int lddl_read_free(lddl_reader* reader);
+/* dask 2021.10 `random_state_data_python(n, seed)` (the per-partition MT states of
+ * bag.random_sample): n states of 624 words = Random(abs(seed)).randint(0, 2**32) in order, each
+ * followed by the index 624 (as setstate stores them: 2**32 becomes 0). out[625 * n]. */
+int lddl_random_state_data(int64_t n, uint64_t seed_abs, uint32_t* out);
 
 /* ---------------------------------------------------------------------------------------------
  * Context = device-resident tokenizer tables.

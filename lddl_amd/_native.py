@@ -29,6 +29,9 @@ SIGNATURES = {
                                         ctypes.c_int, ctypes.POINTER(c_vp), c_i64p, c_i64p, c_vp]),
     'lddl_read_fill': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
     'lddl_read_free': (ctypes.c_int, [c_vp]),
+    'lddl_read_counts': (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    'lddl_read_fill_range': (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp]),
+    'lddl_random_state_data': (ctypes.c_int, [c_i64, c_u64, c_vp]),
     'lddl_ctx_create': (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_vp, c_i64,
                                        ctypes.POINTER(c_vp)]),
     'lddl_ctx_destroy': (ctypes.c_int, [c_vp]),

@@ -75,6 +75,24 @@ def build_product(verbose=False, jobs=8, diag=False, variant=None, defines=()):
     return lib
 
 
+HOST_LIB = os.path.join(LIBDIR, 'liblddl_host.so')
+HOST_SRCS = ('reader.cpp', 'errors.cpp')
+
+
+def build_host():
+    """lddl_amd/_lib/liblddl_host.so: the host-only entry points (the input reader) without the
+    HIP runtime, so the CLI's reader thread can load it while the main thread is still importing
+    torch (liblddl_amd.so must be loaded after torch: one HIP runtime per process). The same
+    sources are also part of liblddl_amd.so."""
+    os.makedirs(LIBDIR, exist_ok=True)
+    srcs = [os.path.join(CSRC, x) for x in HOST_SRCS]
+    deps = srcs + glob.glob(os.path.join(ROOT, 'include', '*.h')) + [os.path.join(CSRC, 'common.h')]
+    if _newer(HOST_LIB, deps):
+        _run(['g++', '-O3', '-std=c++17', '-fPIC', '-shared', '-Wall', '-I' + os.path.join(ROOT, 'include'),
+              '-I' + CSRC, '-o', HOST_LIB] + srcs + ['-lpthread'])
+    return HOST_LIB
+
+
 def build_oracle():
     os.makedirs(os.path.dirname(ORACLE_LIB), exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(ORACLE_DIR, '*.c')))
@@ -87,6 +105,7 @@ def build_oracle():
 
 def build_all(verbose=False):
     lib = build_product(verbose=verbose)
+    build_host()
     orc = build_oracle()
     return lib, orc
 

@@ -342,6 +342,56 @@ extern "C" int lddl_read_fill(lddl_reader* R, uint8_t* text, int64_t* doc_off,
   return 0;
 }
 
+extern "C" int lddl_read_counts(const lddl_reader* R, int64_t* block_ndocs, int64_t* doc_len) {
+  if (!R) LDDL_FAIL(-1, "null reader");
+  if (block_ndocs)
+    memcpy(block_ndocs, R->block_ndocs.data(), sizeof(int64_t) * R->block_ndocs.size());
+  if (doc_len) memcpy(doc_len, R->tlen.data(), sizeof(int64_t) * R->tlen.size());
+  return 0;
+}
+
+extern "C" int lddl_read_fill_range(lddl_reader* R, int64_t d0, int64_t d1, uint8_t* text,
+                                    int64_t* doc_off) {
+  if (!R || d0 < 0 || d1 < d0 || d1 > (int64_t)R->docs.size()) LDDL_FAIL(-1, "bad doc range");
+  const int64_t n = d1 - d0;
+  doc_off[0] = 0;
+  for (int64_t q = 0; q < n; ++q) doc_off[q + 1] = doc_off[q] + R->tlen[d0 + q];
+  parallel_for((n + 1023) / 1024, R->n_threads, [&](int64_t c) {
+    for (int64_t q = c * 1024; q < std::min(n, (c + 1) * 1024); ++q) {
+      const int64_t d = d0 + q;
+      if (R->tlen[d])
+        memcpy(text + doc_off[q], R->blocks[R->docs[d].first].buf.data() + R->tstart[d],
+               (size_t)R->tlen[d]);
+    }
+  });
+  return 0;
+}
+
+// dask 2021.10 random_state_data_python(n, seed): n states of 624 words, each word
+// Random(seed).randint(0, 2**32) drawn in order (randint -> _randbelow(2**32 + 1) ->
+// getrandbits(33): two words, the second's top bit as bit 32, redrawn while >= 2**32 + 1).
+// out[625 * i + 624] = 624 (the state's index).
+extern "C" int lddl_random_state_data(int64_t n, uint64_t seed_abs, uint32_t* out) {
+  if (n < 0 || !out) LDDL_FAIL(-1, "bad arguments");
+  PyMT mt;
+  mt.seed_u64(seed_abs);
+  for (int64_t i = 0; i < n; ++i) {
+    for (int k = 0; k < 624; ++k) {
+      uint64_t v;
+      do {
+        const uint64_t lo = mt.u32();
+        const uint64_t hi = mt.u32() >> 31;
+        v = lo | (hi << 32);
+      } while (v > (1ull << 32));
+      // randint(0, 2**32) may be 2**32 itself: CPython's setstate() stores each word as
+      // (uint32_t)PyLong_AsUnsignedLong(w), i.e. 0
+      out[625 * i + k] = (uint32_t)v;
+    }
+    out[625 * i + 624] = 624;
+  }
+  return 0;
+}
+
 extern "C" int lddl_read_free(lddl_reader* R) {
   delete R;
   return 0;

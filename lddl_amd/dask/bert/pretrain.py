@@ -151,20 +151,22 @@ def iter_doc_batches(args, rank=0, world=1, blocks=None):
     so the GPU work, the rendering and the file writes of consecutive batches overlap."""
     blocks = plan_partitions(args) if blocks is None else blocks
     for batch in rank_batches(args, blocks, rank, world):
-        text, doc_off, nd = readers.read_groups_native(
-            [[blocks[p] for p in g] for g in batch],
-            [partition_seed(args.seed, -1 - g[0]) for g in batch],
-            threads=getattr(args, 'read_threads', 16))
+        rd = readers.NativeRead([[blocks[p] for p in g] for g in batch],
+                                [partition_seed(args.seed, -1 - g[0]) for g in batch],
+                                threads=getattr(args, 'read_threads', 16))
         parts = [p for g in batch for p in g]
         pdo = np.zeros(len(parts) + 1, np.int64)
-        np.cumsum(nd, out=pdo[1:])
-        for sub in _greedy(list(range(len(parts))), lambda i: blocks[parts[i]].nbytes,
-                           args.gpu_batch_bytes):
-            i0, i1 = sub[0], sub[-1] + 1
-            d0, d1 = int(pdo[i0]), int(pdo[i1])
-            t0, t1 = int(doc_off[d0]), int(doc_off[d1])
-            yield ([(parts[i], None) for i in range(i0, i1)],
-                   ('documents', text[t0:t1], doc_off[d0:d1 + 1] - t0, pdo[i0:i1 + 1] - d0))
+        np.cumsum(rd.block_ndocs, out=pdo[1:])
+        try:
+            for sub in _greedy(list(range(len(parts))), lambda i: blocks[parts[i]].nbytes,
+                               args.gpu_batch_bytes):
+                i0, i1 = sub[0], sub[-1] + 1
+                d0, d1 = int(pdo[i0]), int(pdo[i1])
+                text, doc_off = rd.fill(d0, d1)  # this GPU batch's documents only
+                yield ([(parts[i], None) for i in range(i0, i1)],
+                       ('documents', text, doc_off, pdo[i0:i1 + 1] - d0))
+        finally:
+            rd.close()
 
 
 def get_partitions(args, rank=0, world=1):
@@ -332,7 +334,7 @@ def _trace(what, batch):
     """LDDL_TRACE_PIPELINE=1: host timeline of the CLI pipeline on stderr (diagnostics)."""
     if _TRACE:
         import threading
-        sys.stderr.write('[pipe] %8.3f %-14s batch@%s %s\n' % (time.perf_counter() - _T0, what,
+        sys.stderr.write('[pipe] %8.3f %-14s batch@%s %s\n' % (time.perf_counter(), what,
                                                                batch,
                                                                threading.current_thread().name))
 
@@ -541,6 +543,17 @@ class _StageTimer:
             self.t = time.perf_counter()
 
 
+def _warm_parquet_writer(outdir):
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    fn = os.path.join(outdir, '.lddl_amd_warmup.{}.parquet'.format(os.getpid()))
+    try:
+        pq.write_table(pa.table({'A': pa.array(['x'])}), fn)
+    finally:
+        if os.path.exists(fn):
+            os.remove(fn)
+
+
 def main(args):
     if args.bin_size is not None:
         if args.bin_size > args.target_seq_length:
@@ -559,15 +572,24 @@ def main(args):
     local = int(os.environ.get('LOCAL_RANK', '0'))
     vocab = _resolve_vocab(args.vocab_file)
     tic = time.perf_counter()
+    _trace('main', -1)
     outdir = expand_outdir_and_mkdir(args.sink)
     blocks = plan_partitions(args)
     args.n_partitions = len(blocks)
+    _trace('planned', -1)
     if args.sentence_splitter == 'host':
         # host segmentation first: its process pool forks before this process touches the GPU
         batches = [(b, ('sentences',) + build_corpus(b, args.local_n_workers))
                    for b in iter_batches(args, rank, world, blocks)]
     else:
-        batches = iter_doc_batches(args, rank, world, blocks)
+        # the host reader starts now, in its own thread, overlapping the device setup below
+        batches = _prefetch(iter_doc_batches(args, rank, world, blocks))
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(max_workers=max(1, args.write_threads))
+    # pyarrow's parquet writer initialises lazily on its first file (~0.3-0.8 s, measured on the
+    # box): one tiny write on a writer thread now overlaps that with the setup and the first batch
+    pool.submit(_warm_parquet_writer, outdir)
+    _trace('setup_start', -1)
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -580,10 +602,7 @@ def main(args):
         from ... import punkt
         punkt.set_params(ctx, punkt_params(args))
     timer = _StageTimer(args.profile_stages)
-    from concurrent.futures import ThreadPoolExecutor
-    pool = ThreadPoolExecutor(max_workers=max(1, args.write_threads))
-    if args.sentence_splitter == 'gpu':
-        batches = _prefetch(batches)
+    _trace('setup_end', -1)
     timer.mark()
     n_files = 0
     pending = []  # writes of the previous batch (at most two batches of rendered rows in memory)
@@ -602,6 +621,7 @@ def main(args):
     inflight = []  # (copy future, write futures) of the batches not yet written
     for batch, corpus in batches:
         timer('read')
+        _trace('batch_ready', batch[0][0] if batch else -1)
         if stream is None:
             futs = []
             job = process_batch(ctx, args, batch, corpus, outdir, timer, pool, futs, copier)

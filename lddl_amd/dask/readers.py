@@ -56,7 +56,7 @@ def _block_starts(data, blocksize):
     return starts
 
 
-def _next_line_start(f, off, size, chunk=1 << 16):
+def _next_line_start(f, off, size, chunk=1 << 13):
     """First byte after the first newline at or after offset off - 1 (dask read_block)."""
     pos = off - 1
     while pos < size:
@@ -87,16 +87,24 @@ def _file_block_starts(fn, blocksize):
 @dataclass
 class Block:
     """One dask partition before it is read: bytes [start, end) of `path` (empty if end <= start),
-    with the MT state of its random_sample (None: no sampling)."""
+    with the MT state of its random_sample as uint32[625] (624 words + index; None: no
+    sampling)."""
     path: str
     start: int
     end: int
-    state: tuple = None
+    mt: object = None
     ratio: float = 1.0
 
     @property
     def nbytes(self):
         return max(self.end - self.start, 0)
+
+    @property
+    def state(self):
+        """The state as random.Random.getstate() gives it (None: no sampling)."""
+        if self.mt is None:
+            return None
+        return (3, tuple(int(x) for x in self.mt), None)
 
 
 def plan_blocks(path, blocksize=None, sample_ratio=1.0, sample_seed=12345):
@@ -107,8 +115,8 @@ def plan_blocks(path, blocksize=None, sample_ratio=1.0, sample_seed=12345):
         for a, b in zip(st[:-1], st[1:]):
             blocks.append(Block(fn, a, b if (b > a or len(st) <= 2) else a))
     if sample_ratio < 1.0:
-        for b, s in zip(blocks, random_state_data_python(len(blocks), sample_seed)):
-            b.state, b.ratio = s, sample_ratio
+        for b, s in zip(blocks, random_state_data(len(blocks), sample_seed)):
+            b.mt, b.ratio = s, sample_ratio
     return blocks
 
 
@@ -164,9 +172,24 @@ def read_blocks(files, blocksize=None):
 
 
 def random_state_data_python(n, seed):
+    """dask 2021.10 dask.utils.random_state_data_python (the per-partition states of
+    bag.random_sample), as Random.getstate() tuples."""
     r = random.Random(seed)
     m = 1 << 32
     return [(3, tuple(r.randint(0, m) for _ in range(624)) + (624,), None) for _ in range(n)]
+
+
+def random_state_data(n, seed):
+    """random_state_data_python(n, seed) as uint32[n, 625] (words as setstate stores them), from
+    the host library (lddl_random_state_data: 624 x n randint draws in C++ instead of Python)."""
+    import numpy as np
+    out = np.empty((n, 625), np.uint32)
+    if n:
+        lib, check = _host_lib()
+        if abs(int(seed)) >= 1 << 64:
+            raise ValueError('sample seed must be below 2**64 in magnitude')
+        check(lib.lddl_random_state_data(n, abs(int(seed)), out.ctypes.data))
+    return out
 
 
 def _filter(block):
@@ -226,6 +249,118 @@ def split_id_text_bytes(raw):
     return a.encode('utf-8'), b.encode('utf-8')
 
 
+_HOST = None
+
+
+def _host_lib():
+    """liblddl_host.so (lddl_amd/build.py): the reader's entry points without the HIP runtime,
+    so they load without torch (the CLI reads while the main thread imports torch)."""
+    global _HOST
+    if _HOST is None:
+        import ctypes
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), '_lib',
+                            'liblddl_host.so')
+        if not os.path.exists(path):
+            raise ImportError('{} is missing (run `python -m lddl_amd.build`)'.format(path))
+        lib = ctypes.CDLL(path)
+        c_i64, c_vp = ctypes.c_int64, ctypes.c_void_p
+        lib.lddl_read_groups.restype = ctypes.c_int
+        lib.lddl_read_groups.argtypes = [c_i64, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, c_i64,
+                                         c_vp, c_vp, ctypes.c_int, ctypes.POINTER(c_vp),
+                                         ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), c_vp]
+        lib.lddl_read_fill.restype = ctypes.c_int
+        lib.lddl_read_fill.argtypes = [c_vp, c_vp, c_vp, c_vp]
+        lib.lddl_read_free.restype = ctypes.c_int
+        lib.lddl_read_free.argtypes = [c_vp]
+        lib.lddl_read_counts.restype = ctypes.c_int
+        lib.lddl_read_counts.argtypes = [c_vp, c_vp, c_vp]
+        lib.lddl_read_fill_range.restype = ctypes.c_int
+        lib.lddl_read_fill_range.argtypes = [c_vp, c_i64, c_i64, c_vp, c_vp]
+        lib.lddl_random_state_data.restype = ctypes.c_int
+        lib.lddl_random_state_data.argtypes = [c_i64, ctypes.c_uint64, c_vp]
+        lib.lddl_last_error.restype = ctypes.c_char_p
+
+        def check(status):
+            if status < 0:
+                raise RuntimeError('liblddl_host: ' + (lib.lddl_last_error() or b'').decode())
+            return status
+        _HOST = (lib, check)
+    return _HOST
+
+
+class NativeRead:
+    """One lddl_read_groups call (see read_groups_native) whose documents are copied out a range
+    at a time: `block_ndocs` / `doc_len` are known as soon as the blocks are read, split, sampled
+    and shuffled, and fill(d0, d1) copies documents [d0, d1) (one GPU batch) while later batches
+    stay in the reader. close() frees it."""
+
+    def __init__(self, groups, group_seeds, threads=16):
+        import ctypes
+        import numpy as np
+        self._lib, self._check = lib, check = _host_lib()
+        blocks = [b for g in groups for b in g]
+        n = len(blocks)
+        paths = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(b.path) for b in blocks])
+        starts = np.asarray([b.start for b in blocks], np.int64)
+        ends = np.asarray([max(b.end, b.start) for b in blocks], np.int64)
+        ratios = {b.ratio for b in blocks if b.mt is not None}
+        if any(b.mt is None for b in blocks) and ratios:
+            raise ValueError('blocks mix sampled and unsampled reads')
+        if len(ratios) > 1:
+            raise ValueError('blocks with different sample ratios')
+        states = None
+        if ratios:
+            states = np.ascontiguousarray(np.stack([b.mt for b in blocks]), np.uint32)
+        goff = np.zeros(len(groups) + 1, np.int64)
+        np.cumsum([len(g) for g in groups], out=goff[1:])
+        seeds = [abs(int(x)) for x in group_seeds]
+        if any(x >= 1 << 64 for x in seeds):
+            raise ValueError('shuffle seeds must be below 2**64 in magnitude')
+        seeds = np.asarray(seeds, np.uint64)
+        self._h = ctypes.c_void_p()
+        n_docs, n_text = ctypes.c_int64(), ctypes.c_int64()
+        bad = np.zeros(2, np.int64)
+        st = lib.lddl_read_groups(n, paths, starts.ctypes.data, ends.ctypes.data,
+                                  None if states is None else states.ctypes.data,
+                                  float(ratios.pop()) if ratios else 1.0, len(groups),
+                                  goff.ctypes.data, seeds.ctypes.data, int(threads),
+                                  ctypes.byref(self._h), ctypes.byref(n_docs),
+                                  ctypes.byref(n_text), bad.ctypes.data)
+        if st == -2:
+            b = blocks[int(bad[0])]
+            off = b.start + int(bad[1])
+            with open(b.path, 'rb') as f:
+                f.seek(max(off - 8, b.start))
+                ctx = f.read(16)
+            raise UnicodeDecodeError('utf-8', ctx, min(8, off - b.start),
+                                     min(8, off - b.start) + 1,
+                                     'invalid UTF-8 at byte {} of {}'.format(off, b.path))
+        check(st)
+        self.n_docs, self.n_text = n_docs.value, n_text.value
+        self.block_ndocs = np.empty(max(n, 1), np.int64)[:n]
+        self.doc_len = np.empty(max(self.n_docs, 1), np.int64)[:self.n_docs]
+        check(lib.lddl_read_counts(self._h, self.block_ndocs.ctypes.data,
+                                   self.doc_len.ctypes.data))
+
+    def fill(self, d0, d1):
+        """(text uint8, doc_off int64[d1 - d0 + 1]) of documents [d0, d1)."""
+        import numpy as np
+        nb = int(self.doc_len[d0:d1].sum())
+        text = np.empty(nb, np.uint8)
+        doc_off = np.empty(d1 - d0 + 1, np.int64)
+        self._check(self._lib.lddl_read_fill_range(self._h, d0, d1, text.ctypes.data,
+                                                    doc_off.ctypes.data))
+        return text, doc_off
+
+    def close(self):
+        if self._h:
+            self._lib.lddl_read_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
 def read_groups_native(groups, group_seeds, threads=16):
     """The documents of shuffle groups of blocks, read by the library's host reader
     (lddl_read_groups: C++ threads, no per-line Python): for every group, its blocks' lines as
@@ -234,53 +369,9 @@ def read_groups_native(groups, group_seeds, threads=16):
     text after its id (split_id_text_bytes). Returns (text uint8, doc_off int64[n_docs + 1],
     block_ndocs int64[n_blocks]) in block order. Malformed UTF-8 anywhere in a block raises
     UnicodeDecodeError, as dask's strict decode of the block does."""
-    import ctypes
-    import numpy as np
-    from .._native import lib, check
-    blocks = [b for g in groups for b in g]
-    n = len(blocks)
-    paths = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(b.path) for b in blocks])
-    starts = np.asarray([b.start for b in blocks], np.int64)
-    ends = np.asarray([max(b.end, b.start) for b in blocks], np.int64)
-    ratios = {b.ratio for b in blocks if b.state is not None}
-    if any(b.state is None for b in blocks) and ratios:
-        raise ValueError('blocks mix sampled and unsampled reads')
-    if len(ratios) > 1:
-        raise ValueError('blocks with different sample ratios')
-    states = None
-    if ratios:
-        states = np.empty((n, 625), np.uint32)
-        for i, b in enumerate(blocks):
-            assert b.state[0] == 3 and len(b.state[1]) == 625
-            states[i] = b.state[1]
-    goff = np.zeros(len(groups) + 1, np.int64)
-    np.cumsum([len(g) for g in groups], out=goff[1:])
-    seeds = [abs(int(x)) for x in group_seeds]
-    if any(x >= 1 << 64 for x in seeds):
-        raise ValueError('shuffle seeds must be below 2**64 in magnitude')
-    seeds = np.asarray(seeds, np.uint64)
-    h = ctypes.c_void_p()
-    n_docs, n_text = ctypes.c_int64(), ctypes.c_int64()
-    bad = np.zeros(2, np.int64)
-    st = lib.lddl_read_groups(n, paths, starts.ctypes.data, ends.ctypes.data,
-                              None if states is None else states.ctypes.data,
-                              float(ratios.pop()) if ratios else 1.0, len(groups),
-                              goff.ctypes.data, seeds.ctypes.data, int(threads), ctypes.byref(h),
-                              ctypes.byref(n_docs), ctypes.byref(n_text), bad.ctypes.data)
-    if st == -2:
-        b = blocks[int(bad[0])]
-        off = b.start + int(bad[1])
-        with open(b.path, 'rb') as f:
-            f.seek(max(off - 8, b.start))
-            ctx = f.read(16)
-        raise UnicodeDecodeError('utf-8', ctx, min(8, off - b.start), min(8, off - b.start) + 1,
-                                 'invalid UTF-8 at byte {} of {}'.format(off, b.path))
-    check(st)
+    r = NativeRead(groups, group_seeds, threads)
     try:
-        text = np.empty(n_text.value, np.uint8)
-        doc_off = np.empty(n_docs.value + 1, np.int64)
-        ndocs = np.empty(max(n, 1), np.int64)[:n]
-        check(lib.lddl_read_fill(h, text.ctypes.data, doc_off.ctypes.data, ndocs.ctypes.data))
+        text, doc_off = r.fill(0, r.n_docs)
+        return text, doc_off, r.block_ndocs
     finally:
-        lib.lddl_read_free(h)
-    return text, doc_off, ndocs
+        r.close()

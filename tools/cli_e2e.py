@@ -26,7 +26,11 @@ def main():
     ap.add_argument('--masking', action='store_true', default=True)
     ap.add_argument('--files', type=int, default=16)
     ap.add_argument('--num-shards', type=int, default=None)
-    a = ap.parse_args()
+    ap.add_argument('--switch-interval', type=float, default=None,
+                    help='sys.setswitchinterval for the run (GIL hand-off experiments)')
+    a, extra = ap.parse_known_args()  # extra: passed to preprocess_bert_pretrain
+    if a.switch_interval:
+        sys.setswitchinterval(a.switch_interval)
     from lddl_amd import synth
     from lddl_amd.dask.bert import pretrain as P
     root = tempfile.mkdtemp(prefix='lddl_e2e_', dir=os.environ.get('TMPDIR', '/tmp'))
@@ -52,14 +56,19 @@ def main():
                     ['--bin-size', str(a.bin_size)] if a.bin_size else []) + (
                     ['--num-shards', str(a.num_shards)] if a.num_shards else [])
         import torch  # noqa: F401  (first import outside the clock)
+        import resource
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t1 = time.perf_counter()
-        P.main(P.attach_args().parse_args(argv))
+        P.main(P.attach_args().parse_args(argv + extra))
         wall = time.perf_counter() - t1
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
         out = os.path.join(root, 'out')
         out_bytes = sum(os.path.getsize(os.path.join(out, x)) for x in os.listdir(out))
         print(json.dumps({'source_bytes': src_bytes, 'documents': n_doc, 'cli_wall_s': wall,
                           'source_MB_per_s': src_bytes / wall / 1e6, 'output_bytes': out_bytes,
-                          'generate_s': gen_s, 'argv': argv[argv.index('--target-seq-length'):]}))
+                          'generate_s': gen_s, 'cpu_s': cpu_s, 'cpu_per_wall': cpu_s / wall,
+                          'argv': argv[argv.index('--target-seq-length'):] + extra}))
     finally:
         shutil.rmtree(root, ignore_errors=True)
 
