@@ -65,9 +65,25 @@ def main():
         cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
         out = os.path.join(root, 'out')
         out_bytes = sum(os.path.getsize(os.path.join(out, x)) for x in os.listdir(out))
+        shards = None
+        if a.num_shards:  # the balancer's contract: every bin's shards hold N or N+1 samples
+            import pyarrow.parquet as pq
+            with open(os.path.join(out, '.num_samples.json')) as f:
+                ns = json.load(f)
+            per_bin = {}
+            for k, v in ns.items():
+                assert pq.read_metadata(os.path.join(out, k)).num_rows == v, k
+                per_bin.setdefault(k.rsplit('_', 1)[-1] if a.bin_size else '', []).append(v)
+            spread = max(max(v) - min(v) for v in per_bin.values())
+            assert spread <= 1 and all(len(v) == a.num_shards for v in per_bin.values())
+            shards = {'files': len(ns), 'bins': len(per_bin), 'samples': sum(ns.values()),
+                      'max_spread_per_bin': spread}
         print(json.dumps({'source_bytes': src_bytes, 'documents': n_doc, 'cli_wall_s': wall,
                           'source_MB_per_s': src_bytes / wall / 1e6, 'output_bytes': out_bytes,
                           'generate_s': gen_s, 'cpu_s': cpu_s, 'cpu_per_wall': cpu_s / wall,
+                          'shards': shards,
+                          'hbm_peak_reserved_gb': torch.cuda.max_memory_reserved() / 1e9,
+                          'hbm_peak_allocated_gb': torch.cuda.max_memory_allocated() / 1e9,
                           'argv': argv[argv.index('--target-seq-length'):] + extra}))
     finally:
         shutil.rmtree(root, ignore_errors=True)
