@@ -211,13 +211,16 @@ int lddl_pairs_plan_ms(const lddl_pairs* plan, float* ms);
  * Per-partition sequence-length binning.
  * Replaces _to_dataframe_binned (lddl/dask/bert/binning.py:63-93) applied per partition:
  *   bin_id = min((num_tokens - 1) // bin_size, nbins - 1), rows regrouped by bin, stable.
- * Rows of partition p are d_part_off[p] .. d_part_off[p+1]. Outputs (device): d_perm[r] = input
+ * Rows of partition p are d_part_off[p] .. d_part_off[p+1]; row r's num_tokens is d_num_tokens[r],
+ * or, with d_num_tokens NULL, d_tok_off[r+1] - d_tok_off[r] + 3 (a lddl_pairs_emit offset table).
+ * Outputs (device, every entry written): d_perm[r] = input
  * row of output row r (partition order kept, bins ascending inside a partition), d_bin_id[r] its
  * bin, d_counts[p * nbins + b] = rows of partition p in bin b. nbins <= 8192.
  * ------------------------------------------------------------------------------------------- */
-int lddl_bin_partitions(lddl_ctx* ctx, void* stream, const int32_t* d_num_tokens, int64_t n_rows,
-                        const int64_t* d_part_off, int64_t n_part, int32_t bin_size, int32_t nbins,
-                        int64_t* d_perm, int64_t* d_bin_id, int64_t* d_counts);
+int lddl_bin_partitions(lddl_ctx* ctx, void* stream, const int32_t* d_num_tokens,
+                        const int64_t* d_tok_off, int64_t n_rows, const int64_t* d_part_off,
+                        int64_t n_part, int32_t bin_size, int32_t nbins, int64_t* d_perm,
+                        int64_t* d_bin_id, int64_t* d_counts);
 
 /* The same regroup for ONE large segment (a rank's rows of one batch before the load-balance
  * exchange), spread over many workgroups: d_perm / d_bin_id (may be NULL) as above, d_counts[b]

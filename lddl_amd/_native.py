@@ -50,8 +50,8 @@ SIGNATURES = {
     'lddl_pairs_destroy': (ctypes.c_int, [c_vp, c_vp]),
     'lddl_pairs_part_offsets': (ctypes.c_int, [c_vp, c_vp, c_vp]),
     'lddl_pairs_plan_ms': (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float)]),
-    'lddl_bin_partitions': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp,
-                                           c_vp, c_vp]),
+    'lddl_bin_partitions': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32,
+                                           c_vp, c_vp, c_vp]),
     'lddl_bin_stable': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp,
                                        c_vp]),
     'lddl_render_lengths': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,

@@ -79,9 +79,10 @@ def gather_counts(local_counts, group=None):
     W = dist.get_world_size(group) if dist.is_initialized() else 1
     if W == 1:
         return local_counts.reshape(1, -1).cpu().numpy()
-    out = [torch.empty_like(local_counts) for _ in range(W)]
-    dist.all_gather(out, local_counts, group=group)
-    return torch.stack(out).cpu().numpy()
+    flat = local_counts.contiguous().reshape(-1)
+    out = torch.empty(W * flat.numel(), dtype=flat.dtype, device=flat.device)
+    dist.all_gather_into_tensor(out, flat, group=group)
+    return out.cpu().numpy().reshape((W,) + tuple(local_counts.shape))
 
 
 # ---- data-movement primitives ----------------------------------------------------------------

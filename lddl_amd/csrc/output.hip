@@ -39,8 +39,17 @@ __device__ inline int32_t bin_of(int32_t nt, int32_t bin_size, int32_t nbins) {
   return b > nbins - 1 ? nbins - 1 : b;
 }
 
+// num_tokens of row r: an int32 column, or (tok_off given) the pair's token count + 3
+struct NumTok {
+  const int32_t* nt;
+  const int64_t* tok_off;
+  __device__ int32_t operator[](int64_t r) const {
+    return nt ? nt[r] : (int32_t)(tok_off[r + 1] - tok_off[r] + 3);
+  }
+};
+
 __global__ void __launch_bounds__(kBinThreads) bin_partitions_kernel(
-    const int32_t* __restrict__ num_tokens, const int64_t* __restrict__ part_off, int32_t bin_size,
+    NumTok num_tokens, const int64_t* __restrict__ part_off, int32_t bin_size,
     int32_t nbins, int32_t nbits, int64_t* __restrict__ perm, int64_t* __restrict__ bin_id,
     int64_t* __restrict__ counts) {
   __shared__ int64_t s_cnt[kMaxBinsLds];
@@ -105,14 +114,6 @@ __global__ void __launch_bounds__(kBinThreads) bin_partitions_kernel(
 // ---- stable sort by bin of one large segment: tiles of kBinTile rows, one wavefront each ----
 constexpr int kBinTile = 2048;
 
-// num_tokens of row r: an int32 column, or (tok_off given) the pair's token count + 3
-struct NumTok {
-  const int32_t* nt;
-  const int64_t* tok_off;
-  __device__ int32_t operator[](int64_t r) const {
-    return nt ? nt[r] : (int32_t)(tok_off[r + 1] - tok_off[r] + 3);
-  }
-};
 
 __global__ void __launch_bounds__(64) bin_tile_hist_kernel(NumTok num_tokens,
                                                            int64_t n, int32_t bin_size,
@@ -486,19 +487,21 @@ extern "C" int lddl_pairs_meta_unpack(void* stream, const int32_t* d_meta, int64
 }
 
 extern "C" int lddl_bin_partitions(lddl_ctx* c, void* stream, const int32_t* d_num_tokens,
-                                   int64_t n_rows, const int64_t* d_part_off, int64_t n_part,
-                                   int32_t bin_size, int32_t nbins, int64_t* d_perm,
-                                   int64_t* d_bin_id, int64_t* d_counts) {
+                                   const int64_t* d_tok_off, int64_t n_rows,
+                                   const int64_t* d_part_off, int64_t n_part, int32_t bin_size,
+                                   int32_t nbins, int64_t* d_perm, int64_t* d_bin_id,
+                                   int64_t* d_counts) {
   (void)c;
   if (bin_size < 1 || nbins < 1) LDDL_FAIL(-1, "bin_size and nbins must be >= 1");
   if (nbins > kMaxBinsLds) LDDL_FAIL(-1, "nbins %d > %d unsupported", nbins, kMaxBinsLds);
   if (n_part < 0 || n_rows < 0) LDDL_FAIL(-1, "bad sizes");
+  if (!d_num_tokens && !d_tok_off && n_rows) LDDL_FAIL(-1, "need num_tokens or tok_off");
   if (n_part == 0) return 0;
   int nbits = 0;
   while ((1 << nbits) < nbins) ++nbits;
   hipLaunchKernelGGL(bin_partitions_kernel, dim3((unsigned)n_part), dim3(kBinThreads), 0,
-                     as_stream(stream), d_num_tokens, d_part_off, bin_size, nbins, nbits, d_perm,
-                     d_bin_id, d_counts);
+                     as_stream(stream), NumTok{d_num_tokens, d_tok_off}, d_part_off, bin_size,
+                     nbins, nbits, d_perm, d_bin_id, d_counts);
   LDDL_HIP(hipGetLastError());
   return 0;
 }

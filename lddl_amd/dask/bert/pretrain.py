@@ -298,8 +298,8 @@ def process_batch(ctx, args, partitions, corpus, outdir, timer=None, executor=No
     if args.bin_size is not None:
         import torch
         nbins = args.target_seq_length // args.bin_size
-        nt = ((pb.tok_off[1:] - pb.tok_off[:-1]) + 3).to(torch.int32)
-        perm, bin_id, counts = output.bin_partitions(ctx, nt, pb.part_off, args.bin_size, nbins)
+        perm, bin_id, counts = output.bin_partitions(ctx, None, pb.part_off, args.bin_size, nbins,
+                                                     tok_off=pb.tok_off)
         drd = output.render_device(ctx, pb, perm, bin_id)
         counts = counts.cpu().numpy()
     else:

@@ -32,17 +32,19 @@ except ImportError:
     DEFAULT_COMPRESSION = None
 
 
-def bin_partitions(ctx, num_tokens, part_off, bin_size, nbins):
-    """num_tokens: int32 cuda [n]; part_off: int64 cuda [n_part+1].
+def bin_partitions(ctx, num_tokens, part_off, bin_size, nbins, tok_off=None):
+    """num_tokens: int32 cuda [n] (or None with tok_off: a pair table's int64 [n+1] token
+    offsets, num_tokens = len(A) + len(B) + 3); part_off: int64 cuda [n_part+1].
     Returns (perm int64 [n], bin_id int64 [n], counts int64 [n_part, nbins]) on the device."""
-    n = num_tokens.numel()
+    n = num_tokens.numel() if num_tokens is not None else tok_off.numel() - 1
     n_part = part_off.numel() - 1
-    dev = num_tokens.device
+    dev = part_off.device
     perm = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
     bin_id = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
-    counts = torch.zeros(max(n_part * nbins, 1), dtype=torch.int64, device=dev)[:n_part * nbins]
-    check(lib.lddl_bin_partitions(ctx.handle, _stream(), _ptr(num_tokens), n, _ptr(part_off),
-                                  n_part, bin_size, nbins, _ptr(perm), _ptr(bin_id), _ptr(counts)))
+    counts = torch.empty(max(n_part * nbins, 1), dtype=torch.int64, device=dev)[:n_part * nbins]
+    check(lib.lddl_bin_partitions(ctx.handle, _stream(), _ptr(num_tokens), _ptr(tok_off), n,
+                                  _ptr(part_off), n_part, bin_size, nbins, _ptr(perm),
+                                  _ptr(bin_id), _ptr(counts)))
     return perm, bin_id, counts.view(n_part, nbins)
 
 

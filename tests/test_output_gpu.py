@@ -50,6 +50,13 @@ def test_bin_many_partitions_vs_oracle(ctx):
         perm, bin_id, counts = bin_partitions(ctx, torch.from_numpy(nt).cuda(),
                                               torch.from_numpy(off).cuda(), bs, nb)
         perm, bin_id, counts = perm.cpu().numpy(), bin_id.cpu().numpy(), counts.cpu().numpy()
+        # the same rows given as a pair table's token offsets (num_tokens = len(A)+len(B)+3)
+        tok_off = np.concatenate([[0], np.cumsum(nt.astype(np.int64) - 3)]).astype(np.int64)
+        p2, b2, c2 = bin_partitions(ctx, None, torch.from_numpy(off).cuda(), bs, nb,
+                                    tok_off=torch.from_numpy(tok_off).cuda())
+        np.testing.assert_array_equal(p2.cpu().numpy(), perm)
+        np.testing.assert_array_equal(b2.cpu().numpy(), bin_id)
+        np.testing.assert_array_equal(c2.cpu().numpy(), counts)
         for p in range(len(sizes)):
             a, z = off[p], off[p + 1]
             eb, eo, ec = O.bin_samples(nt[a:z], bs, nb)
