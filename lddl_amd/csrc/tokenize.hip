@@ -411,27 +411,30 @@ __device__ WinResult classify_lanes(const Tables& T, const uint32_t* s_ascii,
                                     uint32_t byte, uint64_t BRK, bool tail_known) {
   const int lane = lane_id();
   const bool in = i < b1;
-  uint32_t cls = kSpace;  // beyond the sentence: a separator
+  // ASCII bytes for every lane without a branch (beyond the sentence: a separator); the
+  // non-ASCII and '[' lanes are revisited only in windows that have them (wave-uniform tests,
+  // so a plain window runs no exec-mask branches here)
+  const uint32_t ascii_e = s_ascii[byte & 127u];  // (read by every lane: no branch)
+  uint32_t cls = in ? ascii_e >> 30 : kSpace;
   int cplen = 1;          // bytes of the code point starting here (0: covered continuation)
   int spk = -1;           // literal special token starting here
-  bool slow = false;      // non-ASCII or dropped char: not for the register fast path
+  bool slow = in && cls == kDrop;  // non-ASCII or dropped char: not for the register fast path
   bool cont = false;
-  if (in) {
-    if (byte < 0x80) {
-      cls = s_ascii[byte] >> 30;
-      slow = cls == kDrop;
-      if (byte == '[') spk = match_special_at(T, text, i, b1);
-    } else if (byte >= 0xC0) {
+  if (ballot(in && byte >= 0x80)) {
+    if (in && byte >= 0xC0) {
       int64_t j = i;
       const uint32_t cp = utf8_next(text, b1, j);
       cplen = (int)(j - i);
       cls = tab_entry(T, cp) >> 30;
       slow = true;
-    } else {
+    } else if (in && byte >= 0x80) {
       cont = true;  // resolved below: covered by a valid lead, or a lone byte (U+FFFD, drop)
       cls = kDrop;
       slow = true;
     }
+  }
+  if (ballot(in && byte == '[')) {
+    if (in && byte == '[') spk = match_special_at(T, text, i, b1);
   }
   const uint64_t V2 = ballot(cplen == 2), V3 = ballot(cplen == 3), V4 = ballot(cplen == 4);
   bool cp_last = cplen <= 1;
