@@ -363,7 +363,8 @@ class RankBalance:
                     self.pb.tok_off, self.pb.n_pairs, None, order), [order.numel()])[0])
             return BalancedBins(self.pb, order, n_tokens=n_tokens, **kw)
         rt = self.rt
-        rt.tokens = recvs[0]
+        rt.tokens = recvs[0] if recvs[0].dtype == self.pb.tokens.dtype else recvs[0].view(
+            self.pb.tokens.dtype)
         if self.masking:
             rt.pos = recvs[1].view(self.pb.pos.dtype) if recvs[1].numel() else torch.zeros(
                 0, dtype=self.pb.pos.dtype, device=self.dev)
