@@ -725,18 +725,34 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Batched wave tokenizer. Classification per 64-byte window feeds an LDS queue of units that
-// spans sentences. When kSF units are queued they are resolved in two phases:
+// Streaming batched tokenizer (the product path).
+//
+// A wave claims chunks of kChunk consecutive sentences. Their text is one contiguous byte range
+// [A, A + span), which the wave streams in 64-byte banks, one byte per lane, at fixed positions:
+// a unit may span banks, so nothing is re-read. Sentence starts inside a bank are break bits
+// (BRK); units never cross them. Per bank, ballots give two masks:
+//   UNIT  bytes that belong to a pre-tokenizer unit (not a separator, inside the chunk)
+//   CONT  bytes that continue the unit of the byte before: the same word run (no break between),
+//         a continuation byte of an isolated char, the rest of a literal special token
+// Unit starts are UNIT & ~CONT; unit ends are UNIT & ~(CONT >> 1), which needs the next bank's
+// first CONT bit, so ends are enqueued one bank late. Starts (chunk-relative byte | kind | slow
+// flag) and ends go to two LDS queues in byte order: the k-th start and the k-th end are unit k.
+// Banks of plain ASCII (no byte >= 0x80, no control char, no '[', no special token carried in)
+// take the short path: one LDS class lookup and three compares per lane. The others take the
+// per-code-point classification (UTF-8 leads and continuations, literal specials, the Unicode
+// class table) with carries into the next bank.
+// Every kSF complete units are resolved in two phases:
 //   A (one lane per unit, 64 at a time): literal specials, and one full-length vocab probe of
 //     every ASCII word / punctuation unit. ~3/4 of the units are a single piece and are done.
 //   B (one lane per unit, 64 at a time): greedy longest-match WordPiece of the remaining "hard"
-//     units only (multi-piece words, non-ASCII). Deferring them across kSF units gives every
-//     lane of a phase-B pass a hard unit, instead of ~16 hard units and 48 idle lanes per 64-unit
-//     flush: the divergent longest-match loop (Bloom pass + descending probes per piece) runs
-//     ~3x less often (round 2: phase B was ~47 % of the kernel, counters in profiles/r02_*).
-// Pieces are then placed in queue order by a segmented scan over each in-flight sentence's
-// running count (a ring of kRing sentences); a phase-B chunk's pieces are placed before the next
-// chunk reuses the per-lane piece columns.
+//     units only (multi-piece words, non-ASCII), deferred across kSF units so that every lane of
+//     a phase-B pass has a hard unit.
+// Pieces are placed in queue order by a segmented scan over sentences (a unit's sentence by binary
+// search of the chunk's sentence starts in LDS). At the end of a chunk the remaining units are
+// resolved and every sentence's length (or its fallback) is written.
+// Round 2's design re-started a 64-byte window at the last unit start of the window before and
+// kept a ring of in-flight sentences; its per-window bookkeeping was ~half of the kernel's
+// instructions (profiles/r03l_pmc_tokenizer_variants.txt).
 // ---------------------------------------------------------------------------------------------
 #ifndef LDDL_TOK_SF
 #define LDDL_TOK_SF 192
@@ -745,35 +761,43 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
 #define LDDL_TOK_BW 16
 #endif
 constexpr int kSF = LDDL_TOK_SF;   // units resolved per pass (kSF / 64 phase-A rounds)
-constexpr int kQ = kSF + 64;       // queue capacity (a window adds <= 64 units)
-#ifndef LDDL_TOK_RING
-#define LDDL_TOK_RING 64
-#endif
-constexpr int kRing = LDDL_TOK_RING;  // sentences in flight per wave
+// queue capacity: before a bank < kSF complete units; a bank adds <= 64 ends and leaves <= 65
+// units open (started, end not yet enqueued)
+constexpr int kQ = kSF + 128;
 constexpr int kBW = LDDL_TOK_BW;   // waves per workgroup (one workgroup per CU shares the Bloom filter)
 #ifndef LDDL_TOK_CHUNK
 #define LDDL_TOK_CHUNK 128
 #endif
 constexpr int kChunk = LDDL_TOK_CHUNK;  // consecutive sentences claimed at a time
+static_assert((kChunk & (kChunk - 1)) == 0, "binary search over the chunk's sentences");
 using HIdx = std::conditional_t<(kSF > 256), uint16_t, uint8_t>;
 constexpr int32_t kHardBit = INT32_MIN;  // q_res: pieces are in column (res & 63) of pcs
+// q_s entry: chunk-relative start byte (bits 0..27) | kind (28..30: 0 word / isolated char,
+// 2 + k literal special k) | kQSlow (the unit holds a byte the register fast path cannot take)
+constexpr int32_t kQPos = (1 << 28) - 1;
+constexpr int32_t kQSlow = INT32_MIN;
+constexpr int64_t kMaxSpan = 1 << 28;  // longer chunks go to the lane kernel
+// r_cnt: pieces so far (bits 0..28) | kRFb (the sentence goes to the lane kernel) | kLenHasClsSep
+constexpr int32_t kRFb = 1 << 29;
+constexpr int32_t kRCnt = kRFb - 1;
+static_assert(kLenHasClsSep == (1 << 30), "r_cnt flag layout");
+// s_cls: fast-path byte classes
+enum : uint32_t { kFRun = 0, kFSep = 1, kFIso = 2, kFSlow = 4 };
 
-struct alignas(16) BatchLds {
-  int32_t q_rel[kQ];        // unit start relative to its sentence's first byte
-  uint8_t q_len[kQ], q_kind[kQ], q_slot[kQ], q_slow[kQ];
+struct alignas(16) StreamLds {
+  int32_t q_s[kQ];          // unit starts (see kQPos)
+  int32_t q_e[kQ];          // unit ends (inclusive, chunk-relative)
+  int32_t trash[64];        // target of the lanes that store nothing (no exec-mask branch)
   int32_t q_res[kSF];       // phase A/B result: the single piece id, or kHardBit | column
   uint8_t q_npc[kSF];       // pieces of the unit
   HIdx h_idx[kSF];          // queue positions of the hard units, in order
-  int64_t r_b0[kRing];
-  int32_t r_sent[kRing], r_count[kRing], r_flags[kRing], r_pending[kRing];
+  int32_t s_off[kChunk + 1];  // chunk-relative sentence starts; s_off[n] = the chunk's length
+  int32_t r_cnt[kChunk];    // see kRFb
   // lane l's pieces at pcs[64 q + l]; the same bytes hold lane l's normalised word (32 B at
   // byte 32 l) while phase B loads it into registers, before any piece is written
   alignas(16) int32_t pcs[kPcs * 64];
 };
 static_assert(kPcs * 64 * 4 >= 64 * kNorm, "normalised-word rows must fit the piece columns");
-
-// r_flags: kLenHasClsSep | sentence state
-enum : int32_t { kClosed = 1, kFallback = 2 };
 
 #ifndef LDDL_TOK_MIN_WAVES
 #define LDDL_TOK_MIN_WAVES 1
@@ -786,468 +810,375 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
     int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
     int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr) {
   __shared__ uint32_t s_ascii[128];
+  __shared__ uint8_t s_cls[256];
 #ifdef LDDL_TOK_BLOOM_GLOBAL  // A/B: Bloom filter read through the caches, LDS for more waves
   const uint32_t* s_bloom = T.bloom;
 #else
   __shared__ uint32_t s_bloom[kBloomWords];
 #endif
-  __shared__ BatchLds s_w[kBW];
+  __shared__ StreamLds s_w[kBW];
 #ifdef LDDL_STAMPS
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
   for (int c = threadIdx.x; c < 128; c += blockDim.x) s_ascii[c] = tab_entry(T, (uint32_t)c);
+  for (int c = threadIdx.x; c < 256; c += blockDim.x) {
+    uint32_t v = kFSlow;  // bytes >= 0x80, '[', and the ASCII chars the normaliser drops
+    if (c < 128 && c != '[') {
+      const uint32_t cl = tab_entry(T, (uint32_t)c) >> 30;
+      v = cl == kSpace ? kFSep : cl == kIso ? kFIso : cl == kWord ? kFRun : kFSlow;
+    }
+    s_cls[c] = (uint8_t)v;
+  }
 #ifndef LDDL_TOK_BLOOM_GLOBAL
   for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
 #endif
   __syncthreads();
   const int lane = lane_id();
-  BatchLds& W = s_w[threadIdx.x >> 6];
-  // sentence indices fit int32 (lddl_tokenize: n_sent < INT32_MAX); 32-bit state keeps the
-  // loop's scalar registers from spilling
+  StreamLds& W = s_w[threadIdx.x >> 6];
+  // sentence indices fit int32 (lddl_tokenize: n_sent < INT32_MAX - 2^22)
   const int32_t n_sent32 = (int32_t)n_sent;
-  // Sentences come in chunks of kChunk consecutive sentences: wave w starts with chunk w, then
-  // takes the next unclaimed chunk from chunk_ctr (initialised to the number of waves x kChunk).
-  // A static share per wave would leave a long tail: waves of one SIMD are issued oldest first,
-  // so the first finishes ~25 % before the last, which then runs alone and latency-bound.
-  // q0 = the next sentence to open, q1 = the one after it (whose chunk ends at ce); >= n_sent:
-  // none left.
-  int32_t ce = 0;
-  auto grab = [&]() -> int32_t {
-    int32_t c = 0;
-    if (lane == 0) c = atomicAdd(chunk_ctr, kChunk);
-    c = __builtin_amdgcn_readfirstlane(c);
-    ce = c < n_sent32 - kChunk ? c + kChunk : n_sent32;
-    return c < n_sent32 ? c : n_sent32;
-  };
-  auto succ = [&](int32_t x) -> int32_t {
-    if (x >= n_sent32) return n_sent32;
-    if (x + 1 < ce) return x + 1;
-    return grab();
-  };
-  int32_t q0, q1;
+  // Chunks: wave w starts with chunk w, then takes the next unclaimed chunk from chunk_ctr
+  // (initialised to the number of waves x kChunk). A static share per wave would leave a long
+  // tail: waves of one SIMD are issued oldest first, so the first finishes ~25 % before the last.
+  int32_t c0;
   {
-    const int32_t w = (int32_t)blockIdx.x * kBW + (int32_t)(threadIdx.x >> 6);
-    const int64_t c0 = (int64_t)w * kChunk;
-    q0 = c0 < n_sent32 ? (int32_t)c0 : n_sent32;
-    ce = c0 + kChunk < n_sent32 ? (int32_t)(c0 + kChunk) : n_sent32;
-    q1 = succ(q0);
+    const int64_t w = (int64_t)blockIdx.x * kBW + (threadIdx.x >> 6);
+    c0 = w * kChunk < n_sent32 ? (int32_t)(w * kChunk) : n_sent32;
   }
-  int32_t head = 0, tail = 0;  // ordinals of in-flight sentences: [head, tail)
-  int qn = 0;
-  bool cur = false;
-  int cur_slot = 0;
-  int64_t b0 = 0, b1 = 0, pos = 0;
-  // software prefetch: the next window's bytes are loaded as soon as its start is known (before
-  // the queue flush runs), and the next sentence's offsets one sentence ahead
-  uint32_t pbyte = 0x20u;
-  int64_t ppos = -1;
-  int pk = 64;  // the prefetched window's second-segment lane
-  // ... and the segment ends it was loaded against: consecutive sentences of a chunk are
-  // adjacent, so an empty sentence starts where the next one does and a start alone does not
-  // identify the window
-  int64_t pb1 = -1, pbB = -1;
-  int64_t nb0 = -1, nb1 = -1;
+  const uint64_t upto = (2ull << lane) - 1;  // lanes <= this one (lane 63: all)
 
-  // place queue units [u0, u1) (all resolved) in order: segmented scan per sentence
-  auto place = [&](int u0, int u1) {
-    for (int r0 = u0; r0 < u1; r0 += 64) {
-      const int u = r0 + lane;
-      const bool act = u < u1;
-      const int npc = act ? W.q_npc[u] : 0;
-      const int slot = act ? W.q_slot[u] : -1;
-      const int incl = wave_incl_scan(npc);
-      const int excl = incl - npc;
-      const int prev_slot = wave_prev(slot);
-      const uint64_t F = ballot(act && (lane == 0 || slot != prev_slot));
-      const int s0 = 63 - __clzll(F & (lane == 63 ? ~0ull : ((2ull << lane) - 1)));
-      const int seg_excl = excl - __shfl(excl, s0, 64);
-      const int next_slot = wave_next(slot);
-      const bool seg_last = act && (lane == 63 || u + 1 >= u1 || next_slot != slot);
-      if (act) {
-        const int o = W.r_count[slot] + seg_excl;
-        const int64_t bb = W.r_b0[slot];
-        const int32_t res = W.q_res[u];
-        if (res & kHardBit) {
-          const int col = res & 63;
-          for (int q = 0; q < npc; ++q)
-            if (o + q < max_pieces) ids[bb + o + q] = W.pcs[64 * q + col];
-        } else if (npc && o < max_pieces) {
-          ids[bb + o] = res;
-          const int kind = W.q_kind[u];
-          if (kind - 2 == kCls || kind - 2 == kSep) atomicOr(&W.r_flags[slot], kLenHasClsSep);
-        }
-      }
+  while (c0 < n_sent32) {
+    const int32_t n = n_sent32 - c0 < kChunk ? n_sent32 - c0 : kChunk;
+    const int64_t A = sent_off[c0];
+    const int64_t span64 = sent_off[c0 + n] - A;
+    if (span64 >= kMaxSpan) {  // pathological chunk (>= 256 MiB of text): the lane kernel
+      for (int j = lane; j < n; j += 64) fb_list[atomicAdd(fb_n, 1u)] = c0 + j;
+    } else {
+      for (int j = lane; j <= n; j += 64) W.s_off[j] = (int32_t)(sent_off[c0 + j] - A);
+      for (int j = lane; j < n; j += 64) W.r_cnt[j] = 0;
       wave_sync();
-      if (seg_last) {
-        W.r_count[slot] += seg_excl + npc;
-        W.r_pending[slot] -= lane - s0 + 1;
-      }
-      wave_sync();
-    }
-  };
+      const uint32_t span = (uint32_t)span64;
+      const uint8_t* __restrict__ ctext = text + A;
 
-  auto flush = [&]() {
-    const int m = qn < kSF ? qn : kSF;
-    // phase A: specials and single-piece words
-    int nh = 0;
-    {  // all rounds' text loads, then all first table loads, then the checks: one latency each
-      constexpr int kR = kSF / 64;
-      static_assert(kSF % 64 == 0, "phase A rounds");
-      bool elig[kR], hardr[kR];
-      int lenr[kR];
-      int32_t resr[kR];
-      B32 vv[kR];
-      Probe pr[kR];
+      // the sentence holding chunk-relative byte st (the last one starting at or before it: empty
+      // sentences at the same offset are skipped)
+      auto sent_of = [&](int32_t st) -> int {
+        int j = 0;
 #pragma unroll
-      for (int r = 0; r < kR; ++r) {
-        const int u = 64 * r + lane;
-        elig[r] = hardr[r] = false;
-        lenr[r] = 0;
-        resr[r] = 0;
-        if (u < m) {
-          const int kind = W.q_kind[u], len = W.q_len[u];
-          lenr[r] = len;
-          if (kind >= 2) {
-            resr[r] = T.special_id[kind - 2];
-          } else if (!W.q_slow[u] && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32) {
-            elig[r] = true;
-            vv[r] = load32(text, n_bytes, W.r_b0[W.q_slot[u]] + W.q_rel[u]);
-          } else {
-            hardr[r] = true;
-          }
-#ifdef LDDL_TOK_NO_WP  // A/B experiment only: classification + placement without WordPiece
-          elig[r] = hardr[r] = false;
-          resr[r] = len;
-#endif
+        for (int step = kChunk / 2; step >= 1; step >>= 1) {
+          const int k = j + step;
+          j = W.s_off[k < n ? k : n] <= st ? k : j;  // s_off[n] = span > st
         }
-      }
-#pragma unroll
-      for (int r = 0; r < kR; ++r)
-        if (elig[r]) {
-          if (T.ascii_mode == 1)
-            vv[r] = B32{swar_lower(vv[r].w0), swar_lower(vv[r].w1), swar_lower(vv[r].w2), swar_lower(vv[r].w3)};
-          pr[r] = probe_first(T, vv[r], lenr[r], 0);
-        }
-#pragma unroll
-      for (int r = 0; r < kR; ++r) {
-        if (elig[r]) {
-          resr[r] = probe_finish(T, vv[r], lenr[r], pr[r]);
-          hardr[r] = resr[r] < 0;
-        }
-        const int u = 64 * r + lane;
-        if (u < m && !hardr[r]) {
-          W.q_res[u] = resr[r];
-          W.q_npc[u] = 1;
-        }
-        const uint64_t H = ballot(hardr[r]);
-        if (hardr[r]) W.h_idx[nh + (int)popc_below(H)] = (HIdx)u;
-        nh += __popcll(H);
-      }
-    }
-    wave_sync();
-    // phase B in chunks of 64 hard units, each chunk placed with the units before the next one
-    int placed = 0;
-    for (int h0 = 0; h0 < nh; h0 += 64) {
-      const int hn = nh - h0 < 64 ? nh - h0 : 64;
-      int u = -1;
-      UnitWord uw;
-      uw.status = 1;
-      bool known_miss = false;
-      if (lane < hn) {
-        u = W.h_idx[h0 + lane];
-        const int len = W.q_len[u];
-        const bool slow = W.q_slow[u] != 0;
-        known_miss = !slow && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32;
-        uw = unit_word(T, s_ascii, text, n_bytes, W.r_b0[W.q_slot[u]] + W.q_rel[u], len, slow,
-                       reinterpret_cast<uint8_t*>(W.pcs) + 32 * lane);
-      }
-      wave_sync();  // every normalised word is in registers: the rows become piece columns
-      int npc = 0;
-#ifdef LDDL_TOK_COOP
-      // A/B experiment (the north_star matcher): a half-wave per hard word,
-      // lane (l & 31) probes piece length (l & 31) + 1 at the current start, the ballot's
-      // highest hit is the greedy longest match; the owner lane's piece column gets the pieces
-      (void)known_miss;
-      {
-        const int hl = lane & 31;
-        const uint64_t hm = (lane >> 5) ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
-        int my_n = 0;  // lane < hn: pieces of its own word (set by its half's leader below)
-        for (int w2 = 0; w2 < hn; w2 += 2) {
-          const int src = w2 + (lane >> 5);
-          const bool valid = src < hn;
-          const int sl = valid ? src : 0;
-          auto sh64 = [&](uint64_t x) {
-            return ((uint64_t)(uint32_t)__shfl((int)(x >> 32), sl, 64) << 32) |
-                   (uint32_t)__shfl((int)(uint32_t)x, sl, 64);
-          };
-          const B32 v{sh64(uw.v.w0), sh64(uw.v.w1), sh64(uw.v.w2), sh64(uw.v.w3)};
-          const int nb = __shfl(uw.nb, sl, 64), st = __shfl(uw.status, sl, 64);
-          const uint64_t ends = sh64(uw.ends);
-          int start = 0, n = valid ? (st < 0 ? -1 : 0) : 0;
-          bool live = valid && st == 0 && nb > 0;
-          while (ballot(live)) {
-            const int L = hl + 1;
-            const bool cand = live && start + L <= nb && L <= T.max_piece_bytes &&
-                              ((ends >> (start + L)) & 1ull);
-            const int32_t id = cand ? probe32(T, shr_bytes(v, start), L, start > 0 ? 1u : 0u) : -1;
-            const uint64_t M = ballot(id >= 0) & hm;
-            if (live) {
-              if (!M) {  // no piece at this start: the whole word is [UNK]
-                if (hl == 0) W.pcs[sl] = T.special_id[kUnk];
-                n = 1;
-                live = false;
-              } else {
-                const int best = 63 - __clzll(M);  // lane of the longest hit
-                const int32_t bid = __shfl(id, best, 64);
-                if (n == kPcs) {
-                  n = -1;
-                  live = false;
-                } else {
-                  if (hl == 0) W.pcs[64 * n + sl] = bid;
-                  ++n;
-                  start += (best & 31) + 1;
-                  if (start >= nb) live = false;
-                }
-              }
+        return j;
+      };
+
+      // place queue units [u0, u1) (all resolved) in order: segmented scan per sentence
+      auto place = [&](int u0, int u1) {
+        for (int r0 = u0; r0 < u1; r0 += 64) {
+          const int u = r0 + lane;
+          const bool act = u < u1;
+          const int uc = act ? u : u0;
+          const int32_t qs = W.q_s[uc];
+          const int npc = act ? W.q_npc[uc] : 0;
+          const int slot = act ? sent_of(qs & kQPos) : -1;
+          const int incl = wave_incl_scan(npc);
+          const int excl = incl - npc;
+          const int prev_slot = wave_prev(slot);
+          const uint64_t F = ballot(act && (lane == 0 || slot != prev_slot));
+          const int s0 = 63 - __clzll(F & upto);
+          const int seg_excl = excl - __shfl(excl, s0, 64);
+          const int next_slot = wave_next(slot);
+          const bool seg_last = act && (lane == 63 || u + 1 >= u1 || next_slot != slot);
+          if (act) {
+            const int o = (W.r_cnt[slot] & kRCnt) + seg_excl;
+            const int64_t bb = A + W.s_off[slot];
+            const int32_t res = W.q_res[u];
+            if (res & kHardBit) {
+              const int col = res & 63;
+              for (int q = 0; q < npc; ++q)
+                if (o + q < max_pieces) ids[bb + o + q] = W.pcs[64 * q + col];
+            } else if (npc && o < max_pieces) {
+              ids[bb + o] = res;
+              const int kind = (qs >> 28) & 7;
+              if (kind - 2 == kCls || kind - 2 == kSep) atomicOr(&W.r_cnt[slot], kLenHasClsSep);
             }
           }
-          // the owner lanes take their counts from the halves' leaders
-          const int c0 = __shfl(n, 0, 64), c1 = __shfl(n, 32, 64);
-          if (lane == w2) my_n = c0;
-          if (lane == w2 + 1) my_n = c1;
+          wave_sync();
+          if (seg_last) W.r_cnt[slot] += seg_excl + npc;  // (count bits only: < 2^28 pieces)
+          wave_sync();
         }
-        if (lane < hn) npc = my_n;
-        if (npc < 0) npc = -1;
-      }
-      if (lane < hn) {
-#else
-      if (lane < hn) {
-        Pcs pc{W.pcs + lane};
-        if (uw.status == 0) npc = wordpiece32(T, s_bloom, uw.v, uw.nb, uw.ends, pc, known_miss);
-        else if (uw.status < 0) npc = -1;
-#endif
-        if (npc < 0) {  // the sentence goes to the lane kernel
-          atomicOr(&W.r_flags[W.q_slot[u]], kFallback);
-          npc = 0;
-        }
-        W.q_res[u] = kHardBit | lane;
-        W.q_npc[u] = (uint8_t)npc;
-      }
-      wave_sync();
-      const int lim = h0 + 64 < nh ? (int)W.h_idx[h0 + 64] : m;
-      place(placed, lim);
-      placed = lim;
-    }
-    place(placed, m);
-    // drop the processed units from the queue (sources [m, qn) never overlap targets [0, qn-m)
-    // when qn - m <= 64 <= m; otherwise m == kSF and qn - m <= 63 < kSF)
-    const int rest = qn - m;
-    int32_t rel = 0;
-    uint8_t ql = 0, qk = 0, qs = 0, qw = 0;
-    if (lane < rest) {
-      rel = W.q_rel[m + lane];
-      ql = W.q_len[m + lane];
-      qk = W.q_kind[m + lane];
-      qs = W.q_slot[m + lane];
-      qw = W.q_slow[m + lane];
-    }
-    wave_sync();
-    if (lane < rest) {
-      W.q_rel[lane] = rel;
-      W.q_len[lane] = ql;
-      W.q_kind[lane] = qk;
-      W.q_slot[lane] = qs;
-      W.q_slow[lane] = qw;
-    }
-    wave_sync();
-    qn = rest;
-  };
+      };
 
-  auto retire = [&]() {
-    while (head < tail) {
-      const int sl = (int)(head % kRing);
-      const int st = W.r_flags[sl];
-      if (!(st & kClosed) || W.r_pending[sl] > 0) break;
-      {
-        const int32_t sid = W.r_sent[sl];
-        if (st & kFallback) {
-          if (lane == 0) fb_list[atomicAdd(fb_n, 1u)] = sid;
-        } else {
-          sent_len[sid] = (W.r_count[sl] < max_pieces ? W.r_count[sl] : max_pieces) | (st & kLenHasClsSep);
-        }
-      }
-      ++head;
-    }
-    wave_sync();
-  };
+      int ns = 0, ne = 0;  // queued unit starts / ends
 
-  while (true) {
-    if (!cur) {
-      const int32_t s = q0;
-      if (s >= n_sent32) break;
-      if (tail - head == kRing) {  // ring full: make room
-        flush();
-        retire();
-        continue;
-      }
-      cur_slot = (int)(tail % kRing);
-      if (nb0 >= 0) {
-        b0 = nb0;
-        b1 = nb1;
-      } else {
-        b0 = sent_off[s];
-        b1 = sent_off[s + 1];
-      }
-      nb0 = nb1 = -1;
-      q0 = q1;
-      q1 = succ(q1);
-      if (q0 < n_sent32) {
-        nb0 = sent_off[q0];
-        nb1 = sent_off[q0 + 1];
-      }
-      {  // every lane writes the same values (one merged write each, no exec-mask branch)
-        W.r_b0[cur_slot] = b0;
-        W.r_sent[cur_slot] = (int32_t)s;
-        W.r_count[cur_slot] = 0;
-        W.r_flags[cur_slot] = 0;
-        W.r_pending[cur_slot] = 0;
-      }
-      wave_sync();
-      pos = b0;
-      cur = true;
-      ++tail;
-    }
-    if (pos < b1) {
-      // a tail shorter than a window shares it with the head of the wave's next sentence (lanes
-      // >= k): sentences average ~2 windows, so this saves ~1 window in 6
-      int k = 64;
-      int slotB = cur_slot;
-      int64_t b0B = 0, b1B = 0;
-#ifdef LDDL_TOK_NO_COMBINE  // A/B experiment only: one sentence per window
-      if (false) {
-#else
-      if (b1 - pos < 64 && nb0 >= 0 && tail - head < kRing) {
+      // resolve and place the complete units [0, m), then drop them from the queue
+      auto flush = [&](int m) {
+        // phase A: specials and single-piece words
+        int nh = 0;
+        {  // all rounds' text loads, then all first table loads, then the checks: one latency each
+          constexpr int kR = kSF / 64;
+          static_assert(kSF % 64 == 0, "phase A rounds");
+          bool elig[kR], hardr[kR];
+          int lenr[kR];
+          int32_t resr[kR];
+          B32 vv[kR];
+          Probe pr[kR];
+#pragma unroll
+          for (int r = 0; r < kR; ++r) {
+            const int u = 64 * r + lane;
+            elig[r] = hardr[r] = false;
+            lenr[r] = 0;
+            resr[r] = 0;
+            if (u < m) {
+              const int32_t qs = W.q_s[u];
+              const int st = qs & kQPos, kind = (qs >> 28) & 7;
+              const int len = W.q_e[u] - st + 1;
+              lenr[r] = len;
+              if (kind >= 2) {
+                resr[r] = T.special_id[kind - 2];
+              } else if (qs >= 0 && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32) {
+                elig[r] = true;
+                vv[r] = load32(text, n_bytes, A + st);
+              } else {
+                hardr[r] = true;
+              }
+#ifdef LDDL_TOK_NO_WP  // A/B experiment only: classification + placement without WordPiece
+              elig[r] = hardr[r] = false;
+              resr[r] = len;
 #endif
-        const int32_t sn = q0;  // the sentence nb0 / nb1 belong to
-        k = (int)(b1 - pos);
-        slotB = (int)(tail % kRing);
-        b0B = nb0;
-        b1B = nb1;
-        {
-          W.r_b0[slotB] = b0B;
-          W.r_sent[slotB] = sn;
-          W.r_count[slotB] = 0;
-          W.r_flags[slotB] = 0;
-          W.r_pending[slotB] = 0;
-        }
-        ++tail;
-        nb0 = nb1 = -1;
-        q0 = q1;
-        q1 = succ(q1);
-        if (q0 < n_sent32) {
-          nb0 = sent_off[q0];
-          nb1 = sent_off[q0 + 1];
-        }
-      }
-      const bool segB = lane >= k;
-      const int64_t il = segB ? b0B + (lane - k) : pos + lane;
-      const int64_t b1l = segB ? b1B : b1;
-      const bool pf = ppos == pos && pk == k && pb1 == b1 && (k == 64 || pbB == b1B);
-      const uint32_t byte = pf ? pbyte : (il < b1l ? text[il] : 0x20u);
-      const bool tail_known = k < 64 ? b0B + (64 - k) >= b1B : pos + 64 >= b1;
-      const WinResult R = classify_lanes(T, s_ascii, text, il, b1l, byte, k < 64 ? 1ull << k : 0ull,
-                                         tail_known);
-      // where the next window starts, in the last segment's sentence
-      const int64_t lb1 = k < 64 ? b1B : b1;
-      int64_t next;
-      if (R.next_lane < 0) {
-        next = lb1;
-      } else {
-        const int nl = R.next_lane < 64 ? R.next_lane : 63;
-        next = ((int64_t)__builtin_amdgcn_readlane((int)(il >> 32), nl) << 32) |
-               (uint32_t)__builtin_amdgcn_readlane((int)il, nl);
-        if (R.next_lane == 64) ++next;
-      }
-#ifdef LDDL_TOK_PREFETCH
-      // the next window's bytes, on the same lane mapping it will use (checked by pos and k).
-      // Off by default since the sentence chunks: consecutive windows of a wave read adjacent
-      // text that the previous window's loads already brought into L2 (2 GiB: 33.2 ms with
-      // the prefetch, 32.8 without; profiles/r02_tok_variants_chunks.txt)
-      if (next < lb1) {
-#ifdef LDDL_TOK_NO_COMBINE
-        const int kk = 64;
-#else
-        const int kk = lb1 - next < 64 && nb0 >= 0 && tail - head < kRing ? (int)(lb1 - next) : 64;
-#endif
-        const int64_t ip = lane >= kk ? nb0 + (lane - kk) : next + lane;
-        pbyte = ip < (lane >= kk ? nb1 : lb1) ? text[ip] : 0x20u;
-        ppos = next;
-        pk = kk;
-        pb1 = lb1;
-        pbB = kk < 64 ? nb1 : -1;
-      } else if (nb0 >= 0) {  // the next sentence's first window
-        ppos = nb0;
-        pk = 64;
-        pb1 = nb1;
-        pbB = -1;
-        pbyte = nb0 + lane < nb1 ? text[nb0 + lane] : 0x20u;
-      }
-#endif
-      if (R.fallback) {  // (one segment only: a two-segment window's first units are complete)
-        if (lane == 0) W.r_flags[cur_slot] |= kFallback;
-        pos = b1;
-      } else {
-        // enqueue straight from the masks: unit k's start lane writes its start, kind and slot,
-        // its end lane the length (the unit's start is the last start at or below it), and its
-        // slow bytes (all inside units) set its slow flag after the start lane cleared it. A
-        // trailing incomplete unit writes queue entry qn + n, which stays outside the queue.
-        const int n = R.n_units;
-        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-        if ((R.US >> lane) & 1ull) {
-          const int q = qn + (int)popc_below(R.US);
-          W.q_rel[q] = (int32_t)(il - (segB ? b0B : b0));
-          W.q_kind[q] = (uint8_t)R.ukind;
-          W.q_slot[q] = (uint8_t)(segB ? slotB : cur_slot);
-          W.q_slow[q] = 0;
-        }
-        if ((R.UE >> lane) & 1ull)
-          W.q_len[qn + (int)popc_below(R.UE)] = (uint8_t)(lane - (63 - __clzll(R.US & upto)) + 1);
-        if (((R.slow >> lane) & 1ull) && R.unit_byte) W.q_slow[qn + __popcll(R.US & upto) - 1] = 1;
-        if (k < 64) {  // the first segment's sentence is complete: the second one becomes current
-          const int na = __popcll(R.UE & ((1ull << k) - 1));
-          {  // (all lanes read the same old values and write the same new ones)
-            W.r_pending[cur_slot] += na;
-            W.r_flags[cur_slot] |= kClosed;
-            W.r_pending[slotB] += n - na;
+            }
           }
-          cur_slot = slotB;
-          b0 = b0B;
-          b1 = b1B;
-        } else {
-          W.r_pending[cur_slot] += n;
+#pragma unroll
+          for (int r = 0; r < kR; ++r)
+            if (elig[r]) {
+              if (T.ascii_mode == 1)
+                vv[r] = B32{swar_lower(vv[r].w0), swar_lower(vv[r].w1), swar_lower(vv[r].w2), swar_lower(vv[r].w3)};
+              pr[r] = probe_first(T, vv[r], lenr[r], 0);
+            }
+#pragma unroll
+          for (int r = 0; r < kR; ++r) {
+            if (elig[r]) {
+              resr[r] = probe_finish(T, vv[r], lenr[r], pr[r]);
+              hardr[r] = resr[r] < 0;
+            }
+            const int u = 64 * r + lane;
+            if (u < m && !hardr[r]) {
+              W.q_res[u] = resr[r];
+              W.q_npc[u] = 1;
+            }
+            const uint64_t H = ballot(hardr[r]);
+            if (hardr[r]) W.h_idx[nh + (int)popc_below(H)] = (HIdx)u;
+            nh += __popcll(H);
+          }
         }
         wave_sync();
-        qn += n;
-        pos = next;
+        // phase B in chunks of 64 hard units, each chunk placed with the units before the next one
+        int placed = 0;
+        for (int h0 = 0; h0 < nh; h0 += 64) {
+          const int hn = nh - h0 < 64 ? nh - h0 : 64;
+          int u = -1, st = 0;
+          UnitWord uw;
+          uw.status = 1;
+          bool known_miss = false;
+          if (lane < hn) {
+            u = W.h_idx[h0 + lane];
+            const int32_t qs = W.q_s[u];
+            st = qs & kQPos;
+            const int len = W.q_e[u] - st + 1;
+            const bool slow = qs < 0;
+            known_miss = !slow && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32;
+            uw = unit_word(T, s_ascii, text, n_bytes, A + st, len, slow,
+                           reinterpret_cast<uint8_t*>(W.pcs) + 32 * lane);
+          }
+          wave_sync();  // every normalised word is in registers: the rows become piece columns
+          int npc = 0;
+          if (lane < hn) {
+            Pcs pc{W.pcs + lane};
+            if (uw.status == 0) npc = wordpiece32(T, s_bloom, uw.v, uw.nb, uw.ends, pc, known_miss);
+            else if (uw.status < 0) npc = -1;
+            if (npc < 0) {  // the sentence goes to the lane kernel
+              atomicOr(&W.r_cnt[sent_of(st)], kRFb);
+              npc = 0;
+            }
+            W.q_res[u] = kHardBit | lane;
+            W.q_npc[u] = (uint8_t)npc;
+          }
+          wave_sync();
+          const int lim = h0 + 64 < nh ? (int)W.h_idx[h0 + 64] : m;
+          place(placed, lim);
+          placed = lim;
+        }
+        place(placed, m);
+        // drop the processed units: < 128 starts and < 128 ends remain (read all, then write)
+        const int rs = ns - m, re = ne - m;
+        int32_t a0 = 0, a1 = 0, e0 = 0, e1 = 0;
+        if (lane < rs) a0 = W.q_s[m + lane];
+        if (lane + 64 < rs) a1 = W.q_s[m + 64 + lane];
+        if (lane < re) e0 = W.q_e[m + lane];
+        if (lane + 64 < re) e1 = W.q_e[m + 64 + lane];
+        wave_sync();
+        if (lane < rs) W.q_s[lane] = a0;
+        if (lane + 64 < rs) W.q_s[64 + lane] = a1;
+        if (lane < re) W.q_e[lane] = e0;
+        if (lane + 64 < re) W.q_e[64 + lane] = e1;
+        wave_sync();
+        ns = rs;
+        ne = re;
+      };
+
+      // ---- the chunk's banks ----
+      uint64_t UNITp = 0, CONTp = 0;  // the bank before
+      uint64_t cin = 0;               // the byte before the bank is a word-run byte
+      // slow-path carries into the next bank: code-point coverage of its first lanes (bit k: lane
+      // k continues a lead of the bank before, for leads of 2 / 3 / 4 bytes), special-token bytes,
+      // and the (class | cplen << 4) of the bank's lanes 61..63
+      uint64_t k1 = 0, k2 = 0, k3 = 0, insc = 0;
+      int32_t plc61 = 0, plc62 = 0, plc63 = 0;
+      int32_t jn = 1;  // the next sentence start to mark
+      uint32_t nextS = (uint32_t)__builtin_amdgcn_readfirstlane(W.s_off[1]);
+      const uint32_t last = span ? span - 1 : 0;
+      // software prefetch two banks ahead (clamped into the chunk; bytes past it are unused)
+      uint32_t pf1 = 0x20u, pf2 = 0x20u;
+      if (span) {
+        pf1 = ctext[(uint32_t)lane < last ? (uint32_t)lane : last];
+        pf2 = ctext[64u + lane < last ? 64u + lane : last];
       }
-    }
-    if (pos >= b1) {
-      W.r_flags[cur_slot] |= kClosed;
+      uint32_t x0 = 0;
+      for (; x0 < span; x0 += 64) {
+        const uint32_t byte = pf1;
+        pf1 = pf2;
+        {
+          const uint32_t xq = x0 + 128u + lane;
+          pf2 = ctext[xq < last ? xq : last];
+        }
+        const uint32_t x = x0 + lane;
+        const bool in = x < span;
+        uint64_t BRK = 0;
+        while (nextS < x0 + 64) {
+          BRK |= 1ull << (nextS - x0);
+          ++jn;
+          nextS = jn <= n ? (uint32_t)__builtin_amdgcn_readfirstlane(W.s_off[jn]) : 0xFFFFFFFFu;
+        }
+        const uint32_t v = s_cls[byte];
+        const uint64_t VALID = ballot(in);
+        uint64_t RUN, UNIT, CONT, SL = 0;
+        int32_t sval = (int32_t)x;
+        if (!(ballot(v >= kFSlow) | insc | k1 | k2 | k3)) {  // plain ASCII bank
+          RUN = ballot(v == kFRun) & VALID;
+          UNIT = VALID & ~ballot(v == kFSep);
+          CONT = RUN & ((RUN << 1) | cin) & ~BRK;
+        } else {
+          // this lane's sentence end: the next break above the lane, else the first sentence start
+          // after the bank
+          const uint64_t above = BRK & ~upto;
+          const uint32_t se = above ? x0 + (uint32_t)(__ffsll((long long)above) - 1)
+                                    : (nextS < span ? nextS : span);
+          const int64_t i = A + x, b1 = A + se;
+          uint32_t cls = in ? s_ascii[byte & 127u] >> 30 : kSpace;
+          int cplen = 1;  // bytes of the code point starting here (0: covered continuation)
+          int spk = -1;   // literal special token starting here
+          bool slow = in && cls == kDrop;
+          bool cont = false;
+          if (ballot(in && byte >= 0x80)) {
+            if (in && byte >= 0xC0) {
+              int64_t j = i;
+              const uint32_t cp = utf8_next(text, b1, j);
+              cplen = (int)(j - i);
+              cls = tab_entry(T, cp) >> 30;
+              slow = true;
+            } else if (in && byte >= 0x80) {
+              cont = true;  // covered by a valid lead, or a lone byte (U+FFFD, dropped)
+              cls = kDrop;
+              slow = true;
+            }
+          }
+          if (ballot(in && byte == '[')) {
+            if (in && byte == '[') spk = match_special_at(T, text, i, b1);
+          }
+          const int32_t val = (int32_t)(cls | ((uint32_t)cplen << 4));
+          const uint64_t V2 = ballot(cplen == 2), V3 = ballot(cplen == 3), V4 = ballot(cplen == 4);
+          const uint64_t C1 = ((V2 | V3 | V4) << 1) | k1, C2 = ((V3 | V4) << 2) | k2, C3 = (V4 << 3) | k3;
+          if (C1 | C2 | C3) {  // code points of more than one byte (wave-uniform branch)
+            const bool covered = cont && (((C1 | C2 | C3) >> lane) & 1ull);
+            const int dist = !covered ? 0 : ((C1 >> lane) & 1ull) ? 1 : ((C2 >> lane) & 1ull) ? 2 : 3;
+            int lead = __shfl(val, lane - dist, 64);
+            if (lane < dist) lead = lane - dist == -1 ? plc63 : lane - dist == -2 ? plc62 : plc61;
+            if (covered) {  // a covered continuation takes its lead's class
+              cls = (uint32_t)lead & 3u;
+              cplen = 0;
+            }
+          }
+          const uint64_t S = ballot(spk >= 0), S6 = ballot(spk == kMask);
+          const uint64_t inside = (S << 1) | (S << 2) | (S << 3) | (S << 4) | (S6 << 5) | insc;
+          const bool in_sp = ((S | inside) >> lane) & 1ull;
+          const uint32_t cat = in_sp ? kCatSpecial : cls == kSpace ? kCatSep : cls == kIso ? kCatIso : kCatRun;
+          RUN = ballot(cat == kCatRun);
+          const uint64_t ISO = ballot(cat == kCatIso), LEAD = ballot(cplen > 0);
+          UNIT = ballot(cat != kCatSep);
+          CONT = (RUN & ((RUN << 1) | cin) & ~BRK) | (ISO & ~LEAD) | inside;
+          sval = (int32_t)(x | ((uint32_t)(spk >= 0 ? 2 + spk : 0) << 28));
+          SL = ballot(slow && cat != kCatSep);
+          k1 = (V2 | V3 | V4) >> 63;
+          k2 = (V3 | V4) >> 62;
+          k3 = V4 >> 61;
+          insc = (S >> 63) | (S >> 62) | (S >> 61) | (S >> 60) | (S6 >> 59);
+          plc61 = __builtin_amdgcn_readlane(val, 61);
+          plc62 = __builtin_amdgcn_readlane(val, 62);
+          plc63 = __builtin_amdgcn_readlane(val, 63);
+        }
+        // starts of this bank (lanes without one store to their trash slot)
+        const uint64_t US = UNIT & ~CONT;
+        {
+          const uint32_t r = popc_below(US) + (uint32_t)ns;
+          int32_t* dst = ((US >> lane) & 1ull) ? &W.q_s[r] : &W.trash[lane];
+          *dst = sval;
+        }
+        if (SL) {  // slow bytes flag their unit (started in this bank or before)
+          if ((SL >> lane) & 1ull) atomicOr(&W.q_s[ns + (int)__popcll(US & upto) - 1], kQSlow);
+        }
+        ns += (int)__popcll(US);
+        // ends of the bank before
+        const uint64_t UEp = UNITp & ~((CONTp >> 1) | (CONT << 63));
+        {
+          const uint32_t r = popc_below(UEp) + (uint32_t)ne;
+          int32_t* dst = ((UEp >> lane) & 1ull) ? &W.q_e[r] : &W.trash[lane];
+          *dst = (int32_t)(x - 64u);
+        }
+        ne += (int)__popcll(UEp);
+        cin = RUN >> 63;
+        UNITp = UNIT;
+        CONTp = CONT;
+        if (ne >= kSF) {
+          wave_sync();
+          flush(kSF);
+        }
+      }
+      {  // the last bank's ends (nothing continues past the chunk)
+        const uint64_t UEp = UNITp & ~(CONTp >> 1);
+        const uint32_t r = popc_below(UEp) + (uint32_t)ne;
+        int32_t* dst = ((UEp >> lane) & 1ull) ? &W.q_e[r] : &W.trash[lane];
+        *dst = (int32_t)(x0 - 64u + lane);
+        ne += (int)__popcll(UEp);
+      }
       wave_sync();
-      cur = false;
+      while (ne > 0) flush(ne < kSF ? ne : kSF);
+      // the chunk's sentences
+      for (int j = lane; j < n; j += 64) {
+        const int32_t rc = W.r_cnt[j];
+        if (rc & kRFb) {
+          fb_list[atomicAdd(fb_n, 1u)] = c0 + j;
+        } else {
+          const int32_t cnt = rc & kRCnt;
+          sent_len[c0 + j] = (cnt < max_pieces ? cnt : max_pieces) | (rc & kLenHasClsSep);
+        }
+      }
+      wave_sync();  // before the next chunk reuses s_off / r_cnt
     }
-    if (qn >= kSF) {
-      flush();
-      // the open sentence already has max_pieces pieces: the rest of it cannot be kept
-      if (cur && W.r_count[cur_slot] >= max_pieces) pos = b1;
-      retire();  // sentences complete only when their units are placed, i.e. in a flush
-    }
+    int32_t nc = 0;
+    if (lane == 0) nc = atomicAdd(chunk_ctr, kChunk);
+    nc = __builtin_amdgcn_readfirstlane(nc);
+    c0 = nc < n_sent32 ? nc : n_sent32;
   }
-  while (qn > 0) {
-    flush();
-    retire();
-  }
-  retire();
 #ifdef LDDL_STAMPS
   if (lane == 0 && g_tok_tl) {
     const int64_t wv = (int64_t)blockIdx.x * kBW + (threadIdx.x >> 6);
