@@ -140,6 +140,7 @@ struct lddl_ctx {
   uint8_t* d_render = nullptr;      // full token strings (as in vocab.txt, "##" kept)
   int64_t* d_render_off = nullptr;  // token i = d_render[off[i] .. off[i+1])
   uint32_t* d_bloom = nullptr;
+  uint64_t* d_vlong = nullptr;
   int32_t vocab_size = 0;
   size_t lds_per_block = 0;         // hipDeviceAttributeMaxSharedMemoryPerBlock of `device`
   std::vector<std::string> tokens;  // host copy of the vocab lines

@@ -132,6 +132,13 @@ extern "C" int lddl_ctx_create(int device, const uint8_t* norm_table, int64_t ta
     const uint32_t x = bloom_mix(h, (uint32_t)len, cont[i]);
     bloom[bloom_word(x)] |= bloom_bits(x);
   }
+  // 32-byte zero-padded copies of the pieces (longer pieces keep only their first 32 bytes: a
+  // probe key is at most 32 bytes, so they never reach the tail check)
+  std::vector<uint64_t> vlong(4 * (size_t)V, 0ull);
+  for (int32_t i = 0; i < V; ++i) {
+    const int len = (int)(voff[i + 1] - voff[i]);
+    memcpy(reinterpret_cast<uint8_t*>(vlong.data() + 4 * (size_t)i), vbytes.data() + voff[i], std::min(len, 32));
+  }
   const uint8_t* l1 = norm_table + 20;
   const uint8_t* pages = l1 + 2 * 4352;
   const uint8_t* pool = pages + 4 * 256 * (int64_t)n_pages;
@@ -142,7 +149,8 @@ extern "C" int lddl_ctx_create(int device, const uint8_t* norm_table, int64_t ta
       (rc = upload(&c->d_voff, voff.data(), sizeof(int64_t) * voff.size())) ||
       (rc = upload(&c->d_render, render.data(), render.size())) ||
       (rc = upload(&c->d_render_off, roff.data(), sizeof(int64_t) * roff.size())) ||
-      (rc = upload(&c->d_bloom, bloom.data(), sizeof(uint32_t) * bloom.size()))) {
+      (rc = upload(&c->d_bloom, bloom.data(), sizeof(uint32_t) * bloom.size())) ||
+      (rc = upload(&c->d_vlong, vlong.data(), sizeof(uint64_t) * vlong.size()))) {
     lddl_ctx_destroy(c);
     return rc;
   }
@@ -155,6 +163,7 @@ extern "C" int lddl_ctx_create(int device, const uint8_t* norm_table, int64_t ta
   T.voff = c->d_voff;
   T.vmask = cap - 1;
   T.bloom = c->d_bloom;
+  T.vlong = c->d_vlong;
   T.max_piece_bytes = max_piece;
   static const char* kSpecial[kNumSpecial] = {"[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"};
   for (int k = 0; k < kNumSpecial; ++k) {
@@ -188,7 +197,7 @@ extern "C" int lddl_ctx_destroy(lddl_ctx* c) {
   lddl_punkt_release(c);
   for (void* p : {(void*)c->d_l1, (void*)c->d_pages, (void*)c->d_pool, (void*)c->d_vhash,
                   (void*)c->d_vbytes, (void*)c->d_voff, (void*)c->d_render, (void*)c->d_render_off,
-                  (void*)c->d_bloom})
+                  (void*)c->d_bloom, (void*)c->d_vlong})
     if (p) (void)hipFree(p);
   delete c;
   return 0;

@@ -59,6 +59,9 @@ struct Tables {
   // a-z (uncased table), 2 = all map to themselves (cased), 0 = neither (fast path disabled)
   int32_t ascii_mode;
   const uint32_t* bloom;  // kBloomWords words: Bloom filter of (continuation, piece bytes)
+  // piece i's first 32 bytes, zero-padded, at vlong[4 i .. 4 i + 4): the tail check of a hash hit
+  // on a piece longer than the 12-byte key, as three masked 64-bit compares
+  const uint64_t* vlong;
 };
 
 // Bloom filter over vocab pieces for the longest-match scan: a piece's prefix hash is a

@@ -262,8 +262,18 @@ struct Pcs {
   __device__ int32_t get(int q) const { return b[64 * q]; }
 };
 
+// Bytes 8 .. len-1 (len 13..32) of a against piece id's zero-padded 32-byte copy (the hash key
+// already matched bytes 0..11).
+__device__ inline bool tail_match(const Tables& T, int32_t id, const B32& a, int len) {
+  const ulonglong2* p = reinterpret_cast<const ulonglong2*>(T.vlong + 4 * (int64_t)id);
+  const ulonglong2 lo = p[0], hi = p[1];
+  const uint64_t d = keep_bytes(lo.y ^ a.w1, len - 8) | keep_bytes(hi.x ^ a.w2, len - 16) |
+                     keep_bytes(hi.y ^ a.w3, len - 24);
+  return d == 0;
+}
+
 // Vocab probe of the first `len` (1..32) bytes of a: exact key for <= 12 bytes (k0 = bytes 0..7,
-// k1 = bytes 8..11), longer pieces confirmed against their bytes.
+// k1 = bytes 8..11), longer pieces confirmed against their 32-byte copies.
 __device__ inline int32_t probe32(const Tables& T, const B32& a, int len, uint32_t cont) {
   const uint64_t k0 = keep_bytes(a.w0, len);
   const uint32_t k1 = (uint32_t)keep_bytes(a.w1, len - 8 < 4 ? len - 8 : 4);
@@ -272,17 +282,9 @@ __device__ inline int32_t probe32(const Tables& T, const B32& a, int len, uint32
   for (uint32_t slot = (uint32_t)vhash(k0, k1, len, cont) & T.vmask;; slot = (slot + 1) & T.vmask) {
     const VEnt e = T.vhash[slot];
     if (!(e.meta & kMetaValid)) return -1;
-    if (e.k0 == k0 && e.k1 == k1 && (e.meta & ~0x1FFFFFu) == want) {
-      const int32_t id = meta_id(e.meta);
-      if (len <= 12) return id;
-      const uint8_t* p = T.vbytes + T.voff[id];
-      bool ok = true;
-      for (int i = 12; i < len; ++i) {
-        const uint64_t wv = i < 16 ? a.w1 : i < 24 ? a.w2 : a.w3;
-        ok &= p[i] == (uint8_t)(wv >> (8 * (i & 7)));
-      }
-      if (ok) return id;
-    }
+    if (e.k0 == k0 && e.k1 == k1 && (e.meta & ~0x1FFFFFu) == want &&
+        (len <= 12 || tail_match(T, meta_id(e.meta), a, len)))
+      return meta_id(e.meta);
   }
 }
 
@@ -306,17 +308,9 @@ __device__ inline Probe probe_first(const Tables& T, const B32& a, int len, uint
 __device__ inline int32_t probe_finish(const Tables& T, const B32& a, int len, Probe q) {
   for (;;) {
     if (!(q.e.meta & kMetaValid)) return -1;
-    if (q.e.k0 == q.k0 && q.e.k1 == q.k1 && (q.e.meta & ~0x1FFFFFu) == q.want) {
-      const int32_t id = meta_id(q.e.meta);
-      if (len <= 12) return id;
-      const uint8_t* p = T.vbytes + T.voff[id];
-      bool ok = true;
-      for (int i = 12; i < len; ++i) {
-        const uint64_t wv = i < 16 ? a.w1 : i < 24 ? a.w2 : a.w3;
-        ok &= p[i] == (uint8_t)(wv >> (8 * (i & 7)));
-      }
-      if (ok) return id;
-    }
+    if (q.e.k0 == q.k0 && q.e.k1 == q.k1 && (q.e.meta & ~0x1FFFFFu) == q.want &&
+        (len <= 12 || tail_match(T, meta_id(q.e.meta), a, len)))
+      return meta_id(q.e.meta);
     q.slot = (q.slot + 1) & T.vmask;
     q.e = T.vhash[q.slot];
   }
@@ -329,15 +323,17 @@ __device__ inline uint32_t bloom_candidates32(const uint32_t* bloom, const B32& 
   uint32_t h = 0, cand = 0;
 #pragma unroll
   for (int L = 1; L <= 32; ++L) {
-    if (L > maxl) break;
+    // wave-uniform exit (lanes past their own maxl compute don't-care bits, masked below): no
+    // exec-mask bookkeeping per length
+    if (!ballot(L <= maxl)) break;
     const uint64_t wv = L <= 8 ? a.w0 : L <= 16 ? a.w1 : L <= 24 ? a.w2 : a.w3;
     const uint32_t byte = (uint32_t)(wv >> (8 * ((L - 1) & 7))) & 0xFFu;
     h = h * kBloomP + byte + 1u;
     const uint32_t x = bloom_mix(h, (uint32_t)L, cont);
     const uint32_t m = bloom_bits(x);
-    if ((bloom[bloom_word(x)] & m) == m) cand |= 1u << (L - 1);
+    cand |= (bloom[bloom_word(x)] & m) == m ? 1u << (L - 1) : 0u;
   }
-  return cand;
+  return maxl >= 32 ? cand : cand & ((1u << maxl) - 1u);
 }
 
 // Greedy longest-match WordPiece (HF WordPiece::tokenize) of a normalised word of nb <= 32 bytes
@@ -353,7 +349,10 @@ __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v,
     const uint32_t cont = start > 0;
     const uint64_t e = ends >> start;  // bit L: a piece of length L may end here
     int len = nb - start < T.max_piece_bytes ? nb - start : T.max_piece_bytes;
-    while (len > 0 && !((e >> len) & 1ull)) --len;
+    {  // the longest length <= len that ends on a character boundary (bit L-1 of okl: length L)
+      const uint64_t okl = (e >> 1) & ((1ull << len) - 1ull);
+      len = okl ? 64 - __clzll(okl) : 0;
+    }
     // (the caller may already know that the whole word is not one piece)
     int32_t id = len > 0 && !(first_probe_missed && start == 0 && len == nb) ? probe32(T, a, len, cont)
                                                                               : -1;
