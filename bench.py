@@ -671,8 +671,10 @@ def main():
         return dt, out_tokens, evs, stats, sent_len
 
     dt, out_tokens, evs, stats, sent_len = timed(args.rng)
+    mem_head = torch.cuda.memory_stats()  # the headline's own allocator record
     pcie_line = ref_part = None
     if world == 1 and args.workload == 'c2' and args.extra_lines:
+        torch.cuda.empty_cache()  # (between lines, untimed) each line starts from an empty pool
         # the same step with the text arriving over PCIe (never `value`)
         h_text = torch.from_numpy(corp.text).pin_memory()
         h_so = torch.from_numpy(corp.sent_off).pin_memory()
@@ -715,6 +717,7 @@ def main():
         ref_part = {'partition_bytes': int(ref_pb), 'partitions': int(len(rpart) - 1),
                     'note': 'reference example partitioning: --num-blocks 4096 over the batch'}
         for r in ('replay', 'native'):
+            torch.cuda.empty_cache()
             rdt, rtok, _, rst, _ = timed(r, b=rb)
             ref_part[r] = {'value': rtok / rdt, 'ms_per_step': rdt / args.steps * 1e3,
                            'plan_ms': float(np.mean([x['plan_ms'] for x in rst]))}
@@ -741,11 +744,13 @@ def main():
     alt = None
     if args.alt_rng:  # the other RNG mode on the same batch, reported beside the headline
         other = 'native' if args.rng == 'replay' else 'replay'
+        torch.cuda.empty_cache()
         adt, atok, _, astats, _ = timed(other)
         alt = {'rng': other, 'value': atok / adt, 'ms_per_step': adt / args.steps * 1e3,
                'plan_ms': float(np.mean([x['plan_ms'] for x in astats]))}
     seg = None
     if args.segmented_line and world == 1:  # the same path from raw document text: Punkt first
+        torch.cuda.empty_cache()
         seg = timed_segmented(args, rank, world, ctx, dev)
         if args.punkt_params:  # the trained-model kernel on the same documents
             from lddl_amd.punkt import PunktParams
@@ -786,11 +791,17 @@ def main():
                 rec = json.load(f)
         except (OSError, ValueError):
             continue
-        if rec.get('batch_bytes') == args.batch_bytes:
+        if rec.get('batch_bytes') in (args.batch_bytes, int(n_bytes)):  # requested or actual size
             pmc_kernels, pmc_src = rec.get('kernels', {}), os.path.basename(pmc)
 
+    def pmc_of(kernel):  # by name; template instantiations (`name<...>`) match their base name
+        for k, v in pmc_kernels.items():
+            if k == kernel or k.startswith(kernel + '<'):
+                return v
+        return {}
+
     def traffic(kernel):
-        return pmc_kernels.get(kernel, {}).get('hbm_bytes_per_launch')
+        return pmc_of(kernel).get('hbm_bytes_per_launch')
     # issue peaks per chip (profiles/r02_issue_rate_probe.txt, tools/ubench/issue_rate.hip): a
     # SIMD issues one wave64 VALU instruction per 2 cycles (32-wide SIMD, >= 2 waves) and one SALU
     # instruction per 4 cycles (the CU's scalar unit serves its 4 SIMDs in turn)
@@ -798,7 +809,7 @@ def main():
     salu_peak = 256 * 4 * 2.4e9 / 4
 
     def issue(kernel, ms):
-        k = pmc_kernels.get(kernel, {})
+        k = pmc_of(kernel)
         v, sc = k.get('SQ_INSTS_VALU'), k.get('SQ_INSTS_SALU')
         if not v or not ms:
             return None
@@ -885,9 +896,12 @@ def main():
         res['pcie_inclusive'] = pcie_line
     if ref_part is not None:
         res['ref_partitioning'] = ref_part
-    res['torch_alloc_retries'] = int(mem.get('num_alloc_retries', 0))
+    res['torch_alloc_retries'] = int(mem_head.get('num_alloc_retries', 0))  # headline line
+    res['torch_alloc_retries_all_lines'] = int(mem.get('num_alloc_retries', 0))
     free_b, total_b = torch.cuda.mem_get_info()
-    res['memory_gb'] = {'torch_max_reserved': round(torch.cuda.max_memory_reserved() / 1e9, 1),
+    res['memory_gb'] = {'headline_max_reserved': round(mem_head.get('reserved_bytes.all.peak', 0) / 1e9, 1),
+                        'headline_max_allocated': round(mem_head.get('allocated_bytes.all.peak', 0) / 1e9, 1),
+                        'torch_max_reserved': round(torch.cuda.max_memory_reserved() / 1e9, 1),
                         'torch_max_allocated': round(torch.cuda.max_memory_allocated() / 1e9, 1),
                         'device_free_at_end': round(free_b / 1e9, 1),
                         'device_total': round(total_b / 1e9, 1)}

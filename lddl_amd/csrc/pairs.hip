@@ -97,9 +97,11 @@ __global__ void scatter_docs_kernel(const int64_t* doc_sent_off, int64_t n_doc, 
 }
 
 __global__ void part_offsets_kernel(const int64_t* part_doc_off, int64_t n_part, const int64_t* kd_pos,
-                                    int64_t* kp_off) {
+                                    int64_t* kp_off, unsigned long long* max_docs) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p <= n_part) kp_off[p] = kd_pos[part_doc_off[p]];
+  if (p < n_part)  // kept documents of the largest partition (the planner's LDS table choice)
+    atomicMax(max_docs, (unsigned long long)(kd_pos[part_doc_off[p + 1]] - kd_pos[part_doc_off[p]]));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -145,28 +147,24 @@ struct WaveRng {
     return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
   }
 
-  // regenerate the block with all 64 lanes (three dependency-free phases), then the look-ahead
+  // Regenerate the block in place with all 64 lanes: ten straight-line rounds of 64 consecutive
+  // words (no exec-mask loops), then the look-ahead. Word i reads old[i], old[i+1] and old[i+397]
+  // (i < 227) or new[i-227], written three rounds earlier; a round reads before it writes, and
+  // one wave's LDS operations complete in order, so the rounds need only a compiler fence. Word
+  // 623 reads "old[624]" = the look-ahead word 0 = new[0] (seed_i64 sets it for the first block);
+  // round 9's lanes past 623 write scratch into the look-ahead, which the last round overwrites.
   __device__ void twist() {
     const int l = threadIdx.x;
-    for (int i = l; i < kN - kM; i += 64) {  // [0,227): old[i], old[i+1], old[i+397]
-      const uint32_t v = twist1(mt[i], mt[i + 1], mt[i + kM]);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      const int i = 64 * r + l;
+      const int ci = r < 3 ? i + kM : r > 3 ? i - (kN - kM) : (l < kN - kM - 192 ? i + kM : i - (kN - kM));
+      const uint32_t v = twist1(mt[i], mt[i + 1], mt[ci]);
       mt[i] = v;
+      __asm__ volatile("" ::: "memory");
     }
-    __syncthreads();
-    for (int i = kN - kM + l; i < 2 * (kN - kM); i += 64) {  // [227,454): new[i-227]
-      const uint32_t v = twist1(mt[i], mt[i + 1], mt[i - (kN - kM)]);
-      mt[i] = v;
-    }
-    __syncthreads();
-    for (int i = 2 * (kN - kM) + l; i < kN - 1; i += 64) {  // [454,623): new[i-227]
-      const uint32_t v = twist1(mt[i], mt[i + 1], mt[i - (kN - kM)]);
-      mt[i] = v;
-    }
-    __syncthreads();
-    if (l == 0) mt[kN - 1] = twist1(mt[kN - 1], mt[0], mt[kM - 1]);
-    __syncthreads();
-    if (l < kLook) mt[kN + l] = twist1(mt[l], mt[l + 1], mt[l + kM]);
-    __syncthreads();
+    mt[kN + l] = twist1(mt[l], mt[l + 1], mt[l + kM]);  // look-ahead: next block's words 0..63
+    __asm__ volatile("" ::: "memory");
     mti -= kN;
     wbase = -1024;
     wend = 0;
@@ -205,6 +203,7 @@ struct WaveRng {
         if (i >= kN) { mt[0] = mt[kN - 1]; prev = mt[0]; i = 1; }
       }
       mt[0] = 0x80000000u;
+      mt[kN] = twist1(mt[0], mt[1], mt[kM]);  // look-ahead word 0 (= the first twist's new[0])
     }
     __syncthreads();
     mti = kN;  // CPython leaves index = N after seeding: the first draw twists
@@ -583,6 +582,9 @@ __device__ inline void densify_group(int64_t k0, const int64_t* __restrict__ ks_
 #ifndef LDDL_PLAN_MINW
 #define LDDL_PLAN_MINW 6
 #endif
+// kDocsLds: every partition's document offsets fit the LDS table (host-checked: <= kDocLds
+// documents), so the document lookups carry no global-memory branch; kJB: bytes per shuffle draw
+template <bool kDocsLds, int kJB>
 __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* s_mt = reinterpret_cast<uint32_t*>(smem);
@@ -615,12 +617,12 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
   const int64_t d0 = A.kp_off[p];
   const int32_t nd = (int32_t)(A.kp_off[p + 1] - d0);  // (partition-local indices are 32-bit)
   const int64_t kbase = A.kd_off[d0];
-  const bool doc_lds = nd + 1 <= kDocLds;
-  if (doc_lds)
+  if (kDocsLds)
     for (int64_t d = lane; d <= nd; d += 64) s_doc[d] = (int32_t)(A.kd_off[d0 + d] - kbase);
   __syncthreads();
   auto doc_loc = [&](int32_t d) -> int32_t {  // first kept sentence of document d, partition-local
-    return doc_lds ? uni(s_doc[d]) : (int32_t)(A.kd_off[d0 + d] - kbase);
+    if constexpr (kDocsLds) return uni(s_doc[d]);
+    else return uni((int32_t)(A.kd_off[d0 + d] - kbase));
   };
   const int32_t* ks_len_p = A.ks_len + kbase;
   const int64_t base = (int64_t)A.dup * kbase;
@@ -750,7 +752,7 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
           const bool fits = pool_end <= A.pool_cap && jpool_end <= A.jpool_cap;
           if (!fits && leader) *A.overflow = 1;
           // random.shuffle(cand_indexes): draws j_i (i = nc-1 .. 1) to the pool
-          if (A.jbytes == 1) {
+          if constexpr (kJB == 1) {
             uint8_t* jd = static_cast<uint8_t*>(A.jpool) + jb;
             rng.fy_draws(nc, [&](int64_t i, uint32_t j) {
               if (fits) jd[i] = (uint8_t)j;
@@ -1779,15 +1781,20 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
                        st, d_sent_off, d_sent_len, n_sent, ks_pos, P->ks_start, P->ks_len);
   hipLaunchKernelGGL(scatter_docs_kernel, dim3((unsigned)((n_doc + 256) / 256)), dim3(256), 0, st,
                      d_doc_sent_off, n_doc, ks_pos, kd_pos, P->kd_off);
+  unsigned long long* d_max_docs;
+  TRY(P->alloc(&d_max_docs, 1, st));
+  LDDL_HIP(hipMemsetAsync(d_max_docs, 0, 8, st));
   hipLaunchKernelGGL(part_offsets_kernel, dim3((unsigned)((n_part + 256) / 256)), dim3(256), 0, st,
-                     d_part_doc_off, n_part, kd_pos, P->kp_off);
+                     d_part_doc_off, n_part, kd_pos, P->kp_off, d_max_docs);
   LDDL_HIP(hipGetLastError());
   // dense kept tokens
   TRY(P->alloc(&P->kscan, P->n_kept_sent + 1, st));
   if (scan_exclusive(KeptLen{P->ks_len}, P->n_kept_sent, P->kscan, scratch, st) != hipSuccess)
     TRY(-100);
   int64_t n_kept_tok = 0;
+  unsigned long long max_docs = 0;
   LDDL_HIP(hipMemcpyAsync(&n_kept_tok, P->kscan + P->n_kept_sent, 8, hipMemcpyDeviceToHost, st));
+  LDDL_HIP(hipMemcpyAsync(&max_docs, d_max_docs, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
   // 4 tokens of padding on both sides: the gather's 16-byte loads may overhang a window
   TRY(P->alloc(&P->dense, n_kept_tok + 8, st));
@@ -1915,9 +1922,18 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     A.pool_used = pool_ctl;
     A.overflow = reinterpret_cast<int32_t*>(pool_ctl + 1);
     LDDL_HIP(hipEventRecord(P->ev[0], st));
-    hipLaunchKernelGGL(plan_replay_kernel,
-                       dim3((unsigned)n_part + (A.n_kept_sent ? (unsigned)A.n_dense_wg : 0u)), dim3(64),
-                       lds, st, A);
+    {
+      const dim3 grid((unsigned)n_part + (A.n_kept_sent ? (unsigned)A.n_dense_wg : 0u));
+      const bool docs_lds = max_docs + 1 <= (unsigned long long)kDocLds;
+      if (docs_lds && jbytes == 1)
+        hipLaunchKernelGGL((plan_replay_kernel<true, 1>), grid, dim3(64), lds, st, A);
+      else if (docs_lds)
+        hipLaunchKernelGGL((plan_replay_kernel<true, 2>), grid, dim3(64), lds, st, A);
+      else if (jbytes == 1)
+        hipLaunchKernelGGL((plan_replay_kernel<false, 1>), grid, dim3(64), lds, st, A);
+      else
+        hipLaunchKernelGGL((plan_replay_kernel<false, 2>), grid, dim3(64), lds, st, A);
+    }
     LDDL_HIP(hipGetLastError());
     LDDL_HIP(hipEventRecord(P->ev[1], st));
     if (!prm->masking) break;
