@@ -225,7 +225,10 @@ struct WaveRng {
     return v;
   }
   // Fisher-Yates draws of random.shuffle over n items: j_i = _randbelow(i+1), i = n-1 .. 1,
-  // delivered as sink(i, j_i). Wave-parallel over a window of 64 words (lane t holds word t).
+  // delivered as sink(off, j) by every lane of every window: off = i for the lane whose word
+  // is drawn for step i and accepted, 0 for every other lane (rejected words, words past the
+  // end; index 0 of a draw array is never read, so the sink stores unconditionally - no
+  // exec-mask branch per window). Wave-parallel over a window of 64 words (lane t holds word t).
   // Word t of the window is drawn for step i_t = s0 - t + R_t (R_t = rejections before t) and
   // rejected iff (w_t >> (32 - bit_length(i_t + 1))) > i_t, i.e. with u = i + 1 (the draw's
   // bound) iff (w_t >> clz(u)) >= u. R is the fixed point of R_t = #{v < t : rejected under
@@ -233,9 +236,7 @@ struct WaveRng {
   // least the first wrong word. Words past the last step (u <= 1) come after every valid word
   // and do not affect their R; they are held "accepted" (a verdict that followed their R would
   // keep changing and cost passes: 11.7 instead of ~5 per window), and the first of them ends
-  // the shuffle. The window's bookkeeping is vector work on wave-uniform values plus two
-  // scalar branches per pass, so the scalar unit (the binding pipe of this kernel) carries
-  // little of it.
+  // the shuffle. The window's bookkeeping is branch-free scalar work (s_ff1 / s_bcnt1).
   template <typename Sink>
   __device__ void fy_draws(int32_t n, Sink sink) {
     const int lane = threadIdx.x;
@@ -247,9 +248,9 @@ struct WaveRng {
       int32_t R = 0;
       uint32_t x;
       uint64_t rej;
-      if (s0 >= 64) {  // every word of the window has a step
+      if (s0 >= 64) {  // every word of the window has a step (u >= 2)
         while (true) {
-          const int32_t u = u1 + R;  // >= 2
+          const int32_t u = u1 + R;
           x = w >> __clz((uint32_t)u);
           rej = ballot(x >= (uint32_t)u);
           const int32_t R2 = (int32_t)popc_below(rej);
@@ -263,7 +264,7 @@ struct WaveRng {
         while (true) {
           const int32_t u = u1 + R;
           x = w >> (__clz((uint32_t)u) & 31);
-          rej = ballot(u > 1 && x >= (uint32_t)u);
+          rej = ballot(x >= (uint32_t)u) & ballot(u > 1);
           const int32_t R2 = (int32_t)popc_below(rej);
 #ifdef LDDL_STAMPS
           ++n_pass;
@@ -275,19 +276,14 @@ struct WaveRng {
 #ifdef LDDL_STAMPS
       ++n_win;
 #endif
-      const int32_t i = u1 + R - 1;
+      const int32_t i = u1 + R - 1;  // the lane's step (<= 0 past the end)
+      // (the verdict is recomputed here rather than carried out of the loop as a lane mask)
+      sink(x > (uint32_t)i ? 0 : max(i, 0), x);
+      // the shuffle ends at the first word past the last step (E); words < E are consumed. After
+      // such a window s0 - (64 - popc(rej)) <= 0, since the held words count as accepted.
       const uint64_t fin = ballot(i < 1);
-      const bool acc = !((rej >> lane) & 1ull);
-      if (fin == 0) {  // every word of the window drawn for a step
-        if (acc) sink(i, x);
-        s0 -= 64 - __popcll(rej);
-        mti += 64;
-      } else {  // the shuffle ends in this window, at word E
-        const int E = __ffsll((unsigned long long)fin) - 1;
-        if (acc && lane < E) sink(i, x);
-        mti += E;
-        s0 = 0;
-      }
+      mti = uni(mti + (fin ? (int)__ffsll((unsigned long long)fin) - 1 : 64));
+      s0 -= 64 - (int32_t)__popcll(rej);
     }
     wbase = -1024;
     wend = 0;  // the register window is stale
@@ -732,8 +728,7 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
             const int64_t sz = num > kPoolChunk ? (num + 7) & ~7 : kPoolChunk;
             int64_t nb0 = 0;
             if (leader) nb0 = (int64_t)atomicAdd(&A.pool_used[0], (unsigned long long)sz);
-            nb0 = ((int64_t)__shfl((int)(nb0 >> 32), 0, 64) << 32) |
-                  (uint32_t)__shfl((int)(uint32_t)nb0, 0, 64);
+            nb0 = ((int64_t)uni((int)(nb0 >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)nb0);  // lane 0's
             pool_cur = nb0;
             pool_end = nb0 + sz;
           }
@@ -741,8 +736,7 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
             const int64_t sz = nc > kPoolChunk ? (nc + 7) & ~7 : kPoolChunk;
             int64_t nb0 = 0;
             if (leader) nb0 = (int64_t)atomicAdd(&A.pool_used[2], (unsigned long long)sz);
-            nb0 = ((int64_t)__shfl((int)(nb0 >> 32), 0, 64) << 32) |
-                  (uint32_t)__shfl((int)(uint32_t)nb0, 0, 64);
+            nb0 = ((int64_t)uni((int)(nb0 >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)nb0);  // lane 0's
             jpool_cur = nb0;
             jpool_end = nb0 + sz;
           }
@@ -754,12 +748,12 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
           // random.shuffle(cand_indexes): draws j_i (i = nc-1 .. 1) to the pool
           if constexpr (kJB == 1) {
             uint8_t* jd = static_cast<uint8_t*>(A.jpool) + jb;
-            rng.fy_draws(nc, [&](int64_t i, uint32_t j) {
-              if (fits) jd[i] = (uint8_t)j;
+            rng.fy_draws(nc, [&](int32_t i, uint32_t j) {
+              if (fits) jd[i] = (uint8_t)j;  // (fits is uniform: a scalar branch)
             });
           } else {
             uint16_t* jd = static_cast<uint16_t*>(A.jpool) + jb;
-            rng.fy_draws(nc, [&](int64_t i, uint32_t j) {
+            rng.fy_draws(nc, [&](int32_t i, uint32_t j) {
               if (fits) jd[i] = (uint16_t)j;
             });
           }
@@ -788,7 +782,7 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
   STAMP_ADD(0, st_t);
   {
     int32_t* js = A.jseq + base;
-    rng.fy_draws(np, [&](int64_t i, uint32_t j) { js[i] = (int32_t)j; });
+    rng.fy_draws(np, [&](int32_t i, uint32_t j) { js[i] = (int32_t)j; });  // (js[0] is never read)
   }
   STAMP_ADD(6, st_t);
 #ifdef LDDL_STAMPS
