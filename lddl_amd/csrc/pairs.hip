@@ -44,6 +44,15 @@ struct alignas(16) PairDesc {
   int32_t nb_rn;    // tokens kept in B | is_random_next << 31
 };
 
+// Replay masking, per planner slot: where the pair's decisions (mask pool, entries moff8 * 8 ..)
+// and shuffle draws (draw pool, joff16 * 16 ..) are, and how many. One 16-byte record, one store.
+struct alignas(16) SlotPool {
+  uint32_t moff8;   // mask-pool offset / 8 (regions are 8-entry aligned)
+  uint32_t joff16;  // draw-pool offset / 16 (regions are 16-entry aligned)
+  int32_t nmask;    // num_to_predict
+  int32_t ncand;    // candidates (len(A) + len(B) minus literal [CLS]/[SEP])
+};
+
 constexpr int32_t kKeep = -1;  // mask decision "keep the original token" (pretrain.py:215-216)
 
 // Diagnostic build only (-DLDDL_STAMPS): per-region s_memtime sums of the planner.
@@ -338,8 +347,10 @@ struct WaveRng {
       const uint32_t w1 = (uint32_t)wave_next((int)w0), w2 = (uint32_t)wave_next((int)w1),
                      w3 = (uint32_t)wave_next((int)w2), w4 = (uint32_t)wave_next((int)w3);
       (void)w3;
-      const uint64_t N = ((uint64_t)(w0 >> 5) << 26) | (w1 >> 6);
-      const bool is_mask = lane + 2 <= kLook && N < lt08;
+      // random() < 0.8 <=> N = (w0 >> 5) * 2^26 + (w1 >> 6) < lt08 <=> (w0 >> 5) * 2^32 + w1 <
+      // lt08 * 64 (w1's low 6 bits cannot carry past a multiple of 64): one shift, one compare
+      const uint64_t N64 = ((uint64_t)(w0 >> 5) << 32) | w1;
+      const bool is_mask = lane + 2 <= kLook && N64 < (lt08 << 6);
       const bool v3 = lane + 4 <= kLook;
       const bool is_keep = !is_mask && v3 && w2 < 0x80000000u;
       const bool is_rand = v3 && !is_mask && !is_keep;
@@ -451,13 +462,10 @@ struct PlanArgs {
   // outputs, slot base of partition p = dup * kd_off[kp_off[p]]
   PairDesc* desc;
   int32_t* jseq;       // per slot: j_i draws of the final partition shuffle
-  int32_t* nmask;      // per slot
-  int32_t* mtok;       // mask pool: slot s's decisions at moff[s] .. + nmask[s] (shuffled order)
-  int64_t* moff;       // per slot
-  void* jpool;         // draw pool: j_i of random.shuffle(cand_indexes) at joff[s] + i
+  SlotPool* spool;     // per slot (masking)
+  int32_t* mtok;       // mask pool: slot s's decisions at 8 * moff8 .. + nmask (shuffled order)
+  void* jpool;         // draw pool: j_i of random.shuffle(cand_indexes) at 16 * joff16 + i
   int32_t jbytes;      // 1 (target_seq_length <= 256: every j_i < 256) or 2 bytes per draw
-  int64_t* joff;       // per slot
-  int32_t* ncand;      // per slot: candidates (len(A) + len(B) minus literal [CLS]/[SEP])
   unsigned long long* pool_used;  // [0] masks, [1] overflow flag, [2] draws
   int64_t pool_cap, jpool_cap;
   int32_t* overflow;   // set when the pool is too small (the host re-plans with a larger one)
@@ -623,8 +631,11 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
   const int32_t* ks_len_p = A.ks_len + kbase;
   const int64_t base = (int64_t)A.dup * kbase;
   const int32_t max_num = A.seq - 3;
-  int64_t pool_cur = 0, pool_end = 0;    // this wave's current chunk of the mask pool
-  int64_t jpool_cur = 0, jpool_end = 0;  // ... and of the shuffle-draw pool
+  // this wave's current chunks of the mask pool and of the shuffle-draw pool: next entry, entries
+  // left (32-bit compares), and whether the chunk lies inside the pool
+  int64_t pool_cur = 0, jpool_cur = 0;
+  int32_t pool_left = 0, jpool_left = 0;
+  bool pool_fits = true, jpool_fits = true;
   LenWin La, Lb;
   int64_t np = 0;
 #ifndef LDDL_PLAN_PRIO
@@ -724,27 +735,33 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
           if (num > nc) num = nc;
           // pool space for this pair's shuffle draws (nc) and masks (num): bump allocation in
           // per-wave chunks (one atomic per kPoolChunk entries); each slot records its offsets
-          if (pool_cur + num > pool_end) {
-            const int64_t sz = num > kPoolChunk ? (num + 7) & ~7 : kPoolChunk;
+          if (num > pool_left) {
+            const int32_t sz = num > kPoolChunk ? (num + 7) & ~7 : (int32_t)kPoolChunk;
             int64_t nb0 = 0;
             if (leader) nb0 = (int64_t)atomicAdd(&A.pool_used[0], (unsigned long long)sz);
             nb0 = ((int64_t)uni((int)(nb0 >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)nb0);  // lane 0's
             pool_cur = nb0;
-            pool_end = nb0 + sz;
+            pool_left = sz;
+            pool_fits = nb0 + sz <= A.pool_cap;
           }
-          if (jpool_cur + nc > jpool_end) {
-            const int64_t sz = nc > kPoolChunk ? (nc + 7) & ~7 : kPoolChunk;
+          if (nc > jpool_left) {
+            const int32_t sz = nc > kPoolChunk ? (nc + 15) & ~15 : (int32_t)kPoolChunk;
             int64_t nb0 = 0;
             if (leader) nb0 = (int64_t)atomicAdd(&A.pool_used[2], (unsigned long long)sz);
-            nb0 = ((int64_t)uni((int)(nb0 >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)nb0);  // lane 0's
+            nb0 = ((int64_t)uni((int)(nb0 >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)nb0);
             jpool_cur = nb0;
-            jpool_end = nb0 + sz;
+            jpool_left = sz;
+            jpool_fits = nb0 + sz <= A.jpool_cap;
           }
           const int64_t mb = pool_cur, jb = jpool_cur;
-          pool_cur += (num + 7) & ~7;  // 16-byte aligned regions (fy_resolve_kernel's uint4 I/O)
-          jpool_cur += (nc + 15) & ~15;  // 16-byte aligned for 1-byte draws too
-          const bool fits = pool_end <= A.pool_cap && jpool_end <= A.jpool_cap;
-          if (!fits && leader) *A.overflow = 1;
+          // 16-byte aligned regions (fy_resolve_kernel's uint4 I/O; 1-byte draws too); chunk sizes
+          // are multiples of the steps, so num <= left implies step <= left
+          pool_cur += (num + 7) & ~7;
+          pool_left -= (num + 7) & ~7;
+          jpool_cur += (nc + 15) & ~15;
+          jpool_left -= (nc + 15) & ~15;
+          const bool fits = pool_fits && jpool_fits;
+          if (!fits) *A.overflow = 1;  // (uniform; every lane stores the same flag)
           // random.shuffle(cand_indexes): draws j_i (i = nc-1 .. 1) to the pool
           if constexpr (kJB == 1) {
             uint8_t* jd = static_cast<uint8_t*>(A.jpool) + jb;
@@ -765,12 +782,8 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
             if (fits && lane < cmax) A.mtok[mb + c0 + lane] = mytok;
           }
           STAMP_ADD(4, st_t);
-          {  // (all lanes, as the descriptor above)
-            A.nmask[slot] = num;
-            A.moff[slot] = mb;
-            A.joff[slot] = jb;
-            A.ncand[slot] = nc;
-          }
+          // (all lanes, as the descriptor above)
+          A.spool[slot] = SlotPool{(uint32_t)(mb >> 3), (uint32_t)(jb >> 4), num, nc};
         }
         ++np;
         chunk0 = next0;
@@ -1206,6 +1219,7 @@ __global__ void __launch_bounds__(256) pair_prep_kernel(const int64_t* __restric
                                                         const int64_t* __restrict__ kscan,
                                                         const int32_t* __restrict__ nmask,
                                                         const int64_t* __restrict__ moff,
+                                                        const SlotPool* __restrict__ spool,
                                                         GatherRec* __restrict__ rec,
                                                         int2* __restrict__ cnt) {
   const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1215,10 +1229,13 @@ __global__ void __launch_bounds__(256) pair_prep_kernel(const int64_t* __restric
   GatherRec r;
   r.aoff = kscan[d.a_ks] + d.a_front;
   r.boff = kscan[d.b_ks] + d.b_front;
-  r.moff = nmask ? moff[slot] : 0;
+  // masks: the replay planner's per-slot record, or the native path's arrays (none: no masking)
+  SlotPool sp{0u, 0u, 0, 0};
+  if (spool) sp = spool[slot];
+  r.moff = spool ? (int64_t)sp.moff8 << 3 : nmask ? moff[slot] : 0;
   r.na = d.na;
   r.nb_rn = d.nb_rn;
-  r.nm = nmask ? nmask[slot] : 0;
+  r.nm = spool ? sp.nmask : nmask ? nmask[slot] : 0;
   r.pad = 0;
   rec[q] = r;
   cnt[q] = make_int2(r.na + (r.nb_rn & 0x7FFFFFFF), r.nm);  // compact input of the two scans
@@ -1290,10 +1307,7 @@ struct ResolveArgs {
   const int64_t* src;  // slots in planner order (each pair once; mpos is addressed by moff)
   int64_t n_pairs;
   const PairDesc* desc;
-  const int32_t* nmask;
-  const int32_t* ncand;
-  const int64_t* moff;
-  const int64_t* joff;
+  const SlotPool* spool;
   const void* jpool;   // 1- or 2-byte draws (the kernel's D)
   uint16_t* mpos;
   const int64_t* kscan;
@@ -1342,10 +1356,11 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   const int64_t q = (int64_t)blockIdx.x * 64 + lane;
   if (q >= R.n_pairs) return;
   const int64_t slot = R.src[q];
-  const int32_t num = R.nmask[slot];
+  const SlotPool sp = R.spool[slot];
+  const int32_t num = sp.nmask;
   if (num <= 0) return;
-  const int32_t nc = R.ncand[slot];
-  const int64_t jb = R.joff[slot], mb = R.moff[slot];  // multiples of 16 / 8 (planner)
+  const int32_t nc = sp.ncand;
+  const int64_t jb = (int64_t)sp.joff16 << 4, mb = (int64_t)sp.moff8 << 3;
   const PairDesc d = R.desc[slot];
   const int32_t na = d.na, nb = d.nb_rn & 0x7FFFFFFF;
   const bool fast = nc == na + nb;
@@ -1809,6 +1824,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
 
   }
   P->max_pred = max_pred;
+  SlotPool* spool_out = nullptr;  // replay masking: per-slot pool record (pair_prep reads it)
   if (prm->rng == LDDL_RNG_NATIVE) {
     TRY(plan_native(P, c, prm, d_part_seed, n_part, st));
   } else {
@@ -1817,14 +1833,9 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   TRY(P->alloc(&P->order, slots, st));
   TRY(P->alloc(&jseq, slots, st));
   TRY(P->alloc(&part_npairs, n_part + 1, st));
-  int64_t* joff = nullptr;
-  int32_t* ncand = nullptr;
-  if (prm->masking) {
-    TRY(P->alloc(&P->nmask, slots, st));
-    TRY(P->alloc(&P->moff, slots, st));
-    TRY(P->alloc(&joff, slots, st));
-    TRY(P->alloc(&ncand, slots, st));
-  }
+  SlotPool* spool = nullptr;
+  if (prm->masking) TRY(P->alloc(&spool, slots, st));
+  spool_out = spool;
   PlanArgs A{};
   A.kscan = P->kscan;
   A.ks_len = P->ks_len;
@@ -1863,8 +1874,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   }
   A.desc = P->desc;
   A.jseq = jseq;
-  A.nmask = P->nmask;
-  A.moff = P->moff;
+  A.spool = spool;
   A.part_npairs = part_npairs;
 #ifdef LDDL_STAMPS
   uint64_t* d_stamps;
@@ -1878,8 +1888,6 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
 #endif
   if (prm->seq > 512) TRY((set_error("replay planner supports target_seq_length <= 512"), -1));
   const size_t lds = 4 * (kN + kLook) + 4 * (kDocLds + 4) + 16;  // ~4.8 KB: 7 waves/SIMD fit
-  A.joff = joff;
-  A.ncand = ncand;
   // pools: decisions (int32, shuffled order) and shuffle draws (uint16), sized from the kept
   // tokens (expected use ~0.15 * 1.5 and ~1.5 times dup * tokens); a plan that outgrows them
   // reports the exact sizes and is planned again (deterministic replay)
@@ -1901,6 +1909,9 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
            kPoolChunk * (n_part + 16);  // + the 16-entry alignment of every pair's draws
     if (const char* e = getenv("LDDL_AMD_MASK_POOL")) cap = atoll(e);  // tests: force a re-plan
   }
+  // SlotPool keeps pool offsets as 32-bit multiples of 8 / 16 entries
+  if (cap / 8 >= (int64_t)UINT32_MAX || jcap / 16 >= (int64_t)UINT32_MAX)
+    TRY((set_error("batch too large for the mask pools (split it into smaller GPU batches)"), -1));
   for (int attempt = 0; n_part; ++attempt) {
     int32_t* mtok = nullptr;
     if (prm->masking) {
@@ -2039,8 +2050,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     hipLaunchKernelGGL(map_pairs_kernel, dim3((unsigned)n_part), dim3(256), 0, st, P->kd_off,
                        P->kp_off, prm->dup, part_base, P->order, P->src, slots);
   if (prm->masking && P->n_pairs) {
-    ResolveArgs RA{slots, P->n_pairs, P->desc, P->nmask, ncand, P->moff, joff, jpool,
-                   P->mpos, P->kscan, P->dense, cls, sep};
+    ResolveArgs RA{slots, P->n_pairs, P->desc, spool, jpool, P->mpos, P->kscan, P->dense, cls, sep};
     const dim3 grid((unsigned)((P->n_pairs + 63) / 64));
     if (prm->seq <= 131)  // nc <= 128: all draws in registers (8 uint4 of 1-byte draws)
       hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 8>), grid, dim3(64),
@@ -2062,7 +2072,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   if (npairs)
     hipLaunchKernelGGL(pair_prep_kernel, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, st,
                        P->src, npairs, P->desc, P->kscan, prm->masking ? P->nmask : nullptr,
-                       P->moff, P->rec, pcnt);
+                       P->moff, prm->masking && prm->rng != LDDL_RNG_NATIVE ? spool_out : nullptr,
+                       P->rec, pcnt);
   LDDL_HIP(hipGetLastError());
   int64_t* scr2;
   TRY(P->alloc(&scr2, scan_scratch_elems(npairs), st));
