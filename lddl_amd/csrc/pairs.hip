@@ -472,7 +472,6 @@ struct PlanArgs {
   int64_t* part_npairs;
   uint64_t* stamps;  // diagnostic build: [n_part][8]
   uint64_t* tl;      // diagnostic build: [n_part][2] s_memrealtime at start / end (100 MHz)
-  const int16_t* num_tab;  // [n] = max(1, round((n) * ratio)) (half-even, binary64), n <= seq
 };
 
 constexpr int kDocLds = 512;  // partitions with <= this many documents cache offsets in LDS
@@ -730,7 +729,9 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
             nc = uni(c);
           }
           STAMP_ADD(1, st_t);
-          int32_t num = A.num_tab[na + nb + 3];  // (host table, below)
+          // num_to_predict = round(len(tokens) * masked_lm_ratio) (pretrain.py:197): binary64
+          // product, round half to even - the IEEE operations Python performs
+          int32_t num = uni((int32_t)__builtin_rint((double)(na + nb + 3) * A.ratio));
           if (num < 1) num = 1;
           if (num > nc) num = nc;
           // pool space for this pair's shuffle draws (nc) and masks (num): bump allocation in
@@ -1860,18 +1861,6 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   A.ratio = prm->masked_lm_ratio;
   A.k_short = short_threshold(prm->short_seq_prob);
   A.seq_r64 = ((prm->seq + 63) / 64) * 64;
-  {  // num_to_predict for every pair length n <= seq: round(n * ratio) as CPython computes it
-    std::vector<int16_t> h(prm->seq + 4);
-    for (int n = 0; n < (int)h.size(); ++n) {
-      const double v = rint((double)n * prm->masked_lm_ratio);
-      h[n] = (int16_t)std::min<double>(v, 32767.0);
-    }
-    int16_t* d_tab;
-    TRY(P->alloc(&d_tab, (int64_t)h.size(), st));
-    LDDL_HIP(hipMemcpyAsync(d_tab, h.data(), 2 * h.size(), hipMemcpyHostToDevice, st));
-    LDDL_HIP(hipStreamSynchronize(st));  // (h is a host temporary)
-    A.num_tab = d_tab;
-  }
   A.desc = P->desc;
   A.jseq = jseq;
   A.spool = spool;
