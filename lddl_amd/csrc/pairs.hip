@@ -1189,6 +1189,8 @@ __global__ void __launch_bounds__(64) apply_shuffle_kernel(const int64_t* kd_off
 // src[q]: the planner slot of output pair q (partition shuffle applied); slots[q]: the q-th
 // slot in planner order (every partition's slots base .. base + np - 1), so the per-slot passes
 // read the slot-indexed arrays front to back instead of in shuffled order.
+// (either output may be null: the slots do not depend on the partition shuffle, so they are
+// written before it finishes)
 __global__ void map_pairs_kernel(const int64_t* kd_off, const int64_t* kp_off, int32_t dup,
                                  const int64_t* part_pair_base, const int32_t* order, int64_t* src,
                                  int64_t* slots) {
@@ -1196,9 +1198,17 @@ __global__ void map_pairs_kernel(const int64_t* kd_off, const int64_t* kp_off, i
   const int64_t base = (int64_t)dup * kd_off[kp_off[p]];
   const int64_t q0 = part_pair_base[p], n = part_pair_base[p + 1] - q0;
   for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
-    src[q0 + k] = base + order[base + k];
+    if (src) src[q0 + k] = base + order[base + k];
     if (slots) slots[q0 + k] = base + k;
   }
+}
+
+// the largest partition's pair count (the partition shuffle's LDS size)
+__global__ void max_pairs_kernel(const int64_t* np, int64_t n, unsigned long long* out) {
+  int64_t m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = np[i] > m ? np[i] : m;
+  if (m) atomicMax(out, (unsigned long long)m);
 }
 
 struct Identity {
@@ -1606,7 +1616,8 @@ struct lddl_pairs {
   int64_t *src = nullptr, *tok_off = nullptr, *pos_off = nullptr;
   GatherRec* rec = nullptr;  // per output pair (pair_prep_kernel)
   int64_t* part_base = nullptr;  // [n_part + 1] first output pair of each partition
-  hipEvent_t ev[2] = {nullptr, nullptr};  // around the last plan_replay_kernel launch
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // [0..1] around the last
+  // plan_replay_kernel launch; [2..3] fork / join of the side stream
 
   template <typename T>
   int alloc(T** p, int64_t n, hipStream_t st) {
@@ -1625,6 +1636,7 @@ struct lddl_pairs {
       }
   }
   void release(hipStream_t st) {
+    if (ev[3]) (void)hipStreamWaitEvent(st, ev[3], 0);  // side-stream work has finished
     for (DevArena::Block& b : allocs) arena->give(b, st);
     allocs.clear();
     for (hipEvent_t& e : ev)
@@ -1880,8 +1892,11 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   // pools: decisions (int32, shuffled order) and shuffle draws (uint16), sized from the kept
   // tokens (expected use ~0.15 * 1.5 and ~1.5 times dup * tokens); a plan that outgrows them
   // reports the exact sizes and is planned again (deterministic replay)
-  unsigned long long* pool_ctl;  // [0] masks used, [1] overflow flag, [2] draws used
-  TRY(P->alloc(&pool_ctl, 3, st));
+  unsigned long long* pool_ctl;  // [0] masks used, [1] overflow flag, [2] draws used, [3] max pairs
+  TRY(P->alloc(&pool_ctl, 4, st));
+  TRY(P->alloc(&part_base, n_part + 1, st));
+  P->part_base = part_base;
+  int64_t max_np = 1;
   int64_t cap = 0, jcap = 0;
   void* jpool = nullptr;
   const int jbytes = prm->seq <= 256 ? 1 : 2;  // every draw j_i < nc <= seq - 3
@@ -1904,7 +1919,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   for (int attempt = 0; n_part; ++attempt) {
     int32_t* mtok = nullptr;
     if (prm->masking) {
-      LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 24, st));
+      LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 32, st));
       TRY(P->alloc(&mtok, cap + 4, st));
       TRY(P->alloc(reinterpret_cast<uint8_t**>(&jpool), jbytes * (jcap + 16), st));
     }
@@ -1930,10 +1945,17 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     }
     LDDL_HIP(hipGetLastError());
     LDDL_HIP(hipEventRecord(P->ev[1], st));
-    if (!prm->masking) break;
-    unsigned long long ctl[3];
-    LDDL_HIP(hipMemcpyAsync(ctl, pool_ctl, 24, hipMemcpyDeviceToHost, st));
+    // pairs per partition -> output offsets and the largest count, read back with the pool
+    // counters in the planner's one sync
+    if (!prm->masking) LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 32, st));
+    if (scan_exclusive(Identity{part_npairs}, n_part, part_base, scratch, st) != hipSuccess) TRY(-100);
+    hipLaunchKernelGGL(max_pairs_kernel, dim3(64), dim3(256), 0, st, part_npairs, n_part, pool_ctl + 3);
+    unsigned long long ctl[4];
+    LDDL_HIP(hipMemcpyAsync(ctl, pool_ctl, 32, hipMemcpyDeviceToHost, st));
+    LDDL_HIP(hipMemcpyAsync(&P->n_pairs, part_base + n_part, 8, hipMemcpyDeviceToHost, st));
     LDDL_HIP(hipStreamSynchronize(st));
+    max_np = std::max<int64_t>(1, (int64_t)ctl[3]);
+    if (!prm->masking) break;
     if (!ctl[1]) {
       P->mtok = mtok;
       TRY(P->alloc(&P->mpos, (int64_t)ctl[0], st));
@@ -1946,12 +1968,21 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     cap = (int64_t)ctl[0] + 1024;
     jcap = (int64_t)ctl[2] + 1024;
   }
+  // random.shuffle(partition_pairs): the swaps run on the context's side stream, beside the mask
+  // replay (fy_resolve_kernel needs only the planner-order slots); the main stream waits for them
+  // before the output order (src) is built
+  hipStream_t sst = nullptr;
+  hipEvent_t ev_plan = nullptr, ev_shuf = nullptr;
   if (n_part) {
-    std::vector<int64_t> h_np(n_part);
-    LDDL_HIP(hipMemcpyAsync(h_np.data(), part_npairs, 8 * n_part, hipMemcpyDeviceToHost, st));
-    LDDL_HIP(hipStreamSynchronize(st));
-    int64_t cap = 1;
-    for (int64_t v : h_np) cap = std::max(cap, v);
+    TRY(c->side_stream(&sst) == hipSuccess &&
+                hipEventCreateWithFlags(&P->ev[2], hipEventDisableTiming) == hipSuccess &&
+                hipEventCreateWithFlags(&P->ev[3], hipEventDisableTiming) == hipSuccess
+            ? 0 : (set_error("side stream"), -100));
+    ev_plan = P->ev[2];
+    ev_shuf = P->ev[3];
+    LDDL_HIP(hipEventRecord(ev_plan, st));
+    LDDL_HIP(hipStreamWaitEvent(sst, ev_plan, 0));
+    const int64_t cap = max_np;
     // dynamic-LDS budget of the swap kernel: what the device grants a block (160 KiB on
     // gfx950), minus headroom for the kernel's static LDS
     const size_t kLdsBudget = std::min<size_t>(150 * 1024, c->lds_per_block > 10 * 1024
@@ -1959,20 +1990,21 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     const bool force_global = getenv("LDDL_SHUFFLE_GLOBAL") != nullptr;  // tests: the large-partition path
     if (force_global)
       hipLaunchKernelGGL(apply_shuffle_kernel<int32_t>, dim3((unsigned)n_part), dim3(64),
-                         4 * (size_t)kShufStage, st, P->kd_off, P->kp_off, prm->dup, part_npairs,
+                         4 * (size_t)kShufStage, sst, P->kd_off, P->kp_off, prm->dup, part_npairs,
                          jseq, P->order, (int64_t)0);
     else if (cap <= 65536 && 2 * (size_t)(cap + kShufStage) <= kLdsBudget)
       hipLaunchKernelGGL(apply_shuffle_kernel<uint16_t>, dim3((unsigned)n_part), dim3(64),
-                         2 * (size_t)(cap + kShufStage), st, P->kd_off, P->kp_off, prm->dup,
+                         2 * (size_t)(cap + kShufStage), sst, P->kd_off, P->kp_off, prm->dup,
                          part_npairs, jseq, P->order, cap);
     else if (4 * (size_t)(cap + kShufStage) <= kLdsBudget)
       hipLaunchKernelGGL(apply_shuffle_kernel<int32_t>, dim3((unsigned)n_part), dim3(64),
-                         4 * (size_t)(cap + kShufStage), st, P->kd_off, P->kp_off, prm->dup,
+                         4 * (size_t)(cap + kShufStage), sst, P->kd_off, P->kp_off, prm->dup,
                          part_npairs, jseq, P->order, cap);
     else  // partitions too large for LDS: swaps in global memory
       hipLaunchKernelGGL(apply_shuffle_kernel<int32_t>, dim3((unsigned)n_part), dim3(64),
-                         4 * (size_t)kShufStage, st, P->kd_off, P->kp_off, prm->dup, part_npairs,
+                         4 * (size_t)kShufStage, sst, P->kd_off, P->kp_off, prm->dup, part_npairs,
                          jseq, P->order, (int64_t)0);
+    LDDL_HIP(hipEventRecord(ev_shuf, sst));
   }
   LDDL_HIP(hipGetLastError());
 #ifdef LDDL_STAMPS
@@ -2026,18 +2058,13 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     fprintf(stderr, "\n");
   }
 #endif
-  // layout
-  TRY(P->alloc(&part_base, n_part + 1, st));
-  P->part_base = part_base;
-  if (scan_exclusive(Identity{part_npairs}, n_part, part_base, scratch, st) != hipSuccess) TRY(-100);
-  LDDL_HIP(hipMemcpyAsync(&P->n_pairs, part_base + n_part, 8, hipMemcpyDeviceToHost, st));
-  LDDL_HIP(hipStreamSynchronize(st));
+  // layout (part_base and n_pairs came with the planner's sync)
   TRY(P->alloc(&P->src, P->n_pairs, st));
   int64_t* slots = nullptr;  // planner-order slots for the mask replay
   if (prm->masking) TRY(P->alloc(&slots, P->n_pairs, st));
-  if (n_part)
+  if (n_part && slots)
     hipLaunchKernelGGL(map_pairs_kernel, dim3((unsigned)n_part), dim3(256), 0, st, P->kd_off,
-                       P->kp_off, prm->dup, part_base, P->order, P->src, slots);
+                       P->kp_off, prm->dup, part_base, (const int32_t*)nullptr, (int64_t*)nullptr, slots);
   if (prm->masking && P->n_pairs) {
     ResolveArgs RA{slots, P->n_pairs, P->desc, spool, jpool, P->mpos, P->kscan, P->dense, cls, sep};
     const dim3 grid((unsigned)((P->n_pairs + 63) / 64));
@@ -2050,6 +2077,12 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     else
       hipLaunchKernelGGL((fy_resolve_kernel<uint16_t, uint16_t, 0>), grid, dim3(64),
                          (size_t)2 * 64 * (size_t)prm->seq, st, RA);
+    LDDL_HIP(hipGetLastError());
+  }
+  if (n_part) {  // the output order: after the partition shuffle on the side stream
+    LDDL_HIP(hipStreamWaitEvent(st, ev_shuf, 0));
+    hipLaunchKernelGGL(map_pairs_kernel, dim3((unsigned)n_part), dim3(256), 0, st, P->kd_off,
+                       P->kp_off, prm->dup, part_base, (const int32_t*)P->order, P->src, (int64_t*)nullptr);
     LDDL_HIP(hipGetLastError());
   }
   }  // replay
