@@ -344,15 +344,33 @@ def run_c5(args):
                     yield b
         it = batches()
         dev = torch.device('cuda', 0)
+        if args.c5_blas != 'default':  # ('cublas' selects rocBLAS on ROCm)
+            torch.backends.cuda.preferred_blas_library('cublas' if args.c5_blas == 'rocblas' else 'cublaslt')
         model = TinyBert(len(loaders[0]._ctx)).to(dev)
-        opt = torch.optim.SGD(model.parameters(), lr=1e-4)
+        params = list(model.parameters())
+
+        def sgd_step(lr=1e-4):
+            # plain SGD as one fused foreach update (torch.optim.SGD spent ~150 ms of host time
+            # per step here: profiles/r03c5_workers_train_step.txt)
+            with torch.no_grad():
+                torch._foreach_add_(params, [q.grad for q in params], alpha=-lr)
+            for q in params:
+                q.grad = None
+
+        phase_s = [0.0, 0.0, 0.0]  # host seconds in forward / backward / optimizer (no syncs)
 
         def train(b):
+            p0 = time.perf_counter()
             with torch.autocast('cuda', dtype=torch.bfloat16):
                 loss = model(b)
+            p1 = time.perf_counter()
             loss.backward()
-            opt.step()
-            opt.zero_grad(set_to_none=True)
+            p2 = time.perf_counter()
+            sgd_step()
+            p3 = time.perf_counter()
+            phase_s[0] += p1 - p0
+            phase_s[1] += p2 - p1
+            phase_s[2] += p3 - p2
             return loss
 
         def timed(k_steps, with_train):
@@ -388,8 +406,15 @@ def run_c5(args):
 
         for _ in range(args.warmup):
             train(next(it))
+        phase_s[:] = [0.0, 0.0, 0.0]
+        m0 = torch.cuda.memory_stats()
         dt, real, slots, st, tw, tn = timed(args.steps, True)
+        m1 = torch.cuda.memory_stats()
         train_gpu_ms = timed.gpu_ms
+        host_phases = {k: round(v / args.steps * 1e3, 3) for k, v in
+                       zip(('forward', 'backward', 'optimizer'), phase_s)}
+        dev_allocs = int(m1.get('num_device_alloc', 0) - m0.get('num_device_alloc', 0))
+        dev_frees = int(m1.get('num_device_free', 0) - m0.get('num_device_free', 0))
         ldt, lreal, lslots, lst, _, _ = timed(args.steps, False)
         kern_ms = [e[0].elapsed_time(e[1]) for e in lst['events']]
         # algorithmic bytes of the fused collate kernel per launch: the A/B strings read once +
@@ -420,6 +445,8 @@ def run_c5(args):
                 'loader_wait_ms_per_step': tn / args.steps * 1e3,
                 'train_step_host_ms': tw / args.steps * 1e3,
                 'train_step_gpu_ms': train_gpu_ms,
+                'train_step_host_ms_by_phase': host_phases,
+                'device_mallocs_frees_in_timed_steps': [dev_allocs, dev_frees],
                 'host_cpus_granted': granted_cores()[0],
                 'dataloader_processes': len(loaders) * args.c5_workers,
                 'note': 'each batch feeds a bf16 TinyBert training step (embeddings + LayerNorm + '
@@ -465,6 +492,8 @@ def main():
     ap.add_argument('--c5-corpus-bytes', type=int, default=96 << 20)
     ap.add_argument('--c5-bin-size', type=int, default=64,
                     help='C5 loader bins (64 -> 8 bins, the reference example local_example.sh)')
+    ap.add_argument('--c5-blas', choices=('default', 'rocblas', 'hipblaslt'), default='default',
+                    help='c5: GEMM library of the training step (torch preferred_blas_library)')
     ap.add_argument('--c5-workers', type=int, default=2,
                     help='DataLoader workers per bin (= shards per bin of the C5 dataset)')
     ap.add_argument('--chunks', type=int, default=1,

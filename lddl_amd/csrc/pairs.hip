@@ -254,7 +254,10 @@ struct WaveRng {
       ensure();
       const uint32_t w = temper(mt[mti + lane]);
       const int32_t u1 = s0 + 1 - lane;
-      int32_t R = 0;
+      // Jacobi start: ~0.3 rejections per word (any start converges to the same fixed point,
+      // the left-most wrong word being fixed by every pass; simulated: 5.3 -> 4.8 passes per
+      // window at target_seq_length 128)
+      int32_t R = (lane * 77) >> 8;
       uint32_t x;
       uint64_t rej;
       if (s0 >= 64) {  // every word of the window has a step (u >= 2)

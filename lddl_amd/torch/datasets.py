@@ -51,7 +51,10 @@ class ShuffleBuffer:
         remaining = to_yield
         for f in self._files:
             self._logger.to('worker').info('Reading {}'.format(f.path))
-            for b in pq.read_table(f.path).to_batches():
+            # one thread per reader: the loader runs one reader per DataLoader worker, and
+            # pyarrow's default pool (os.cpu_count() threads in every worker) oversubscribes
+            # the host's granted CPUs and throttles the training process
+            for b in pq.read_table(f.path, use_threads=False).to_batches():
                 for s in self._decode(b):
                     if remaining <= 0:
                         return
