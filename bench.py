@@ -332,8 +332,8 @@ def run_c5(args):
         prep_s = time.perf_counter() - t0
         dl = get_bert_pretrain_data_loader(
             path, local_rank=0, vocab_file=VOCAB_CASED,
-            data_loader_kwargs={'batch_size': 256, 'num_workers': args.c5_workers,
-                                'prefetch_factor': 4},
+            data_loader_kwargs=dict({'batch_size': 256, 'num_workers': args.c5_workers},
+                                    **({'prefetch_factor': 4} if args.c5_workers else {})),
             mlm_probability=0.15, base_seed=args.seed, log_level=logging.WARNING,
             sequence_length_alignment=8, ignore_index=-1)
         loaders = getattr(dl, '_dataloaders', [dl])
