@@ -273,7 +273,7 @@ def c5_dataset(args, root):
     sink = os.path.join(root, 'out')
     argv = ['--schedule', 'local', '--wikipedia', os.path.join(root, 'source'), '--sink', sink,
             '--target-seq-length', '512', '--bin-size', str(args.c5_bin_size), '--num-blocks', '64',
-            '--vocab-file', VOCAB_CASED, '--num-shards', str(args.c5_workers),
+            '--vocab-file', VOCAB_CASED, '--num-shards', str(max(1, args.c5_workers)),
             '--sample-ratio', '1.0']
     P.main(P.attach_args().parse_args(argv))
     return sink
