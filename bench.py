@@ -115,6 +115,15 @@ def granted_cores():
         aff, 'none' if quota is None else '{:g}'.format(quota), src, os.cpu_count())
 
 
+def cgroup_cpu_stat():
+    """cgroup v2 cpu.stat counters (usage_usec, nr_throttled, throttled_usec, ...) or {}."""
+    try:
+        with open('/sys/fs/cgroup/cpu.stat') as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f if ln.strip())}
+    except (OSError, ValueError):
+        return {}
+
+
 def cpu_baseline(corp, part, seeds, args):
     """The oracle (C restatement of the reference algorithm) on a bounded sample of the same
     workload, one single-threaded process per granted host core (the reference's
@@ -408,8 +417,12 @@ def run_c5(args):
             train(next(it))
         phase_s[:] = [0.0, 0.0, 0.0]
         m0 = torch.cuda.memory_stats()
+        c0 = cgroup_cpu_stat()
         dt, real, slots, st, tw, tn = timed(args.steps, True)
+        c1 = cgroup_cpu_stat()
         m1 = torch.cuda.memory_stats()
+        cg = {k: c1[k] - c0.get(k, 0) for k in ('usage_usec', 'nr_periods', 'nr_throttled',
+                                                  'throttled_usec') if k in c1}
         train_gpu_ms = timed.gpu_ms
         host_phases = {k: round(v / args.steps * 1e3, 3) for k, v in
                        zip(('forward', 'backward', 'optimizer'), phase_s)}
@@ -447,6 +460,7 @@ def run_c5(args):
                 'train_step_gpu_ms': train_gpu_ms,
                 'train_step_host_ms_by_phase': host_phases,
                 'device_mallocs_frees_in_timed_steps': [dev_allocs, dev_frees],
+                'cgroup_cpu_stat_delta': cg,  # CPU quota throttling of the container while timed
                 'host_cpus_granted': granted_cores()[0],
                 'dataloader_processes': len(loaders) * args.c5_workers,
                 'note': 'each batch feeds a bf16 TinyBert training step (embeddings + LayerNorm + '
