@@ -86,3 +86,35 @@ def test_partition_shuffle_global_path(ctx, docs_dev, monkeypatch):
     monkeypatch.setenv('LDDL_SHUFFLE_GLOBAL', '1')
     for name in ('s128_mask', PAIR_CASES[0]):
         test_pairs_golden_gpu(name, ctx, docs_dev)
+
+
+def test_pairs_large_partition_vs_oracle(ctx):
+    """A partition with more documents than the planner's LDS document table (> 511): the
+    planner instantiation that reads document offsets from global memory, next to a small
+    partition, checked token for token against the oracle (seq 128, static masking)."""
+    from lddl_amd import synth
+    from lddl_amd.pairs import make_pairs
+    from oracle import oracle as O
+    vocab = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         'lddl_amd', 'assets', 'vocab_synth_uncased_30522.txt')
+    corp = synth.generate(seed=77, n_bytes=3_500_000, nonascii_frac=0.02, threads=4)
+    n_doc = corp.n_doc
+    assert n_doc > 600, n_doc
+    part = np.asarray([0, n_doc - 40, n_doc], np.int64)  # 40 documents, then the rest
+    seeds = np.asarray([5, 6], np.int64)
+    so = torch.from_numpy(corp.sent_off).cuda()
+    ids, sl = ctx.tokenize(torch.from_numpy(corp.text).cuda(), so)
+    pb = make_pairs(ctx, so, ids, sl, torch.from_numpy(corp.doc_sent_off).cuda(),
+                    torch.from_numpy(part).cuda(), torch.from_numpy(seeds).cuda(), seq=128, dup=2,
+                    masking=True).to_host()
+    tok = O.Tokenizer(vocab)
+    e_ids, e_off = tok.tokenize(corp.text, corp.sent_off)
+    exp = {'tokens': [], 'num_tokens': [], 'len_a': [], 'pos': [], 'labels': []}
+    for p in range(2):
+        ds = corp.doc_sent_off[part[p]:part[p + 1] + 1]
+        out = O.partition_pairs(ds, e_off, e_ids, int(seeds[p]), 2, 128, True, tok.vocab_size,
+                                *(tok.token_id(t) for t in ('[CLS]', '[SEP]', '[MASK]')))
+        for k in exp:
+            exp[k].append(out[k])
+    for k in exp:
+        assert np.array_equal(pb[k], np.concatenate(exp[k])), k
