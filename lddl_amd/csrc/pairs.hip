@@ -315,7 +315,9 @@ struct WaveRng {
       ensure();
       const int32_t cnt = min(T - done, 32);
       const int32_t t = done + lane;
-      const bool front = lane < cnt && temper(mt[mti + 2 * lane]) < 0x80000000u;
+      // random() < 0.5 <=> the tempered first word's top bit is clear; tempering is linear over
+      // GF(2) and that bit is the parity of raw bits 31, 27, 24 and 16
+      const bool front = lane < cnt && !(__popc(mt[mti + 2 * lane] & 0x89010000u) & 1);
       const bool sa = t < d || (t >= ad && ((t - ad) & 1));
       a_front += __popcll(ballot(front && sa));
       b_front += __popcll(ballot(front && !sa));
