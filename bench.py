@@ -416,10 +416,21 @@ def run_c5(args):
         for _ in range(args.warmup):
             train(next(it))
         phase_s[:] = [0.0, 0.0, 0.0]
+        import gc
+        gc_t = {'s': 0.0, 'n': 0, 't0': 0.0}
+
+        def gc_cb(phase, info):  # time the main process spends in Python's garbage collector
+            if phase == 'start':
+                gc_t['t0'] = time.perf_counter()
+            else:
+                gc_t['s'] += time.perf_counter() - gc_t['t0']
+                gc_t['n'] += 1
+        gc.callbacks.append(gc_cb)
         m0 = torch.cuda.memory_stats()
         c0 = cgroup_cpu_stat()
         dt, real, slots, st, tw, tn = timed(args.steps, True)
         c1 = cgroup_cpu_stat()
+        gc.callbacks.remove(gc_cb)
         m1 = torch.cuda.memory_stats()
         cg = {k: c1[k] - c0.get(k, 0) for k in ('usage_usec', 'nr_periods', 'nr_throttled',
                                                   'throttled_usec') if k in c1}
@@ -461,6 +472,8 @@ def run_c5(args):
                 'train_step_host_ms_by_phase': host_phases,
                 'device_mallocs_frees_in_timed_steps': [dev_allocs, dev_frees],
                 'cgroup_cpu_stat_delta': cg,  # CPU quota throttling of the container while timed
+                'python_gc_ms_per_step': round(gc_t['s'] / args.steps * 1e3, 3),
+                'python_gc_collections': gc_t['n'],
                 'host_cpus_granted': granted_cores()[0],
                 'dataloader_processes': len(loaders) * args.c5_workers,
                 'note': 'each batch feeds a bf16 TinyBert training step (embeddings + LayerNorm + '
