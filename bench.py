@@ -115,6 +115,31 @@ def granted_cores():
         aff, 'none' if quota is None else '{:g}'.format(quota), src, os.cpu_count())
 
 
+def load_pmc(batch_sizes):
+    """Per-kernel counters per launch from the committed PMC passes (profiles/pmc_*.json, made by
+    tools/prof_counters.sh + tools/make_pmc_json.py) taken on one of `batch_sizes` (requested or
+    actual bytes); the last such file in name order wins. Returns (kernels, file name)."""
+    import glob
+    kernels, src = {}, None
+    for pmc in sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_*.json'))):
+        try:
+            with open(pmc) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if rec.get('batch_bytes') in batch_sizes:
+            kernels, src = rec.get('kernels', {}), os.path.basename(pmc)
+    return kernels, src
+
+
+def pmc_entry(kernels, kernel):
+    """A kernel's counters by name; template instantiations (`name<...>`) match their base name."""
+    for k, v in kernels.items():
+        if k == kernel or k.startswith(kernel + '<'):
+            return v
+    return {}
+
+
 def cgroup_cpu_stat():
     """cgroup v2 cpu.stat counters (usage_usec, nr_throttled, throttled_usec, ...) or {}."""
     try:
@@ -839,22 +864,10 @@ def main():
     stage_gbs = stage_bytes / (pair_ms * 1e-3) / 1e9
     # per-kernel counters per launch from the committed PMC passes (profiles/pmc_*.json, made by
     # tools/prof_counters.sh + tools/make_pmc_json.py) when taken on the same batch size
-    pmc_kernels, pmc_src = {}, None
-    import glob
-    for pmc in sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_*.json'))):
-        try:
-            with open(pmc) as f:
-                rec = json.load(f)
-        except (OSError, ValueError):
-            continue
-        if rec.get('batch_bytes') in (args.batch_bytes, int(n_bytes)):  # requested or actual size
-            pmc_kernels, pmc_src = rec.get('kernels', {}), os.path.basename(pmc)
+    pmc_kernels, pmc_src = load_pmc((args.batch_bytes, int(n_bytes)))
 
-    def pmc_of(kernel):  # by name; template instantiations (`name<...>`) match their base name
-        for k, v in pmc_kernels.items():
-            if k == kernel or k.startswith(kernel + '<'):
-                return v
-        return {}
+    def pmc_of(kernel):
+        return pmc_entry(pmc_kernels, kernel)
 
     def traffic(kernel):
         return pmc_of(kernel).get('hbm_bytes_per_launch')

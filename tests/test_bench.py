@@ -48,3 +48,14 @@ def test_granted_cores():
     cores, how = bench.granted_cores()
     assert 1 <= cores <= len(os.sched_getaffinity(0))
     assert 'sched_getaffinity' in how and 'os.cpu_count()' in how
+
+
+def test_pmc_json_matches_actual_batch_and_template_names():
+    """The committed PMC passes are found by the batch's actual byte count and the planner's
+    template instantiation is found by its base name (bench.py `traffic` / `issue_roofline`)."""
+    kernels, src = bench.load_pmc((10_000_000_000, 10_000_001_451))
+    assert src is not None and kernels
+    plan = bench.pmc_entry(kernels, 'plan_replay_kernel')
+    assert plan.get('SQ_INSTS_SALU') and plan.get('hbm_bytes_per_launch')
+    assert bench.pmc_entry(kernels, 'tokenize_batch_kernel').get('SQ_INSTS_VALU')
+    assert bench.pmc_entry(kernels, 'no_such_kernel') == {}
