@@ -393,7 +393,24 @@ def run_c5(args):
 
         phase_s = [0.0, 0.0, 0.0]  # host seconds in forward / backward / optimizer (no syncs)
 
+        pad_mult = 64
+
+        def padded(b):
+            # the step's input padded to a multiple of 64 positions (the loader's batches come in
+            # up to 64 lengths; every new length loads new GEMM code objects - 40-135 ms of
+            # hipModuleLoad each, profiles/r03h_c5_hip_api.txt - and 8 shapes are warmed up below)
+            L = b['input_ids'].size(1)
+            Lp = -(-L // pad_mult) * pad_mult
+            if Lp == L:
+                return b
+            out = dict(b)
+            for k_ in ('input_ids', 'token_type_ids', 'attention_mask'):
+                out[k_] = torch.nn.functional.pad(b[k_], (0, Lp - L), value=0)
+            out['labels'] = torch.nn.functional.pad(b['labels'], (0, Lp - L), value=-1)
+            return out
+
         def train(b):
+            b = padded(b)
             p0 = time.perf_counter()
             with torch.autocast('cuda', dtype=torch.bfloat16):
                 loss = model(b)
@@ -438,6 +455,13 @@ def run_c5(args):
                 x.stats = None
             return dt, int(real.item()), slots, st, tw, tn
 
+        for Lp in range(pad_mult, 512 + 1, pad_mult):  # every padded shape, before timing
+            z = torch.zeros(256, Lp, dtype=torch.long, device=dev)
+            lab = torch.full((256, Lp), -1, dtype=torch.long, device=dev)
+            lab[:, 1::7] = 5
+            for _ in range(2):
+                train({'input_ids': z, 'token_type_ids': z, 'attention_mask': z + 1, 'labels': lab,
+                       'next_sentence_labels': torch.zeros(256, dtype=torch.long, device=dev)})
         for _ in range(args.warmup):
             train(next(it))
         phase_s[:] = [0.0, 0.0, 0.0]
