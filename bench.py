@@ -911,7 +911,11 @@ def main():
                 'valu_instructions_per_launch': v, 'achieved': a, 'peak': valu_peak,
                 'unit': 'wave64 VALU instr/s', 'frac': a / valu_peak,
                 'salu_instructions_per_launch': sc, 'salu_achieved': sa, 'salu_peak': salu_peak,
-                'salu_frac': sa / salu_peak, 'source': pmc_src,
+                'salu_frac': sa / salu_peak,
+                # the model both hot kernels fit: scalar and vector issue barely
+                # overlap, a SALU instruction costs a SIMD 4 cycles and a VALU one 2
+                'issue_model_frac': (4.0 * (sc or 0) + 2.0 * v) / (256 * 4 * 2.4e9 * ms * 1e-3),
+                'source': pmc_src,
                 'note': 'PMC pass taken on an earlier build of the same batch size'}
 
     plan_roof = {'kernel': 'plan_replay_kernel' if args.rng == 'replay' else
