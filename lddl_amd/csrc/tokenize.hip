@@ -366,12 +366,37 @@ __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v,
 #endif
     if (id < 0 && len > 1) {
       uint32_t cand = bloom_candidates32(bloom, a, len - 1, cont) & (uint32_t)(e >> 1);
+#ifdef LDDL_TOK_SEQ_PROBES  // A/B: one candidate's table load at a time
       while (cand) {
         len = 32 - __clz(cand);
         id = probe32(T, a, len, cont);
         if (id >= 0) break;
         cand &= ~(1u << (len - 1));
       }
+#else
+      // the two longest remaining candidates' home slots are loaded together (the chain of
+      // dependent table loads per piece is what a lane waits on), the longer one decides first
+      while (cand) {
+        const int l1 = 32 - __clz(cand);
+        const uint32_t rest = cand & ~(1u << (l1 - 1));
+        const int l2 = rest ? 32 - __clz(rest) : 0;
+        const Probe q1 = probe_first(T, a, l1, cont);
+        const Probe q2 = probe_first(T, a, l2 ? l2 : l1, cont);
+        id = probe_finish(T, a, l1, q1);
+        if (id >= 0) {
+          len = l1;
+          break;
+        }
+        if (l2) {
+          id = probe_finish(T, a, l2, q2);
+          if (id >= 0) {
+            len = l2;
+            break;
+          }
+        }
+        cand = l2 ? rest & ~(1u << (l2 - 1)) : 0u;
+      }
+#endif
     }
     if (id < 0) {  // no piece: the whole word is [UNK]
       pc.put(0, T.special_id[kUnk]);
