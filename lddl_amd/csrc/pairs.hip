@@ -355,15 +355,18 @@ struct WaveRng {
       // random() < 0.8 <=> N = (w0 >> 5) * 2^26 + (w1 >> 6) < lt08 <=> (w0 >> 5) * 2^32 + w1 <
       // lt08 * 64 (w1's low 6 bits cannot carry past a multiple of 64): one shift, one compare
       const uint64_t N64 = ((uint64_t)(w0 >> 5) << 32) | w1;
-      const bool is_mask = lane + 2 <= kLook && N64 < (lt08 << 6);
-      const bool v3 = lane + 4 <= kLook;
-      const bool is_keep = !is_mask && v3 && w2 < 0x80000000u;
-      const bool is_rand = v3 && !is_mask && !is_keep;
+      // the decision at word t: [MASK] (2 words), else keep (random() < 0.5: w2's top bit clear,
+      // 4 words), else a random word (randint's first word w4 accepted: 5 words; rejected: the
+      // rare scan below); len 0 when the decision's words run past the look-ahead. Written as
+      // selects on three compares and a shift, so that no lane-mask logic runs on the scalar unit.
+      const bool mk = N64 < (lt08 << 6);
+      const uint32_t top = w2 >> 31;  // 1: not keep
       const uint32_t r4 = w4 >> (32 - kV);
-      const bool rand4 = is_rand && lane + 5 <= kLook && r4 < (uint32_t)V;  // randint's 1st word
-      int len = is_mask ? 2 : is_keep ? 4 : rand4 ? 5 : 0;
-      int32_t tok = is_mask ? mask_id : rand4 ? (int32_t)r4 : kKeep;
-      if (is_rand && !rand4) {  // randint rejected its first word: scan on (rare)
+      const bool r4ok = r4 < (uint32_t)V;
+      const int need = mk ? 2 : 4 + (int)top;
+      int len = lane + need > kLook ? 0 : mk ? 2 : top ? (r4ok ? 5 : 0) : 4;
+      int32_t tok = mk ? mask_id : top ? (int32_t)r4 : kKeep;
+      if (!mk && top && !r4ok) {  // randint rejected its first word: scan on (rare)
         for (int j = 5; lane + j < kLook; ++j) {
           const uint32_t r = temper(wp[j]) >> (32 - kV);
           if (r < (uint32_t)V) {
