@@ -392,7 +392,8 @@ struct WaveRng {
       }
       const int lp = __shfl(len, p & 63, 64);
       const int32_t tp = __shfl(tok, p & 63, 64);
-      const uint64_t okm = ballot(lane < 32 && p < 64 && lp > 0);  // a prefix of the lanes
+      // a prefix of the lanes (two compares, the scalar unit ANDs their ballots)
+      const uint64_t okm = ballot(p < 64) & ballot(lp > 0) & 0xFFFFFFFFull;
       int take = __ffsll((unsigned long long)~okm) - 1;
       if (take > cnt - c) take = cnt - c;
       const int32_t tk = __shfl(tp, (lane - c) & 63, 64);  // decision k goes to lane c + k
@@ -529,10 +530,12 @@ struct LenWin {
   // the reference's accumulate-until-target loops (pretrain.py:276-280, 314-317)
   __device__ int find(int a, int lim, int64_t T) {
     if (!has(a)) load(a);
+    // (window sums are < 2^31: 32-bit compares; two ballots combined by one scalar AND)
+    const int32_t T32 = T < -1 ? -1 : T > INT32_MAX ? INT32_MAX : (int32_t)T;
     for (int pass = 0; pass < 2; ++pass) {
       const int32_t base = a > wbase ? (int32_t)rdlane((uint32_t)pre, a - 1 - wbase) : 0;
       const int j = wbase + (int)threadIdx.x;
-      const uint64_t m = ballot(j >= a && j < lim && (int64_t)(pre - base) >= T);
+      const uint64_t m = ballot((uint32_t)(j - a) < (uint32_t)(lim - a)) & ballot(pre - base >= T32);
       if (m) return wbase + __ffsll((unsigned long long)m) - 1;
       if (wbase + 64 >= lim) return lim - 1;
       if (pass == 0 && wbase != a) load(a);  // restart the window at a and look again
