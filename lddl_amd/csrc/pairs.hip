@@ -521,9 +521,11 @@ struct LenWin {
     }
     const int32_t hi = (int32_t)rdlane((uint32_t)pre, b - 1 - wbase);
     const int32_t lo = a > wbase ? (int32_t)rdlane((uint32_t)pre, a - 1 - wbase) : 0;
-    const int cnt = b - a;
-    const uint64_t m = fl >> (a - wbase);
-    if ((cnt >= 64 ? m : (m & ((1ull << cnt) - 1))) != 0) flags |= kLenHasClsSep;
+    if (fl) {  // (a window without literal [CLS]/[SEP] skips the span mask: the common case)
+      const int cnt = b - a;
+      const uint64_t m = fl >> (a - wbase);
+      if ((cnt >= 64 ? m : (m & ((1ull << cnt) - 1))) != 0) flags |= kLenHasClsSep;
+    }
     return hi - lo;
   }
   // the smallest i in [a, lim) with length(a .. i) >= T, else lim - 1 (a < lim <= n): the end of
