@@ -317,10 +317,14 @@ struct WaveRng {
       const int32_t t = done + lane;
       // random() < 0.5 <=> the tempered first word's top bit is clear; tempering is linear over
       // GF(2) and that bit is the parity of raw bits 31, 27, 24 and 16
-      const bool front = lane < cnt && !(__popc(mt[mti + 2 * lane] & 0x89010000u) & 1);
-      const bool sa = t < d || (t >= ad && ((t - ad) & 1));
-      a_front += __popcll(ballot(front && sa));
-      b_front += __popcll(ballot(front && !sa));
+      // (every lane reads: mti + 126 stays inside the LDS block; lanes >= cnt are masked off
+      // by the scalar lane mask, not by an exec-mask branch)
+      const uint32_t par = __popc(mt[mti + 2 * lane] & 0x89010000u) & 1u;
+      const uint64_t F = ballot(par == 0) & ((1ull << cnt) - 1);  // cnt <= 32
+      const int32_t x = t - ad;
+      const uint64_t S = ballot(t < d) | (ballot(x >= 0) & ballot((x & 1) != 0));
+      a_front += __popcll(F & S);
+      b_front += __popcll(F & ~S);
       mti = uni(mti + 2 * cnt);
       done += cnt;
     }
