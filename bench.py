@@ -88,6 +88,16 @@ def make_batch(rank, args):
     return corp, part, seeds
 
 
+def st_moved_sum(x, world, dev):
+    """Sum of a per-rank count over all ranks (gloo on the host in the shared-device
+    rehearsal, RCCL otherwise)."""
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.int64, device=RED_DEV or dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
+
+
 def granted_cores():
     """Host cores this process may actually use: the CPU affinity mask, capped by the cgroup CPU
     quota (cgroup v2 cpu.max, else v1 cfs_quota_us / cfs_period_us). os.cpu_count() reports the
@@ -367,7 +377,9 @@ def run_c5(args):
         dl = get_bert_pretrain_data_loader(
             path, local_rank=0, vocab_file=VOCAB_CASED,
             data_loader_kwargs=dict({'batch_size': 256, 'num_workers': args.c5_workers},
-                                    **({'prefetch_factor': 4} if args.c5_workers else {})),
+                                    **({'prefetch_factor': 4} if args.c5_workers else {}),
+                                    **({'multiprocessing_context': args.c5_mp}
+                                       if args.c5_workers and args.c5_mp != 'fork' else {})),
             mlm_probability=0.15, base_seed=args.seed, log_level=logging.WARNING,
             sequence_length_alignment=8, ignore_index=-1)
         loaders = getattr(dl, '_dataloaders', [dl])
@@ -380,7 +392,9 @@ def run_c5(args):
         dev = torch.device('cuda', 0)
         if args.c5_blas != 'default':  # ('cublas' selects rocBLAS on ROCm)
             torch.backends.cuda.preferred_blas_library('cublas' if args.c5_blas == 'rocblas' else 'cublaslt')
-        model = TinyBert(len(loaders[0]._ctx)).to(dev)
+        with open(VOCAB_CASED, 'rb') as f:  # (not loaders[0]._ctx: that would create the
+            n_vocab = sum(1 for _ in f)        # loader's Context before its workers start)
+        model = TinyBert(n_vocab).to(dev)
         params = list(model.parameters())
 
         def sgd_step(lr=1e-4):
@@ -448,7 +462,10 @@ def run_c5(args):
                     gev.append((e0, e1))
                     tw += time.perf_counter() - w0
             torch.cuda.synchronize()
-            timed.gpu_ms = float(np.mean([a.elapsed_time(z) for a, z in gev])) if gev else None
+            gms = [a.elapsed_time(z) for a, z in gev]
+            timed.gpu_ms = float(np.mean(gms)) if gev else None
+            timed.gpu_ms_pct = ([round(float(np.percentile(gms, q)), 2) for q in (50, 90, 100)]
+                                if gev else None)
             dt = time.perf_counter() - t
             st = {k: sum((x.stats[k] for x in loaders), []) for k in loaders[0].stats}
             for x in loaders:
@@ -483,7 +500,23 @@ def run_c5(args):
         m1 = torch.cuda.memory_stats()
         cg = {k: c1[k] - c0.get(k, 0) for k in ('usage_usec', 'nr_periods', 'nr_throttled',
                                                   'throttled_usec') if k in c1}
-        train_gpu_ms = timed.gpu_ms
+        train_gpu_ms, train_gpu_pct = timed.gpu_ms, timed.gpu_ms_pct
+        # the same training step alone, on batches already resident in HBM (no loader in the
+        # loop): what the step costs when nothing else runs beside it
+        res_b = [next(it) for _ in range(8)]
+        torch.cuda.synchronize()
+        ra = []
+        t_alone = time.perf_counter()
+        for i in range(args.steps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            train(res_b[i % len(res_b)])
+            e1.record()
+            ra.append((e0, e1))
+        torch.cuda.synchronize()
+        t_alone = time.perf_counter() - t_alone
+        alone_gms = [a.elapsed_time(z) for a, z in ra]
+        del res_b
         host_phases = {k: round(v / args.steps * 1e3, 3) for k, v in
                        zip(('forward', 'backward', 'optimizer'), phase_s)}
         dev_allocs = int(m1.get('num_device_alloc', 0) - m0.get('num_device_alloc', 0))
@@ -518,6 +551,16 @@ def run_c5(args):
                 'loader_wait_ms_per_step': tn / args.steps * 1e3,
                 'train_step_host_ms': tw / args.steps * 1e3,
                 'train_step_gpu_ms': train_gpu_ms,
+                'train_step_gpu_ms_p50_p90_max': train_gpu_pct,
+                'train_step_alone': {
+                    'ms_per_step': t_alone / args.steps * 1e3,
+                    'gpu_ms': float(np.mean(alone_gms)),
+                    'gpu_ms_p50_p90_max': [round(float(np.percentile(alone_gms, q)), 2)
+                                           for q in (50, 90, 100)],
+                    'note': 'the same step on 8 HBM-resident batches in turn, no loader in the '
+                            'loop'},
+                'worker_start_method': args.c5_mp,
+                'pinned_stager_allocations': loaders[0]._stager.allocations,
                 'train_step_host_ms_by_phase': host_phases,
                 'device_mallocs_frees_in_timed_steps': [dev_allocs, dev_frees],
                 'cgroup_cpu_stat_delta': cg,  # CPU quota throttling of the container while timed
@@ -572,6 +615,8 @@ def main():
                     help='c5: GEMM library of the training step (torch preferred_blas_library)')
     ap.add_argument('--c5-workers', type=int, default=2,
                     help='DataLoader workers per bin (= shards per bin of the C5 dataset)')
+    ap.add_argument('--c5-mp', choices=('fork', 'forkserver', 'spawn'), default='fork',
+                    help='c5: start method of the DataLoader workers (multiprocessing_context)')
     ap.add_argument('--chunks', type=int, default=1,
                     help='c2: split the step into partition-aligned chunks, tokenizing chunk k+1 '
                          'on a side stream under chunk k\'s pair planner')
@@ -842,10 +887,14 @@ def main():
         sent_len = [sl]
     pieces = sum(int((sl.cpu().numpy() & ((1 << 30) - 1)).sum(dtype=np.int64)) for sl in sent_len)
     bal_ms = None
+    moved_all = rows_all = None
     if stream:  # one more, untimed step with the balance phases timed (summed over sub-batches)
         diag['balance'] = {}
         step()
         bal_ms = diag.pop('balance')
+        # rows that crossed ranks in one timed step, summed over ranks (the imbalance only)
+        moved_all = int(st_moved_sum(stats[-1]['moved_rows'], world, dev))
+        rows_all = int(st_moved_sum(stats[-1]['pairs'], world, dev))
     alt = None
     if args.alt_rng:  # the other RNG mode on the same batch, reported beside the headline
         other = 'native' if args.rng == 'replay' else 'replay'
@@ -983,8 +1032,13 @@ def main():
     res['roofline'] = plan_roof if plan_ms >= tok_ms else tok_roof
     if bal_ms is not None:
         res['balance_phases_ms_untimed_step'] = bal_ms
-        res['balance'] = {'num_shards': n_shards, 'moved_rows_per_step': st.get('moved_rows'),
-                          'max_shard_spread_rows': st.get('shard_counts_spread')}
+        res['balance'] = {'num_shards': n_shards, 'moved_rows_per_step': moved_all,
+                          'rows_per_step': rows_all,
+                          'max_shard_spread_rows': st.get('shard_counts_spread'),
+                          'exchange_ms_untimed_step': bal_ms.get('exchange'),
+                          'note': 'moved_rows_per_step: rows received from other ranks in one '
+                                  'step, all ranks (only the per-bin surplus over each rank\'s '
+                                  'shard quota moves, balance.py)'}
     if alt is not None:
         res['alt_rng'] = alt
     if seg is not None:

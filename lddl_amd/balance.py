@@ -2,29 +2,31 @@
 
 The reference balances shards through the filesystem after preprocessing
 (lddl/dask/load_balance.py:41-369: MPI Allreduce of per-file counts, then read / concat /
-rewrite of parquet files) so that, per bin, every shard ends with N or N+1 samples (`Progress`
-targets, load_balance.py:161-169). Here the same contract is met batch by batch while the
-samples are in HBM, so a rank never holds more than one batch of pair tables, at any corpus size:
+rewrite of parquet files, moving only `L - (L + S) // 2` samples between a large and a small
+shard, :129-140) so that, per bin, every shard ends with N or N+1 samples (`Progress` targets,
+:161-169). Here the same contract is met batch by batch while the samples are in HBM, so a rank
+never holds more than one batch of pair tables, at any corpus size, and only the imbalance
+crosses ranks:
 
-  * the global order of bin b is batch after batch, rank after rank inside a batch, each rank's
-    rows in their stable bin order (`lddl_bin_stable`, binning.py:63-93 semantics);
-  * global row g of bin b goes to shard g % S (round-robin deal). Every prefix of a deal is
-    balanced, so after ANY number of batches each shard holds N or N+1 rows of every bin, the
-    first total % S shards the extra one — and a batch can be balanced, written and freed before
-    the next batch is built;
   * per batch, each rank all-gathers its per-bin counts (int64[W, B], RCCL: the north star's
-    bin-count all-gather); with the totals of earlier batches every rank then knows the global
-    index of every row, and the rows of (source rank j, bin b, shard s) form one arithmetic run
-    of j's bin-b rows (`deal_runs`: first row (s - g0) mod S, stride S);
-  * shard s belongs to rank s * W // S. Rows of other ranks' shards cross in one all-to-all-v of
-    row metadata and one per ragged column (token ids, masked positions as bytes, labels);
-  * a rank's output is its shards' runs, bin-major, then shard, then source rank (= global order
-    inside a shard): a row order over [own table | received rows] built on the device
-    (`lddl_expand_segments`), materialised into one table (two-source ragged gathers) only when
-    rows arrived.
+    bin-count all-gather). From them and the totals of earlier batches every rank derives the
+    same plan (host integer math, replicated);
+  * shard targets: after the batch, shard s holds cum_s(n) = n // S + (s < n % S) rows of a bin
+    that has seen n rows in all — N or N+1 after EVERY batch (`shard_cum`); this batch adds
+    cum_s(prior + total) - cum_s(prior) rows to shard s (`batch_shard_counts`);
+  * shard s belongs to rank s * W // S; a rank's quota of bin b is the sum over its shards. Each
+    rank keeps the first min(count, quota) of its bin-b rows (stable bin order); the surplus
+    tails of the ranks above quota, in rank order, fill the ranks below quota, in rank order (a
+    two-pointer merge, `surplus_moves`). So exactly sum_j max(0, c_jb - q_jb) rows of bin b move,
+    the least any plan can move, and nothing when the ranks' batches are already balanced;
+  * the moving rows cross in one all-to-all-v of row metadata and one per ragged column (token
+    ids, masked positions as bytes, labels);
+  * a rank's output of bin b is [its kept rows | received rows, by source rank], dealt in
+    consecutive runs to its shards in ascending order: a row order over [own table | received
+    rows] built on the device (`lddl_expand_segments`), materialised into one table (two-source
+    ragged gathers) only when rows arrived.
 
-At world size 1 nothing moves: the result is a row order over the batch's own table. At W > 1
-(W - 1) / W of the rows cross ranks, the price of a balance that needs only the current batch.
+At world size 1 nothing moves: the result is a row order over the batch's own table.
 
 Every device step is a HIP kernel of liblddl_amd.so (`HipOps`); the plan is host integer math,
 replicated on every rank. The per-rank phases (`RankBalance`: bin, plan, pack, unpack, regroup)
@@ -49,29 +51,54 @@ def shard_owner(num_shards, world):
     return (np.arange(num_shards, dtype=np.int64) * world) // num_shards
 
 
+def shard_cum(n, num_shards):
+    """int64[S, B]: rows of each shard once n[b] rows of bin b have been dealt in all: N or N+1,
+    the first n % S shards +1 (the reference's Progress targets, load_balance.py:161-169)."""
+    n = np.asarray(n, np.int64)
+    S = int(num_shards)
+    return n[None, :] // S + (np.arange(S)[:, None] < (n % S)[None, :]).astype(np.int64)
+
+
 def shard_targets(counts, num_shards):
-    """int64[S, B]: samples of bin b in shard s after dealing sum(counts) rows (N or N+1; the
-    first total % S shards get +1, the reference's Progress targets, load_balance.py:161-169)."""
+    """int64[S, B]: samples of bin b per shard after sum(counts) rows (shard_cum of the total)."""
     total = np.asarray(counts, np.int64).reshape(-1, np.shape(counts)[-1]).sum(0)
-    base, rem = total // num_shards, total % num_shards
-    return base[None, :] + (np.arange(num_shards)[:, None] < rem[None, :]).astype(np.int64)
+    return shard_cum(total, num_shards)
 
 
-def deal_runs(g0, counts, num_shards):
-    """Rows whose global indices are g0 .. g0 + counts - 1 (per bin), dealt to shard g % S:
-    returns (first, n), int64[..., B, S]: shard s gets the block's rows first + t * S, t < n."""
-    g0 = np.asarray(g0, np.int64)
-    c = np.asarray(counts, np.int64)[..., None]
-    first = (np.arange(num_shards, dtype=np.int64) - g0[..., None]) % num_shards
-    n = np.where(first < c, (c - 1 - first) // num_shards + 1, 0)
-    return first, n
+def batch_shard_counts(prior, total, num_shards):
+    """int64[S, B]: rows of bin b that one batch of total[b] rows adds to shard s, after prior[b]
+    rows in earlier batches; the running layout stays N / N+1 after every batch."""
+    return shard_cum(np.asarray(prior, np.int64) + total, num_shards) - shard_cum(prior, num_shards)
 
 
-def batch_start(prior, counts):
-    """g0[j, b]: global index of rank j's first bin-b row of this batch (prior[b] rows of bin b in
-    earlier batches; ranks in order)."""
-    counts = np.asarray(counts, np.int64)
-    return np.asarray(prior, np.int64)[None, :] + np.cumsum(counts, 0) - counts
+def rank_quota(shard_n, world):
+    """int64[W, B]: rows of bin b that rank k must hold after the batch (its shards' counts)."""
+    S, B = shard_n.shape
+    q = np.zeros((world, B), np.int64)
+    np.add.at(q, shard_owner(S, world), shard_n)
+    return q
+
+
+def surplus_moves(counts, quota):
+    """(m, off), int64[W, W, B]: m[j, k, b] rows of bin b go from rank j to rank k; they are the
+    rows off[j, k, b] .. + m of j's surplus (its bin-b rows past its quota). Surplus ranks in rank
+    order fill deficit ranks in rank order; only the imbalance moves:
+    m.sum() == sum(max(0, counts - quota))."""
+    counts, quota = np.asarray(counts, np.int64), np.asarray(quota, np.int64)
+    sur = np.maximum(counts - quota, 0)
+    need = np.maximum(quota - counts, 0)
+    s0 = np.cumsum(sur, 0) - sur
+    d0 = np.cumsum(need, 0) - need
+    lo = np.maximum(s0[:, None, :], d0[None, :, :])
+    hi = np.minimum((s0 + sur)[:, None, :], (d0 + need)[None, :, :])
+    m = np.maximum(hi - lo, 0)
+    return m, np.where(m > 0, lo - s0[:, None, :], 0)
+
+
+def _host_staged(group):
+    """True when the backend moves host tensors only (gloo): device tensors are then staged
+    through host memory (the one-GPU rehearsal of several ranks; RCCL takes them directly)."""
+    return dist.get_backend(group) != 'nccl'
 
 
 def gather_counts(local_counts, group=None):
@@ -80,6 +107,8 @@ def gather_counts(local_counts, group=None):
     if W == 1:
         return local_counts.reshape(1, -1).cpu().numpy()
     flat = local_counts.contiguous().reshape(-1)
+    if flat.is_cuda and _host_staged(group):
+        flat = flat.cpu()
     out = torch.empty(W * flat.numel(), dtype=flat.dtype, device=flat.device)
     dist.all_gather_into_tensor(out, flat, group=group)
     return out.cpu().numpy().reshape((W,) + tuple(local_counts.shape))
@@ -251,62 +280,50 @@ class RankBalance:
     # plan ----------------------------------------------------------------------------------
     def set_plan(self, counts, prior):
         """counts int64[W, B]: every rank's rows per bin in this batch; prior int64[B]: rows of
-        each bin in earlier batches (all ranks)."""
+        each bin in earlier batches (all ranks). Replicated: every rank computes the same plan."""
         W, me, B, S = self.W, self.me, self.nbins, self.S
         self.counts = np.asarray(counts, np.int64)
-        first, n = deal_runs(batch_start(prior, self.counts), self.counts, S)  # [W, B, S]
-        owner = shard_owner(S, W)
-        self.shards = [int(s) for s in np.nonzero(owner == me)[0]]
+        shard_n = batch_shard_counts(prior, self.counts.sum(0), S)   # [S, B]
+        quota = rank_quota(shard_n, W)                                # [W, B]
+        m, off = surplus_moves(self.counts, quota)                    # [W, W, B]
+        self.shards = [int(x) for x in np.nonzero(shard_owner(S, W) == me)[0]]
         mine = np.asarray(self.shards, np.int64)
+        keep = np.minimum(self.counts[me], quota[me])
         bin0 = np.concatenate([[0], np.cumsum(self.counts[me])])[:-1]
-        # rows leaving this rank: destination-major, then bin, then shard (each run strided by S)
+        # rows leaving this rank: destination-major, then bin; one contiguous run of the bin's
+        # surplus tail each (through perm, the stable bin order)
         seg, lens = [], []
-        self.send_rows_per_dst = [0] * W
         for k in range(W):
-            if k == me:
-                continue
-            ks = np.nonzero(owner == k)[0]
             for b in range(B):
-                for s in ks:
-                    c = int(n[me, b, s])
-                    if c:
-                        seg.append((int(bin0[b] + first[me, b, s]), S, 0))
-                        lens.append(c)
-                        self.send_rows_per_dst[k] += c
+                c = int(m[me, k, b])
+                if c:
+                    seg.append((int(bin0[b] + keep[b] + off[me, k, b]), 1, 0))
+                    lens.append(c)
         self._send_seg = (seg, lens)
+        self.send_rows_per_dst = [int(x) for x in m[me].sum(1)]
         self.n_send = sum(self.send_rows_per_dst)
-        # rows arriving from rank j: j's runs of (bin, my shard), in j's send order
-        self.recv_rows_per_src = [0 if j == me else int(n[j][:, mine].sum()) for j in range(W)]
+        self.recv_rows_per_src = [int(x) for x in m[:, me].sum(1)]
         self.n_recv = sum(self.recv_rows_per_src)
         recv0 = np.concatenate([[0], np.cumsum(self.recv_rows_per_src)])
-        # output order over [own rows (through perm) | received rows]: bin, my shard, source rank
+        within = np.cumsum(m[:, me, :], 1) - m[:, me, :]  # [W, B]: bin b's run inside j's rows
+        # output order over [own rows (through perm) | received rows]: per bin, the kept rows,
+        # then the received ones by source rank
         n_local = self.pb.n_pairs
-        within = {}  # (j, b, s) -> offset of the run inside j's rows for me
-        for j in range(W):
-            if j == me:
-                continue
-            o = 0
-            for b in range(B):
-                for s in mine:
-                    within[(j, b, int(s))] = o
-                    o += int(n[j, b, s])
         seg, lens = [], []
         for b in range(B):
-            for s in mine:
-                for j in range(W):
-                    c = int(n[j, b, s])
-                    if not c:
-                        continue
-                    if j == me:
-                        seg.append((int(bin0[b] + first[me, b, s]), S, 0))
-                    else:
-                        seg.append((int(n_local + recv0[j] + within[(j, b, int(s))]), 1, 1))
+            if keep[b]:
+                seg.append((int(bin0[b]), 1, 0))
+                lens.append(int(keep[b]))
+            for j in range(W):
+                c = int(m[j, me, b])
+                if c:
+                    seg.append((int(n_local + recv0[j] + within[j, b]), 1, 1))
                     lens.append(c)
         self._order_seg = (seg, lens)
-        per_bin = n[:, :, mine].sum(axis=(0, 2)) if len(mine) else np.zeros(B, np.int64)
-        self.bin_off = np.concatenate([[0], np.cumsum(per_bin)]).astype(np.int64)
-        self.batch_shard_counts = n.sum(0).T.copy()  # [S, B]
-        self.shard_counts = self.batch_shard_counts[mine] if len(mine) else np.zeros((0, B), np.int64)
+        assert np.array_equal(keep + m[:, me, :].sum(0), quota[me])
+        self.bin_off = np.concatenate([[0], np.cumsum(quota[me])]).astype(np.int64)
+        self.batch_shard_counts = shard_n
+        self.shard_counts = shard_n[mine] if len(mine) else np.zeros((0, B), np.int64)
         self.send_idx = self._expand(self._send_seg)
 
     def _expand(self, segs):
@@ -376,10 +393,13 @@ class RankBalance:
 # ---- drivers ---------------------------------------------------------------------------------
 def _a2a(payload, group):
     send, send_splits, recv_splits = payload
+    dev = send.device
+    if send.is_cuda and _host_staged(group):
+        send = send.cpu()
     recv = _alloc(sum(recv_splits), send.dtype, send.device)
     dist.all_to_all_single(recv, send, [int(x) for x in recv_splits],
                            [int(x) for x in send_splits], group=group)
-    return recv
+    return recv.to(dev)
 
 
 class StreamBalancer:

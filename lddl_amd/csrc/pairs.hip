@@ -599,13 +599,10 @@ __device__ inline void densify_group(int64_t k0, const int64_t* __restrict__ ks_
 // waves per SIMD the compiler must keep: 8 caps the kernel at 78 SGPRs (140 spilled to VGPR
 // lanes); 6 lets it use all 106 (59 spilled) at 7 waves/SIMD, 176 -> 169.6 ms per 10 GB
 // (profiles/r02_plan_minw_ab.txt)
-#ifndef LDDL_PLAN_MINW
-#define LDDL_PLAN_MINW 6
-#endif
 // kDocsLds: every partition's document offsets fit the LDS table (host-checked: <= kDocLds
 // documents), so the document lookups carry no global-memory branch; kJB: bytes per shuffle draw
 template <bool kDocsLds, int kJB>
-__global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArgs A) {
+__global__ void __launch_bounds__(64, 6) plan_replay_kernel(PlanArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* s_mt = reinterpret_cast<uint32_t*>(smem);
   int32_t* s_doc = reinterpret_cast<int32_t*>(s_mt + kN + kLook);  // [kDocLds + 1]
@@ -654,10 +651,7 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
   bool pool_fits = true, jpool_fits = true;
   LenWin La, Lb;
   int64_t np = 0;
-#ifndef LDDL_PLAN_PRIO
-#define LDDL_PLAN_PRIO 4  // priority levels used (s_setprio has 4); 0 = age order only
-#endif
-#if LDDL_PLAN_PRIO > 0
+  constexpr int kPrioLevels = 4;  // priority levels used (s_setprio has 4)
   // issue priority by progress: a SIMD issues its highest-priority (then oldest) wave first, so
   // waves that are behind (e.g. a partition dispatched into a freed slot) catch up and the waves
   // of a SIMD finish together instead of leaving the last ones running alone
@@ -666,21 +660,18 @@ __global__ void __launch_bounds__(64, LDDL_PLAN_MINW) plan_replay_kernel(PlanArg
   // the priority steps at the document counts where progress crosses a quarter (no 64-bit
   // division per document)
   int32_t prio_next = 0, prio_done = 0;
-#endif
   for (int dp = 0; dp < A.dup; ++dp) {
     for (int32_t di = 0; di < nd; ++di) {
-#if LDDL_PLAN_PRIO > 0
       if (prio_done >= prio_next) {
         ++prio_q;
-        prio_next = (int32_t)(((int64_t)(prio_q + 1) * prio_tot + LDDL_PLAN_PRIO - 1) / LDDL_PLAN_PRIO);
-        const int lvl = LDDL_PLAN_PRIO - 1 - prio_q;
+        prio_next = (int32_t)(((int64_t)(prio_q + 1) * prio_tot + kPrioLevels - 1) / kPrioLevels);
+        const int lvl = kPrioLevels - 1 - prio_q;
         if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
         else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
         else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
       }
       ++prio_done;
-#endif
       const int32_t ls0 = doc_loc(di);
       const int64_t s0 = kbase + ls0;
       const int ns = doc_loc(di + 1) - ls0;
@@ -1468,11 +1459,8 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
 // masked tokens before it in the half-wave, from four ballots.
 typedef int32_t tok4_t __attribute__((ext_vector_type(4), aligned(4)));
 
-#ifndef LDDL_GMINW
-#define LDDL_GMINW 1
-#endif
 template <int K>
-__global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(GatherArgs G, GatherLds Lg) {
+__global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, GatherLds Lg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, sl = lane & 31;
   const int64_t wg = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
@@ -1571,13 +1559,8 @@ __global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(Gather
         for (int e = 0; e < 4; ++e) {
           if (mk[e]) {
             const int32_t xe = x + e, pos = xe < na[k] ? xe + 1 : xe + 2;
-#ifdef LDDL_GATHER_NT_MASKS  // A/B experiment only
-            __builtin_nontemporal_store((uint16_t)pos, G.out_pos + po[k] + rank);
-            __builtin_nontemporal_store(v[k][e], G.out_lab + po[k] + rank);
-#else
             G.out_pos[po[k] + rank] = (uint16_t)pos;
             G.out_lab[po[k] + rank] = v[k][e];
-#endif
             const int32_t d = dec[k][pos];
             if (d != kKeep) v[k][e] = d;
             ++rank;
@@ -1587,15 +1570,6 @@ __global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(Gather
       }
       // non-temporal: the output is streamed, never re-read by this step
       int32_t* out = G.out_tok + tof[k];
-#ifdef LDDL_GATHER_PLAIN_STORE  // A/B experiment only
-      if (x + 3 < n) {
-        *reinterpret_cast<tok4_t*>(out + x) = v[k];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (x + e < n) out[x + e] = v[k][e];
-      }
-#else
       if (x + 3 < n) {
         __builtin_nontemporal_store(v[k], reinterpret_cast<tok4_t*>(out + x));
       } else {
@@ -1603,7 +1577,6 @@ __global__ void __launch_bounds__(64 * kGWaves, LDDL_GMINW) gather_kernel(Gather
         for (int e = 0; e < 4; ++e)
           if (x + e < n) __builtin_nontemporal_store(v[k][e], out + x + e);
       }
-#endif
       more |= n > cb + 128;
     }
     if (!ballot(more)) break;
@@ -2166,10 +2139,7 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
     hipLaunchKernelGGL(kern, dim3((unsigned)gx, (unsigned)((nwg + gx - 1) / gx)), dim3(64 * kGWaves),
                        lds, st, G, Lg);
   };
-#ifndef LDDL_GK
-#define LDDL_GK 2
-#endif
-  if (P->seq <= 600) launch(gather_kernel<LDDL_GK>, LDDL_GK);
+  if (P->seq <= 600) launch(gather_kernel<2>, 2);
   else launch(gather_kernel<1>, 1);  // (LDS: seq-entry decision tables)
   LDDL_HIP(hipGetLastError());
   if (d_tok_off)

@@ -475,11 +475,7 @@ __device__ inline bool eval_candidate(const PunktTab& t, const Src& src, int64_t
 // enders in one run, so one per run is what keeps writes inside the range).
 // 6 waves per SIMD (<= 80 VGPRs): 5.8 ms per 2 GiB vs 6.1 at the compiler's 96 VGPRs / 5 waves
 // and 6.3 at 8 waves (64 VGPRs, spills) -- profiles/r01_v14_segment_variants.txt
-#ifndef LDDL_SEG_WPE
-#define LDDL_SEG_WPE 6
-#endif
-#define LDDL_SEG_ATTR __attribute__((amdgpu_waves_per_eu(LDDL_SEG_WPE)))
-__global__ void __launch_bounds__(64 * kSegWaves) LDDL_SEG_ATTR segment_classify_kernel(
+__global__ void __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(6))) segment_classify_kernel(
     PunktTab t, const uint8_t* __restrict__ x, int64_t n_bytes, const int64_t* __restrict__ doc_off,
     int64_t n_doc, int32_t* __restrict__ cand, int32_t* __restrict__ ccnt, int32_t* __restrict__ rs_rel,
     int32_t* __restrict__ cnt) {

@@ -356,24 +356,8 @@ __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v,
     // (the caller may already know that the whole word is not one piece)
     int32_t id = len > 0 && !(first_probe_missed && start == 0 && len == nb) ? probe32(T, a, len, cont)
                                                                               : -1;
-#ifdef LDDL_TOK_ONE_PROBE  // A/B experiment only: one full-length probe per unit
-    pc.put(0, id < 0 ? T.special_id[kUnk] : id);
-    return 1;
-#endif
-#ifdef LDDL_TOK_NO_BLOOM  // A/B experiment only: descending probes without the Bloom filter
-    while (id < 0 && --len > 0)
-      if ((e >> len) & 1ull) id = probe32(T, a, len, cont);
-#endif
     if (id < 0 && len > 1) {
       uint32_t cand = bloom_candidates32(bloom, a, len - 1, cont) & (uint32_t)(e >> 1);
-#ifdef LDDL_TOK_SEQ_PROBES  // A/B: one candidate's table load at a time
-      while (cand) {
-        len = 32 - __clz(cand);
-        id = probe32(T, a, len, cont);
-        if (id >= 0) break;
-        cand &= ~(1u << (len - 1));
-      }
-#else
       // the two longest remaining candidates' home slots are loaded together (the chain of
       // dependent table loads per piece is what a lane waits on), the longer one decides first
       while (cand) {
@@ -396,7 +380,6 @@ __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v,
         }
         cand = l2 ? rest & ~(1u << (l2 - 1)) : 0u;
       }
-#endif
     }
     if (id < 0) {  // no piece: the whole word is [UNK]
       pc.put(0, T.special_id[kUnk]);
@@ -579,10 +562,6 @@ __device__ int unit_pieces(const Tables& T, const uint32_t* bloom, const uint32_
                            int len, int kind, bool unit_slow, Pcs& pc, uint8_t* w,
                            bool& cs_flag) {
   cs_flag = false;
-#ifdef LDDL_TOK_NO_WP  // A/B experiment only: classification + placement without WordPiece
-  pc.put(0, (int32_t)len);
-  return 1;
-#endif
   if (kind >= 2) {
     pc.put(0, T.special_id[kind - 2]);
     cs_flag = kind - 2 == kCls || kind - 2 == kSep;
@@ -778,21 +757,12 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
 // kept a ring of in-flight sentences; its per-window bookkeeping was ~half of the kernel's
 // instructions (profiles/r03l_pmc_tokenizer_variants.txt).
 // ---------------------------------------------------------------------------------------------
-#ifndef LDDL_TOK_SF
-#define LDDL_TOK_SF 192
-#endif
-#ifndef LDDL_TOK_BW
-#define LDDL_TOK_BW 16
-#endif
-constexpr int kSF = LDDL_TOK_SF;   // units resolved per pass (kSF / 64 phase-A rounds)
+constexpr int kSF = 192;   // units resolved per pass (kSF / 64 phase-A rounds)
 // queue capacity: before a bank < kSF complete units; a bank adds <= 64 ends and leaves <= 65
 // units open (started, end not yet enqueued)
 constexpr int kQ = kSF + 128;
-constexpr int kBW = LDDL_TOK_BW;   // waves per workgroup (one workgroup per CU shares the Bloom filter)
-#ifndef LDDL_TOK_CHUNK
-#define LDDL_TOK_CHUNK 128
-#endif
-constexpr int kChunk = LDDL_TOK_CHUNK;  // consecutive sentences claimed at a time
+constexpr int kBW = 16;   // waves per workgroup (one workgroup per CU shares the Bloom filter)
+constexpr int kChunk = 128;  // consecutive sentences claimed at a time
 static_assert((kChunk & (kChunk - 1)) == 0, "binary search over the chunk's sentences");
 using HIdx = std::conditional_t<(kSF > 256), uint16_t, uint8_t>;
 constexpr int32_t kHardBit = INT32_MIN;  // q_res: pieces are in column (res & 63) of pcs
@@ -823,23 +793,16 @@ struct alignas(16) StreamLds {
 };
 static_assert(kPcs * 64 * 4 >= 64 * kNorm, "normalised-word rows must fit the piece columns");
 
-#ifndef LDDL_TOK_MIN_WAVES
-#define LDDL_TOK_MIN_WAVES 1
-#endif
 #ifdef LDDL_STAMPS
 __device__ unsigned long long* g_tok_tl;  // diagnostic build: [wave][2] s_memrealtime start / end
 #endif
-__global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_kernel(
+__global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
     Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
     int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
     int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr) {
   __shared__ uint32_t s_ascii[128];
   __shared__ uint8_t s_cls[256];
-#ifdef LDDL_TOK_BLOOM_GLOBAL  // A/B: Bloom filter read through the caches, LDS for more waves
-  const uint32_t* s_bloom = T.bloom;
-#else
   __shared__ uint32_t s_bloom[kBloomWords];
-#endif
   __shared__ StreamLds s_w[kBW];
 #ifdef LDDL_STAMPS
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
@@ -853,9 +816,7 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
     }
     s_cls[c] = (uint8_t)v;
   }
-#ifndef LDDL_TOK_BLOOM_GLOBAL
   for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
-#endif
   __syncthreads();
   const int lane = lane_id();
   StreamLds& W = s_w[threadIdx.x >> 6];
@@ -966,10 +927,6 @@ __global__ void __launch_bounds__(64 * kBW, LDDL_TOK_MIN_WAVES) tokenize_batch_k
               } else {
                 hardr[r] = true;
               }
-#ifdef LDDL_TOK_NO_WP  // A/B experiment only: classification + placement without WordPiece
-              elig[r] = hardr[r] = false;
-              resr[r] = len;
-#endif
             }
           }
 #pragma unroll
@@ -1235,11 +1192,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     return 0;
   }
   // fallback list: [0] = count, then sentence indices
-#ifdef LDDL_TOK_COUNT_FLUSH
-  constexpr int kFbHead = 3;  // [0] fallback count, [1] flushes, [2] units flushed
-#else
   constexpr int kFbHead = 1;
-#endif
   DevArena::Block fbb;
   // + the batch kernel's chunk counter after the list
   LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)(n_sent + kFbHead + 1), st, fbb));
@@ -1312,14 +1265,6 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
                      d_text, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + kFbHead,
                      reinterpret_cast<const uint32_t*>(fb));
   LDDL_HIP(hipGetLastError());
-#ifdef LDDL_TOK_COUNT_FLUSH
-  {
-    uint32_t h[3];
-    LDDL_HIP(hipMemcpyAsync(h, fb, 12, hipMemcpyDeviceToHost, st));
-    LDDL_HIP(hipStreamSynchronize(st));
-    fprintf(stderr, "[tok] flushes=%u units=%u (%.1f per flush)\n", h[1], h[2], (double)h[2] / (h[1] + 1e-9));
-  }
-#endif
   c->arena.give(fbb, st);
   return 0;
 }

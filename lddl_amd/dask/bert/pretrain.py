@@ -112,16 +112,6 @@ def rank_batches(args, blocks, rank=0, world=1):
     return _greedy(groups, lambda g: sum(blocks[p].nbytes for p in g), args.gpu_batch_bytes)
 
 
-def n_gpu_batches(args, blocks, rank=0, world=1):
-    """GPU batches of `rank` (iter_doc_batches / iter_batches): the read batches of whole
-    shuffle groups, the GPU path's cut into runs of <= --gpu-batch-bytes of input."""
-    rb = rank_batches(args, blocks, rank, world)
-    if args.sentence_splitter == 'host':
-        return len(rb)
-    return sum(len(_greedy([p for g in b for p in g], lambda p: blocks[p].nbytes,
-                           args.gpu_batch_bytes)) for b in rb)
-
-
 def iter_batches(args, rank=0, world=1, blocks=None, as_bytes=False):
     """This rank's partitions in GPU batches, read lazily: yields [(p, lines)] per batch. The
     documents of each shuffle group are shuffled over the group's partitions (each keeps its
@@ -392,31 +382,86 @@ def write_txt(outdir, rd, part_rows, index, masking, nbins, counts, n_part):
     return paths
 
 
+def _open_file_budget(needed, headroom=256):
+    """Raise this process's soft RLIMIT_NOFILE so that `needed` parquet writers can stay open
+    (plus headroom for pyarrow, sockets and libraries); False if the hard limit is too low."""
+    import resource
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    want = needed + headroom
+    if soft == resource.RLIM_INFINITY or want <= soft:
+        return True
+    if hard != resource.RLIM_INFINITY and want > hard:
+        return False
+    try:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (want, hard))
+    except (ValueError, OSError):
+        return False
+    return True
+
+
 class ShardWriters:
     """This rank's balanced shards, written as the batches stream through: one parquet file per
     (shard, bin) named like the load balancer's (`shard-<k>.parquet_<b>`, or `shard-<k>.parquet`
     unbinned, load_balance.py:90-92), one row group per batch in batch order. Each batch's
     writes run on the thread pool while the next batch is on the GPU; a writer is never
-    appended from two threads (a batch's writes finish before the next batch's start)."""
+    appended from two threads (a batch's writes finish before the next batch's start).
 
-    def __init__(self, outdir, nbins, binned, masking, pool):
+    Every (shard, bin) file stays open until close() (the reference example's 4096 shards x 8
+    bins are 32,768 files on one rank): the soft RLIMIT_NOFILE is raised for them. When the hard
+    limit (or `max_open`) cannot hold them all, each batch's row group is written to a piece file
+    and closed at once, and close() appends the pieces of each shard, in batch order, into its
+    file (the same files, one more pass over the data)."""
+
+    def __init__(self, outdir, nbins, binned, masking, pool, n_local_shards=None, max_open=None):
         self.outdir, self.nbins, self.binned, self.masking, self.pool = (outdir, nbins, binned,
                                                                          masking, pool)
         self.writers, self.pending, self.shards, self.jobs = {}, [], set(), []
+        needed = (n_local_shards or 0) * nbins
+        self.pieces = None  # {(shard, bin): [piece paths]} in piece mode
+        if (max_open is not None and needed > max_open) or not _open_file_budget(needed):
+            self.pieces = {}
+            self.piece_dir = os.path.join(outdir, '.lddl_amd_pieces.{}'.format(os.getpid()))
+            os.makedirs(self.piece_dir, exist_ok=True)
 
     def name(self, s, b):
         return os.path.join(self.outdir, 'shard-{}.parquet{}'.format(
             s, '_{}'.format(b) if self.binned else ''))
 
     def _append(self, key, rd, r0, r1):
+        from ... import output
+        self._write(key, output.table(rd, r0, r1, self.masking, self.binned))
+
+    def _write(self, key, t):
         import pyarrow.parquet as pq
         from ... import output
-        t = output.table(rd, r0, r1, self.masking, self.binned)
+        if self.pieces is not None:
+            lst = self.pieces.setdefault(key, [])
+            fn = os.path.join(self.piece_dir, '{}_{}.{}'.format(key[0], key[1], len(lst)))
+            pq.write_table(t, fn, compression=output.DEFAULT_COMPRESSION)
+            lst.append(fn)
+            return
         w = self.writers.get(key)
         if w is None:
             w = self.writers[key] = pq.ParquetWriter(self.name(*key), t.schema,
                                                      compression=output.DEFAULT_COMPRESSION)
         w.write_table(t)
+
+    def _merge(self, key):
+        """Piece mode: the pieces of one (shard, bin), row group by row group, into its file."""
+        import pyarrow.parquet as pq
+        from ... import output
+        w = None
+        for fn in self.pieces.pop(key):
+            pf = pq.ParquetFile(fn)
+            for g in range(pf.num_row_groups):
+                t = pf.read_row_group(g)
+                if w is None:
+                    w = pq.ParquetWriter(self.name(*key), t.schema,
+                                         compression=output.DEFAULT_COMPRESSION)
+                w.write_table(t)
+            os.remove(fn)
+        if w is not None:
+            w.close()
 
     def add(self, ctx, bb, copier=None):
         """Render this batch's rows of the rank's shards (GPU) and queue their writes. With a
@@ -455,12 +500,20 @@ class ShardWriters:
         for f in self.pending:
             f.result()
         self.pending = []
+        merged = set()
+        if self.pieces is not None:  # one writer open per pool thread at a time
+            merged = set(self.pieces)
+            for f in [self.pool.submit(self._merge, k) for k in list(self.pieces)]:
+                f.result()
+            os.rmdir(self.piece_dir)
         paths = []
         for s in sorted(self.shards):
             for b in range(self.nbins):
                 w = self.writers.pop((s, b), None)
                 if w is not None:
                     w.close()
+                elif (s, b) in merged:
+                    pass  # written from its pieces above
                 else:
                     pq.write_table(output.schema(self.masking, self.binned).empty_table(),
                                    self.name(s, b), compression=output.DEFAULT_COMPRESSION)
@@ -478,6 +531,17 @@ def num_samples_of_shards(shard_counts, binned):
             out['shard-{}.parquet{}'.format(s, '_{}'.format(b) if binned else '')] = int(
                 shard_counts[s, b])
     return out
+
+
+def _any_rank(flag, device):
+    """True when `flag` holds on any rank (all-reduce MAX: RCCL on a device tensor, gloo on the
+    host)."""
+    import torch
+    import torch.distributed as dist
+    dev = device if dist.get_backend() == 'nccl' else 'cpu'
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(t.item())
 
 
 def _empty_pairs(ctx, masking):
@@ -593,9 +657,16 @@ def main(args):
     import torch
     import torch.distributed as dist
     if world > 1:
-        torch.cuda.set_device(local)
-        if not dist.is_initialized():
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if os.environ.get('LDDL_SHARE_DEVICE') == '1':
+            # every rank on device 0, gloo collectives staged through host memory: a rehearsal
+            # of the multi-rank path on a one-GPU machine (never how a node is run)
+            torch.cuda.set_device(0)
+            if not dist.is_initialized():
+                dist.init_process_group('gloo')
+        else:
+            torch.cuda.set_device(local)
+            if not dist.is_initialized():
+                dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     from ...context import Context
     ctx = Context(vocab, do_lower_case=True)  # BertTokenizerFast default, SURVEY H5
     if args.sentence_splitter == 'gpu':
@@ -613,13 +684,26 @@ def main(args):
         bin_size = args.bin_size if binned else args.target_seq_length
         nbins = args.target_seq_length // bin_size
         stream = StreamBalancer(ctx, bin_size, nbins, num_shards=args.num_shards)
-        writers = ShardWriters(outdir, nbins, binned, args.masking, pool)
-        # every rank steps the balancer once per GPU batch of the rank with the most of them
-        n_steps = max(n_gpu_batches(args, blocks, r, world) for r in range(world))
-    k = 0
+        from ...balance import shard_owner
+        writers = ShardWriters(outdir, nbins, binned, args.masking, pool,
+                               n_local_shards=int((shard_owner(args.num_shards, world) == rank).sum()),
+                               max_open=args.max_open_files)
     copier = ThreadPoolExecutor(max_workers=1)  # device -> host copies of rendered batches
     inflight = []  # (copy future, write futures) of the batches not yet written
-    for batch, corpus in batches:
+    batch_it = iter(batches)
+    while True:
+        item = next(batch_it, None)
+        if stream is not None and world > 1:
+            # every rank steps the balancer until no rank has a batch left: the loop ends on the
+            # iterators themselves (one tiny all-reduce per step), never on a separate count
+            if not _any_rank(item is not None, ctx.device):
+                break
+            if item is None:  # this rank is out of batches: it still takes part in the exchange
+                writers.add(ctx, stream.step(_empty_pairs(ctx, args.masking)), copier)
+                continue
+        elif item is None:
+            break
+        batch, corpus = item
         timer('read')
         _trace('batch_ready', batch[0][0] if batch else -1)
         if stream is None:
@@ -641,7 +725,6 @@ def main(args):
             writers.add(ctx, bb, copier)
             del bb
             timer('render')
-            k += 1
         timer.mark()
     for f in pending:
         f.result()
@@ -652,8 +735,6 @@ def main(args):
             f.result()
     timer('write_wait')
     if stream is not None:
-        for _ in range(k, n_steps):
-            writers.add(ctx, stream.step(_empty_pairs(ctx, args.masking)), copier)
         n_files += len(writers.close())
         timer('write_wait')
         if rank == 0:
@@ -765,6 +846,10 @@ def attach_args(parser=None):
                              "the shards, RCCL exchange; one batch resident); 'reference' writes "
                              "the part files and runs balance_dask_output over them, the "
                              "reference's exact shard layout")
+    parser.add_argument('--max-open-files', type=int, default=None,
+                        help='--num-shards: most shard files kept open at once (default: as many '
+                             'as RLIMIT_NOFILE allows, raised to its hard limit); above it, each '
+                             'batch is written as a piece and the pieces are merged at the end')
     parser.add_argument('--write-threads', type=int, default=min(os.cpu_count() or 1, 16),
                         help='lddl_amd: parquet files written concurrently (threads). Default: '
                              'min(cpus, 16)')

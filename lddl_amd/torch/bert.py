@@ -8,16 +8,14 @@ tensor that call is a no-op).
 
 Process split (SURVEY §7 "Fork + HIP"): the reference runs the whole collate inside forked
 DataLoader workers. HIP must not be used there, so the workers only decode parquet record
-batches, run the shuffle buffer and pack each batch into flat numpy buffers (`_pack_batch`);
-the process that owns the GPU uploads the packed batch, runs the encode + masking kernels and
-then the user's extra collate_fn. Sample order, bin choice and epoch logic are the reference's.
+batches, run the shuffle buffer and pack each batch into flat numpy buffers (`packing.py`,
+which imports nothing of the native library); the process that owns the GPU uploads the packed
+batch through a reused pinned ring (`HostStager`), runs the encode + masking kernel and then
+the user's extra collate_fn. The HIP Context is created only after every bin's workers have
+started (`_LazyContext`). Sample order, bin choice and epoch logic are the reference's.
 """
-import ctypes
-import io
 import logging
 import os
-import re
-import time
 
 import numpy as np
 import torch
@@ -26,104 +24,75 @@ from .._native import lib, check
 from ..context import Context, _ptr, _stream
 from ..utils import get_all_bin_ids, get_all_parquets_under, get_file_paths_for_bin_id
 from .dataloader import Binned, DataLoader
-from .datasets import ParquetDataset
+from .datasets import ParquetDataset  # noqa: F401
 from .log import DatasetLogger
+from .packing import (BertPretrainDataset, PackedBatch, _canon, _decode_record_batch,  # noqa: F401
+                      _npy_u16, _ntok, _pack, _pack_batch)
 from .utils import get_node_rank, get_nproc_per_node, get_rank
 
 
-def _decode_record_batch(b):
-    """lddl/torch/bert.py:42-54: (A, B, is_random_next[, masked_lm_positions, labels])."""
-    b = b.to_pydict()
-    if 'masked_lm_positions' in b:
-        assert 'masked_lm_labels' in b
-    cols = tuple(b[k] for k in ('A', 'B', 'is_random_next', 'masked_lm_positions',
-                                'masked_lm_labels') if k in b)
-    for s in zip(*cols):
-        yield s
+class HostStager:
+    """A ring of reused pinned host buffers: all host arrays of one batch are packed into one
+    slot and go to the device in ONE asynchronous copy.
+
+    A copy from pageable memory would make the host wait for everything queued before it (the
+    consumer's training step); a fresh `.pin_memory()` per array and batch (round 3) called
+    hipHostMalloc whenever torch's host cache missed (86 calls, up to 143 ms each,
+    profiles/r03h_c5_hip_api.txt). A slot is reused once the event recorded after its copy has
+    completed, so at most `depth` batches are in flight and no pinned memory is allocated once
+    the slots have grown to the largest batch."""
+
+    ALIGN = 64
+
+    def __init__(self, depth=4):
+        self._bufs = [None] * depth
+        self._done = [None] * depth
+        self._i = 0
+        self.allocations = 0  # pinned (re)allocations so far: flat after warm-up
+
+    def stage(self, arrays, device):
+        """arrays: host numpy arrays -> device tensors (same dtypes and shapes), in order."""
+        arrays = [np.ascontiguousarray(a) for a in arrays]
+        offs, n = [], 0
+        for a in arrays:
+            offs.append(n)
+            n += -(-max(a.nbytes, 1) // self.ALIGN) * self.ALIGN
+        k = self._i % len(self._bufs)
+        self._i += 1
+        if self._done[k] is not None:
+            self._done[k].synchronize()  # this slot's previous copy has left the host buffer
+        buf = self._bufs[k]
+        if buf is None or buf.numel() < n:
+            cap = 1 << max(16, (n - 1).bit_length())
+            buf = self._bufs[k] = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+            self.allocations += 1
+        hv = buf.numpy()
+        for a, o in zip(arrays, offs):
+            hv[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
+        d = torch.empty(n, dtype=torch.uint8, device=device)
+        d.copy_(buf[:n], non_blocking=True)
+        ev = self._done[k] = torch.cuda.Event()
+        ev.record()
+        out = []
+        for a, o in zip(arrays, offs):
+            t = d[o:o + max(a.nbytes, 1)]
+            if a.nbytes == 0:  # a 1-byte placeholder keeps the pointer valid (never read)
+                out.append(t.view(torch.uint8)[:0])
+            else:
+                out.append(t.view(_TORCH_DTYPE[a.dtype.str[1:]]).view(a.shape))
+        return out
 
 
-class BertPretrainDataset(ParquetDataset):
-    def _decode_record_batch(self, b):
-        return _decode_record_batch(b)
+_TORCH_DTYPE = {'u1': torch.uint8, 'i1': torch.int8, 'i2': torch.int16, 'i4': torch.int32,
+                'i8': torch.int64, 'u2': torch.int16, 'f4': torch.float32}
+_DEFAULT_STAGER = {}
 
 
-def _npy_u16(b):
-    """Decode `serialize_np_array` bytes (lddl/utils.py:98-102, np.save of uint16[k])."""
-    if b[:6] == b'\x93NUMPY' and b[6] == 1:
-        hl = int.from_bytes(b[8:10], 'little')
-        hdr = b[10:10 + hl]
-        if b"'<u2'" in hdr and b'False' in hdr:
-            return np.frombuffer(b, np.uint16, offset=10 + hl)
-    return np.load(io.BytesIO(b)).astype(np.uint16)
-
-
-# whitespace of Python's str.split() (str.isspace()) that the kernel's ASCII splitter (space and
-# \t-\r, the bytes.split() set) does not treat as a separator
-_ODD_WS = re.compile('[\x1c-\x1f\x85\xa0\u1680\u2000-\u200a\u2028\u2029\u202f\u205f\u3000]')
-
-
-# UTF-8 byte sequences that every string holding such whitespace contains (\xe2\x80 also
-# starts common punctuation: those strings get the exact regex check)
-_ODD_WS_SEQ = (b'\x1c', b'\x1d', b'\x1e', b'\x1f', b'\xc2\x85', b'\xc2\xa0', b'\xe1\x9a\x80',
-               b'\xe2\x80', b'\xe2\x81\x9f', b'\xe3\x80\x80')
-
-
-def _canon(s):
-    """The string as the GPU splitter sees it, UTF-8 encoded: the reference splits with Python's
-    str.split() (Unicode whitespace, bert.py:80-81); the kernel splits on ASCII space / \\t-\\r.
-    Strings holding any other whitespace are re-joined with single spaces first (same tokens)."""
-    b = s.encode('utf-8')
-    if any(q in b for q in _ODD_WS_SEQ) and _ODD_WS.search(s):
-        return ' '.join(s.split()).encode('utf-8')
-    return b
-
-
-def _ntok(b):
-    """len(b.split()) (ASCII whitespace) without building the token list: a string of tokens
-    joined by single spaces (what the preprocessor writes) has count(' ') + 1."""
-    if not b:
-        return 0
-    if (b[0] == 32 or b[-1] == 32 or b'  ' in b or b'\t' in b or b'\n' in b or b'\r' in b or
-            b'\x0b' in b or b'\x0c' in b):
-        return len(b.split())
-    return b.count(b' ') + 1
-
-
-def _pack(batch, static):
-    """Flat host buffers of a batch: A and B strings back to back (separators canonicalised to
-    ASCII), their token counts (bytes.split() of the canonical strings = the reference's
-    str.split(), bert.py:80-81) and offsets and, with static masking, the labels strings and
-    decoded positions. Runs in the DataLoader workers, so the main process never has to wait for
-    the batch's shape."""
-    As = [_canon(s[0]) for s in batch]
-    Bs = [_canon(s[1]) for s in batch]
-    na = np.fromiter(map(_ntok, As), np.int32, len(batch))
-    nb = np.fromiter(map(_ntok, Bs), np.int32, len(batch))
-    la = np.fromiter(map(len, As), np.int64, len(batch))
-    lb = np.fromiter(map(len, Bs), np.int64, len(batch))
-    a_off = np.zeros(len(batch) + 1, np.int64)
-    a_off[1:] = np.cumsum(la)
-    b_off = a_off[-1] + np.concatenate([[0], np.cumsum(lb)])
-    parts = As + Bs
-    extra = None
-    if static:
-        labs = [_canon(s[4]) for s in batch]
-        lab_off = np.zeros(len(batch) + 1, np.int64)
-        lab_off[1:] = np.cumsum([len(x) for x in labs])
-        lab_off += b_off[-1]
-        pos = [_npy_u16(s[3]) for s in batch]
-        pos_off = np.zeros(len(batch) + 1, np.int64)
-        pos_off[1:] = np.cumsum([len(p) for p in pos])
-        parts += labs
-        extra = (lab_off, np.concatenate(pos) if pos else np.zeros(0, np.uint16), pos_off)
-    blob = np.frombuffer(bytearray(b''.join(parts)), np.uint8)
-    return blob, a_off, b_off, na, nb, extra
-
-
-def _dev(a, device):
-    """Host array -> device through a pinned staging copy: a copy from pageable memory would
-    make the host wait for everything queued before it (the consumer's training step)."""
-    return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(device, non_blocking=True)
+def _stager_for(device):
+    s = _DEFAULT_STAGER.get(str(device))
+    if s is None:
+        s = _DEFAULT_STAGER[str(device)] = HostStager()
+    return s
 
 
 def _to_encoded_inputs(batch, tokenizer, sequence_length_alignment=8, ignore_index=-1):
@@ -162,39 +131,29 @@ def _mask_tokens(inputs, special_tokens_mask=None, tokenizer=None, mlm_probabili
     return inputs, labels
 
 
-class PackedBatch:
-    """A collated batch as flat host buffers (built in a DataLoader worker, picklable)."""
-
-    def __init__(self, batch):
-        t0 = time.perf_counter()
-        self.static = len(batch[0]) > 3
-        self.blob, self.a_off, self.b_off, self.na, self.nb, self.extra = _pack(batch, self.static)
-        self.nsl = np.asarray([s[2] for s in batch], np.int64)
-        self.pack_s = time.perf_counter() - t0  # host time of the pack (in the worker)
-
-    def __len__(self):
-        return len(self.nsl)
-
-
-def _pack_batch(batch):
-    return PackedBatch(batch)
-
-
-def encode_packed(pk, ctx, sequence_length_alignment=8, ignore_index=-1, mask=None, events=None):
+def encode_packed(pk, ctx, sequence_length_alignment=8, ignore_index=-1, mask=None, events=None,
+                  stager=None):
     """`_to_encoded_inputs` on an already packed batch (main process, GPU).
 
     mask = (mlm_probability, seed, counter) on a dynamic-masking batch runs `_mask_tokens` fused
     into the same kernel (lddl_collate_encode_masked) and returns `labels` instead of
     `special_tokens_mask`. events: optional pair of torch.cuda.Event recorded around the
-    encode kernel (timing)."""
+    encode kernel (timing). stager: the HostStager whose pinned ring carries the batch to the
+    device (default: one per device)."""
     dev = ctx.device
     B = len(pk)
     seq = int((pk.na + pk.nb).max()) + 3  # the batch's shape (bert.py:91-96), known on the host
     L = ((seq - 1) // sequence_length_alignment + 1) * sequence_length_alignment
-    d_blob = _dev(pk.blob, dev) if len(pk.blob) else torch.zeros(1, dtype=torch.uint8, device=dev)
-    d_off = _dev(np.concatenate([pk.a_off, pk.b_off]), dev)
+    host = [pk.blob, np.concatenate([pk.a_off, pk.b_off]), np.concatenate([pk.na, pk.nb]), pk.nsl]
+    if pk.static:
+        lab_off, pos, pos_off = pk.extra
+        if len(pos) and int(pos.max()) >= L:  # the reference's labels[i][positions] raises
+            raise IndexError('masked_lm_positions holds {} >= sequence length {}'.format(
+                int(pos.max()), L))
+        host += [lab_off, pos_off, pos.view(np.int16)]
+    staged = (stager or _stager_for(dev)).stage(host, dev)  # one H2D copy for the whole batch
+    d_blob, d_off, d_cnt, d_nsl = staged[:4]
     d_a, d_b = d_off[:B + 1], d_off[B + 1:]
-    d_cnt = _dev(np.concatenate([pk.na, pk.nb]), dev)
     d_na, d_nb = d_cnt[:B], d_cnt[B:]
     out = {k: torch.empty(B, L, dtype=torch.long, device=dev)
            for k in ('input_ids', 'token_type_ids', 'attention_mask')}
@@ -209,18 +168,12 @@ def encode_packed(pk, ctx, sequence_length_alignment=8, ignore_index=-1, mask=No
             _ptr(labels), float(p), ignore_index, len(ctx), seed, counter))
         if events is not None:
             events[1].record()
-        out['next_sentence_labels'] = _dev(pk.nsl, dev)
+        out['next_sentence_labels'] = d_nsl
         out['labels'] = labels
         return out
     stm = labels = d_lab_off = d_pos = d_pos_off = None
     if pk.static:
-        lab_off, pos, pos_off = pk.extra
-        if len(pos) and int(pos.max()) >= L:  # the reference's labels[i][positions] raises
-            raise IndexError('masked_lm_positions holds {} >= sequence length {}'.format(
-                int(pos.max()), L))
-        d_lab_off, d_pos_off = _dev(lab_off, dev), _dev(pos_off, dev)
-        d_pos = _dev(pos.view(np.int16), dev) if len(pos) else torch.zeros(1, dtype=torch.int16,
-                                                                           device=dev)
+        d_lab_off, d_pos_off, d_pos = staged[4:]
         labels = torch.empty(B, L, dtype=torch.long, device=dev)
     else:
         stm = torch.empty(B, L, dtype=torch.long, device=dev)
@@ -233,7 +186,7 @@ def encode_packed(pk, ctx, sequence_length_alignment=8, ignore_index=-1, mask=No
                                   _ptr(d_pos), _ptr(d_pos_off), _ptr(labels), ignore_index))
     if events is not None:
         events[1].record()
-    out['next_sentence_labels'] = _dev(pk.nsl, dev)
+    out['next_sentence_labels'] = d_nsl
     if pk.static:
         out['labels'] = labels
     else:
@@ -241,13 +194,29 @@ def encode_packed(pk, ctx, sequence_length_alignment=8, ignore_index=-1, mask=No
     return out
 
 
+class _LazyContext:
+    """The loader's HIP Context, created on first use: after the DataLoader workers of every bin
+    have been started, so no worker is ever forked from a process holding this library's HIP
+    state."""
+
+    def __init__(self, vocab_file, do_lower_case):
+        self._args = (vocab_file, do_lower_case)
+        self.ctx = None
+
+    def get(self):
+        if self.ctx is None:
+            self.ctx = Context(self._args[0], do_lower_case=self._args[1])
+        return self.ctx
+
+
 class GPUCollateLoader:
     """Iterates a torch DataLoader of PackedBatch and finishes the collate on the GPU."""
 
     def __init__(self, loader, ctx, mlm_probability, ignore_index, sequence_length_alignment,
-                 extra_collate, seed, start_epoch=0):
+                 extra_collate, seed, start_epoch=0, stager=None):
         self._loader = loader
-        self._ctx = ctx
+        self._lazy = ctx if isinstance(ctx, _LazyContext) else None
+        self._ctx_obj = None if self._lazy is not None else ctx
         self._mlm = mlm_probability
         self._ignore = ignore_index
         self._align = sequence_length_alignment
@@ -255,7 +224,12 @@ class GPUCollateLoader:
         self._seed = seed            # Philox key: distinct per (base_seed, rank, bin)
         self._epoch = start_epoch    # counter = epoch << 32 | batch: no stream repeats across
         self._counter = start_epoch << 32  # epochs, and a resumed run continues, not replays
+        self._stager = stager
         self.stats = None  # dict(pack_s=[], blob_bytes=[], events=[], slots=[]): record timings
+
+    @property
+    def _ctx(self):
+        return self._lazy.get() if self._lazy is not None else self._ctx_obj
 
     @property
     def dataset(self):
@@ -268,9 +242,16 @@ class GPUCollateLoader:
         return getattr(self._loader, k)
 
     def __iter__(self):
+        """Starts (or, persistent, resets) the DataLoader's workers NOW, before the first batch
+        is asked for: `Binned` creates every bin's iterator before it draws from any, so all
+        workers exist before the Context does."""
         self._counter = self._epoch << 32
         self._epoch += 1
-        for pk in self._loader:
+        return self._batches(iter(self._loader))
+
+    def _batches(self, it):
+        for pk in it:
+            ctx = self._ctx
             ev = None
             if self.stats is not None:
                 self.stats['pack_s'].append(pk.pack_s)
@@ -279,8 +260,9 @@ class GPUCollateLoader:
             # the batch shape is known on the host (counted in the worker): nothing here waits
             # for the GPU, the collate kernel is queued behind the consumer's training step
             with torch.no_grad():  # dynamic masking: collate + _mask_tokens in one kernel
-                enc = encode_packed(pk, self._ctx, self._align, self._ignore,
-                                    mask=(self._mlm, self._seed, self._counter), events=ev)
+                enc = encode_packed(pk, ctx, self._align, self._ignore,
+                                    mask=(self._mlm, self._seed, self._counter), events=ev,
+                                    stager=self._stager)
             if not pk.static:
                 self._counter += 1
             if self.stats is not None:
@@ -342,9 +324,10 @@ def get_bert_pretrain_data_loader(path, local_rank=0, shuffle_buffer_size=16384,
                           shuffle_buffer_warmup_factor=shuffle_buffer_warmup_factor,
                           base_seed=base_seed, logger=logger, start_epoch=start_epoch)
     extra_collate = data_loader_kwargs.get('collate_fn', lambda x: x)
-    ctx = None
-    if not return_raw_samples:
-        ctx = Context(vocab_file, do_lower_case=tokenizer_kwargs.get('do_lower_case', True))
+    ctx = stager = None
+    if not return_raw_samples:  # the Context is created after the workers start (_LazyContext)
+        ctx = _LazyContext(vocab_file, tokenizer_kwargs.get('do_lower_case', True))
+        stager = HostStager()
         data_loader_kwargs['collate_fn'] = _pack_batch
     data_loader_kwargs['persistent_workers'] = True
 
@@ -354,7 +337,7 @@ def get_bert_pretrain_data_loader(path, local_rank=0, shuffle_buffer_size=16384,
             return dl
         return GPUCollateLoader(dl, ctx, mlm_probability, ignore_index,
                                 sequence_length_alignment, extra_collate,
-                                mask_seed(base_seed, get_rank(), bin_id), start_epoch)
+                                mask_seed(base_seed, get_rank(), bin_id), start_epoch, stager)
 
     paths = get_all_parquets_under(path)
     bin_ids = get_all_bin_ids(paths)

@@ -73,8 +73,12 @@ class ShuffleBuffer:
             remaining -= 1
 
 
+def _identity(x):
+    return x
+
+
 class ParquetDataset(IterableDataset):
-    def __init__(self, file_paths, transform=lambda x: x, local_rank=0, shuffle_buffer_size=16384,
+    def __init__(self, file_paths, transform=_identity, local_rank=0, shuffle_buffer_size=16384,
                  shuffle_buffer_warmup_factor=16, base_seed=12345, logger=None, start_epoch=0):
         super().__init__()
         self._transform = transform

@@ -113,43 +113,61 @@ def host_rows(h):
     return out
 
 
-def check_stream(inputs, outputs, bin_size, nbins, num_shards):
+def check_stream(inputs, outputs, bin_size, nbins, num_shards, moved=None):
     """inputs[t][r]: rank r's to_host() table of batch t; outputs[t][r]: (host dict of the
-    materialised output table, bin_off, shards, shard_counts). Checks the deal contract: the
-    global order of bin b is batch-major, then rank-major, then each rank's stable bin order;
-    global row g of bin b belongs to shard g % S, shard s to rank s * W // S; each rank's output
-    of a batch is bin-major, then its shards ascending, rows in global order; and after every
-    batch each shard holds N or N+1 rows of every bin (the reference's Progress targets).
+    materialised output table, bin_off, shards, shard_counts); moved[t][r] (optional): the rows
+    rank r received. Checks the balance contract, restated by brute force:
+
+      * after every batch, shard s holds n // S (+1 for the first n % S shards) rows of a bin that
+        has seen n rows (the reference's Progress targets): N or N+1;
+      * shard s belongs to rank s * W // S; a rank's quota of bin b is its shards' share of the
+        batch; each rank keeps the first min(count, quota) of its bin-b rows (stable bin order),
+        the surplus tails of all ranks, in rank order, form a pool that the ranks below quota
+        take from in rank order;
+      * a rank's bin-b output is [kept | taken], dealt in consecutive runs to its shards in
+        ascending order; the rows moved are exactly the pool (the imbalance, nothing else).
     Returns the cumulative int64[S, B] shard counts."""
     W, S = len(inputs[0]), num_shards
     owner = shard_owner(S, W)
     prior = np.zeros(nbins, np.int64)
     cum = np.zeros((S, nbins), np.int64)
     for t in range(len(inputs)):
-        glob = [[] for _ in range(nbins)]
+        per_rank = []  # [r][b]: rank r's rows of bin b in stable order
         for h in inputs[t]:
             nt = np.diff(h['tok_off']) + 3
             bins = np.minimum((nt - 1) // bin_size, nbins - 1)
             rows = host_rows(h)
+            lst = [[] for _ in range(nbins)]
             for q in np.argsort(bins, kind='stable'):
-                glob[bins[q]].append(rows[q])
-        per_shard = [[[] for _ in range(nbins)] for _ in range(S)]
+                lst[bins[q]].append(rows[q])
+            per_rank.append(lst)
+        total = np.array([sum(len(per_rank[r][b]) for r in range(W)) for b in range(nbins)])
+        after = shard_targets((prior + total)[None, :], S)
+        shard_n = after - shard_targets(prior[None, :], S)
+        prior += total
+        expect = [[None] * nbins for _ in range(W)]
+        n_moved = np.zeros(W, np.int64)
         for b in range(nbins):
-            for i, row in enumerate(glob[b]):
-                per_shard[(prior[b] + i) % S][b].append(row)
-            prior[b] += len(glob[b])
+            quota = [int(shard_n[owner == r, b].sum()) for r in range(W)]
+            pool = [(r, x) for r in range(W) for x in per_rank[r][b][quota[r]:]]
+            for r in range(W):
+                kept = per_rank[r][b][:quota[r]]
+                take, pool = pool[:quota[r] - len(kept)], pool[quota[r] - len(kept):]
+                n_moved[r] += len(take)
+                assert all(src != r for src, _ in take)
+                expect[r][b] = kept + [x for _, x in take]
+            assert not pool
         for k, (h, bin_off, shards, shard_counts) in enumerate(outputs[t]):
             assert list(shards) == [s for s in range(S) if owner[s] == k]
             rows = host_rows(h)
             assert len(rows) == bin_off[-1]
             for b in range(nbins):
-                exp = [x for s in shards for x in per_shard[s][b]]
-                assert rows[bin_off[b]:bin_off[b + 1]] == exp, \
-                    'batch {} rank {} bin {} differs from the dealt global order'.format(t, k, b)
+                assert rows[bin_off[b]:bin_off[b + 1]] == expect[k][b], \
+                    'batch {} rank {} bin {} differs from the balance contract'.format(t, k, b)
                 for m, s in enumerate(shards):
-                    assert shard_counts[m][b] == len(per_shard[s][b])
-        for s in range(S):
-            for b in range(nbins):
-                cum[s, b] += len(per_shard[s][b])
-        np.testing.assert_array_equal(cum, shard_targets(prior[None, :], S))
+                    assert shard_counts[m][b] == shard_n[s, b]
+            if moved is not None:
+                assert moved[t][k] == n_moved[k]
+        cum += shard_n
+        np.testing.assert_array_equal(cum, after)
     return cum

@@ -1,6 +1,7 @@
 """Streaming load balance across ranks (lddl_amd/balance.py).
 
-* the deal plan (pure host): `deal_runs` against a brute-force deal, N / N+1 after every prefix;
+* the plan (pure host): `surplus_moves` against a brute-force two-list fill (only the imbalance
+  moves), N / N+1 after every prefix of batches;
 * `stream_virtual` (W ranks in one process, several batches) and `StreamBalancer` under gloo at
   world size 2 on the CPU, both running the product's plan / pack / regroup code with CPU
   data-movement primitives (tests/balance_util.py);
@@ -16,36 +17,52 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from balance_util import TorchCpuOps, check_stream, random_table
-from lddl_amd.balance import (StreamBalancer, balance, batch_start, deal_runs, shard_targets,
-                              stream_virtual)
+from lddl_amd.balance import (StreamBalancer, balance, batch_shard_counts, rank_quota,
+                              shard_targets, stream_virtual, surplus_moves)
 
 
-def test_deal_runs_brute_force():
+def test_surplus_moves_brute_force():
+    """Surplus ranks (rank order) fill deficit ranks (rank order); the moved total is exactly the
+    imbalance sum(max(0, c - q)) and every rank ends at its quota."""
     rng = np.random.default_rng(0)
-    for _ in range(200):
-        S = int(rng.integers(1, 20))
-        g0 = int(rng.integers(0, 100))
-        c = int(rng.integers(0, 60))
-        first, n = deal_runs(np.array([g0]), np.array([c]), S)
-        for s in range(S):
-            rows = [i for i in range(c) if (g0 + i) % S == s]
-            assert n[0, s] == len(rows)
-            if rows:
-                assert rows == list(range(first[0, s], c, S))
+    for _ in range(300):
+        W = int(rng.integers(1, 9))
+        B = int(rng.integers(1, 4))
+        counts = rng.integers(0, 30, (W, B))
+        q = np.zeros((W, B), np.int64)
+        for b in range(B):  # a random quota with the same total
+            q[:, b] = np.bincount(rng.integers(0, W, counts[:, b].sum()), minlength=W)
+        m, off = surplus_moves(counts, q)
+        for b in range(B):
+            pool = [(j, i) for j in range(W) for i in range(max(0, counts[j, b] - q[j, b]))]
+            exp = np.zeros((W, W), np.int64)
+            for k in range(W):
+                need = max(0, q[k, b] - counts[k, b])
+                take, pool = pool[:need], pool[need:]
+                for j, i in take:
+                    exp[j, k] += 1
+                    if exp[j, k] == 1:
+                        assert off[j, k, b] == i
+            np.testing.assert_array_equal(m[:, :, b], exp)
+        assert m.sum() == np.maximum(counts - q, 0).sum()
+        np.testing.assert_array_equal(np.minimum(counts, q) + m.sum(0), q)
 
 
-def test_deal_prefixes_balanced():
-    """Any sequence of batches of any sizes leaves every shard within one row (N or N+1)."""
+def test_batch_prefixes_balanced():
+    """Any sequence of batches of any sizes leaves every shard within one row (N or N+1), and a
+    rank's quota is the sum of its shards'."""
     rng = np.random.default_rng(1)
     for W, S, B in ((1, 1, 3), (2, 5, 4), (4, 4, 8), (8, 24, 64), (3, 2, 5)):
         prior = np.zeros(B, np.int64)
         tot = np.zeros((S, B), np.int64)
         for _ in range(6):
             counts = rng.integers(0, 40, (W, B))
-            _, n = deal_runs(batch_start(prior, counts), counts, S)
-            tot += n.sum(0).T
+            n = batch_shard_counts(prior, counts.sum(0), S)
+            tot += n
             prior += counts.sum(0)
             np.testing.assert_array_equal(tot, shard_targets(prior[None, :], S))
+            q = rank_quota(n, W)
+            np.testing.assert_array_equal(q.sum(0), counts.sum(0))
 
 
 def _to_host_out(bb, ops):
@@ -63,7 +80,8 @@ def test_stream_virtual_cpu(W, S, masking, T):
                 for r in range(W)] for t in range(T)]
     outs = stream_virtual(ops, batches, 8, 8, num_shards=S)
     check_stream([[pb.to_host() for pb in pbs] for pbs in batches],
-                 [[_to_host_out(o, ops) for o in os_] for os_ in outs], 8, 8, S)
+                 [[_to_host_out(o, ops) for o in os_] for os_ in outs], 8, 8, S,
+                 moved=[[o.moved_rows for o in os_] for os_ in outs])
     if W == 1:
         assert all(o[0].moved_rows == 0 and o[0].rows is not None for o in outs)  # no copy
 
@@ -99,10 +117,12 @@ def test_stream_gloo_world2(S):
         res = dict(out)
     T = len(res[0][0])
     cum = check_stream([[res[r][0][t][0] for r in range(2)] for t in range(T)],
-                       [[res[r][0][t][1] for r in range(2)] for t in range(T)], 8, 8, S)
+                       [[res[r][0][t][1] for r in range(2)] for t in range(T)], 8, 8, S,
+                       moved=[[res[r][0][t][2] for r in range(2)] for t in range(T)])
     for r in range(2):  # every rank's running layout is the same, and the one checked
         np.testing.assert_array_equal(res[r][1], cum)
-    assert res[1][0][0][2] > 0 and res[0][0][0][2] > 0  # rows crossed in both directions
+    # rows crossed in both directions (batch 0: rank 0 -> 1, batch 1: rank 1 -> 0)
+    assert res[1][0][0][2] > 0 and res[0][0][1][2] > 0
 
 
 # ---- GPU ------------------------------------------------------------------------------------
@@ -143,7 +163,7 @@ def _split_rows(pb, cuts):
                                    (8, 24, 1), (3, 5, 3)])
 def test_stream_virtual_gpu(gpu_tables, W, S, T):
     """W virtual ranks x T batches on one GPU, HIP kernels: skewed row splits (rows must move),
-    checked against the deal contract; bin totals against the oracle's stable bin order."""
+    checked against the balance contract (moved rows == the imbalance); bin totals against the oracle's stable bin order."""
     from oracle import oracle as O
     from lddl_amd.balance import HipOps
     ctx, pb = gpu_tables
@@ -155,7 +175,8 @@ def test_stream_virtual_gpu(gpu_tables, W, S, T):
     ops = HipOps(ctx)
     outs = stream_virtual(ops, batches, 8, 64, num_shards=S)
     check_stream([[p.to_host() for p in pbs] for pbs in batches],
-                 [[_to_host_out(o, ops) for o in os_] for os_ in outs], 8, 64, S)
+                 [[_to_host_out(o, ops) for o in os_] for os_ in outs], 8, 64, S,
+                 moved=[[o.moved_rows for o in os_] for os_ in outs])
     nt = np.diff(pb.tok_off.cpu().numpy()) + 3
     eb, eo, ec = O.bin_samples(nt.astype(np.int32), 8, 64)
     assert sum(o.n_rows for os_ in outs for o in os_) == n
@@ -181,3 +202,22 @@ def test_balance_world1_no_copy(gpu_tables):
     np.testing.assert_array_equal(np.diff(bb.bin_off), ec)
     np.testing.assert_array_equal(bb.bin_ids(), eb[eo])
     assert bb.n_tokens == int(pb.tokens.numel())
+
+
+@pytest.mark.gpu
+def test_stream_virtual_gpu_balanced_moves_nothing(gpu_tables):
+    """W = 8 virtual ranks dealt the rows round-robin (every rank within one row of every bin's
+    share): only rounding remainders move, at most W - 1 rows per bin, where the round-robin deal
+    of round 3 moved (W - 1) / W of all rows."""
+    import torch as _t
+    from lddl_amd.balance import HipOps, _gather_table
+    ctx, pb = gpu_tables
+    W, nb = 8, 64
+    ops = HipOps(ctx)
+    parts = [_gather_table(ops, pb, None, _t.arange(r, pb.n_pairs, W, device=pb.tok_off.device))
+             for r in range(W)]
+    outs = stream_virtual(ops, [parts], 8, nb, num_shards=W)
+    moved = sum(o.moved_rows for o in outs[0])
+    check_stream([[p.to_host() for p in parts]], [[_to_host_out(o, ops) for o in outs[0]]], 8, nb,
+                 W, moved=[[o.moved_rows for o in outs[0]]])
+    assert moved <= (W - 1) * nb and moved < 0.05 * pb.n_pairs

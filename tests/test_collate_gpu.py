@@ -216,3 +216,25 @@ def test_fused_collate_mask_equals_two_pass(g, ctx_c, align):
     for k in ('token_type_ids', 'attention_mask', 'next_sentence_labels'):
         assert torch.equal(one[k], two[k])
     assert int((lab != -1).sum()) > 0
+
+
+@pytest.mark.gpu
+def test_host_stager_round_trip_and_reuse():
+    """HostStager: one H2D copy per batch through a reused pinned ring; every dtype and shape
+    (empty arrays included) arrives intact, and no pinned memory is allocated once the ring's
+    slots have grown."""
+    import torch
+    from lddl_amd.torch.bert import HostStager
+    st = HostStager(depth=3)
+    rng = np.random.default_rng(5)
+    dev = torch.device('cuda', 0)
+    for it in range(40):
+        n = 1000 + (it % 7) * 300
+        arrs = [rng.integers(0, 255, n * 3, dtype=np.uint8), rng.integers(-2**40, 2**40, n + 1),
+                rng.integers(-2**30, 2**30, 2 * n, dtype=np.int32), np.zeros(0, np.uint8),
+                rng.integers(0, 2**15, 17, dtype=np.int16)]
+        got = st.stage(arrs, dev)
+        for a, g in zip(arrs, got):
+            assert g.is_cuda and g.numel() == a.size
+            np.testing.assert_array_equal(g.cpu().numpy().view(a.dtype), a)
+    assert st.allocations <= 3 * 2

@@ -287,3 +287,38 @@ def test_native_reader_rejects_malformed_utf8(tmp_path):
         blocks = R.plan_blocks(str(p), None, 0.01, 3)
         with pytest.raises(UnicodeDecodeError):
             R.read_groups_native([blocks], [1])
+
+
+def test_shard_writers_piece_mode_same_files(tmp_path):
+    """ShardWriters with fewer open files allowed than (shard, bin) files: per-batch pieces
+    merged at close give the same files, row group for row group, as open writers; empty
+    (shard, bin) pairs still get their empty file."""
+    from concurrent.futures import ThreadPoolExecutor
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from lddl_amd.dask.bert.pretrain import ShardWriters
+    out = {}
+    for mode, max_open in (('open', None), ('pieces', 2)):
+        d = tmp_path / mode
+        d.mkdir()
+        with ThreadPoolExecutor(4) as pool:
+            w = ShardWriters(str(d), 2, True, True, pool, n_local_shards=3, max_open=max_open)
+            assert (w.pieces is not None) == (mode == 'pieces')
+            w.shards.update([0, 1, 2])
+            for t in range(3):  # batches
+                for s in range(3):
+                    for b in range(2):
+                        if (s, b) == (2, 1):
+                            continue  # never receives rows
+                        n = 1 + (t + s + b) % 3
+                        w._write((s, b), pa.table({
+                            'A': pa.array(['a{}{}{}{}'.format(t, s, b, i) for i in range(n)]),
+                            'num_tokens': pa.array(np.arange(n, dtype=np.uint16))}))
+            assert len(w.close()) == 6
+        out[mode] = {fn: pq.read_table(d / fn) for fn in os.listdir(d)}
+        assert not any(x.startswith('.lddl_amd_pieces') for x in os.listdir(d))
+    assert set(out['open']) == set(out['pieces']) and len(out['open']) == 6
+    for fn in out['open']:
+        assert out['open'][fn].equals(out['pieces'][fn]), fn
+        assert pq.ParquetFile(tmp_path / 'open' / fn).num_row_groups == \
+            pq.ParquetFile(tmp_path / 'pieces' / fn).num_row_groups

@@ -19,7 +19,7 @@ class _Pk:
 def _counters(monkeypatch, start_epoch, epochs, n_batches=3):
     seen = []
 
-    def fake_encode(pk, ctx, align, ignore, mask=None, events=None):
+    def fake_encode(pk, ctx, align, ignore, mask=None, events=None, stager=None):
         seen.append(mask)
         return {'input_ids': types.SimpleNamespace(numel=lambda: 0)}
 

@@ -287,10 +287,23 @@ def test_pretrain_cli_txt_output(tmp_path, binned):
 
 @pytest.mark.parametrize('binned,masking', [(True, True), (False, False)])
 def test_pretrain_cli_num_shards_balanced(tmp_path, binned, masking):
-    """--num-shards (stream plan): shard s of bin b holds exactly the rows g = s (mod S) of bin
-    b's global order — the part.* rows of the same run, partitions in order — in that order, N or
-    N+1 per shard, with .num_samples.json; the files are identical when the corpus streams
-    through the GPU in four batches; then get_bert_pretrain_data_loader consumes them."""
+    """--num-shards (stream plan, world size 1): per GPU batch, bin b's rows (the part.* rows of
+    the batch's partitions, in order) are cut into consecutive runs, shard s taking
+    batch_shard_counts' share (N or N+1 per shard after every batch), with .num_samples.json;
+    checked for one batch and for one batch per partition (`--gpu-batch-bytes 1`); then
+    get_bert_pretrain_data_loader consumes them."""
+    from lddl_amd.balance import batch_shard_counts
+
+    def dealt(batches, S):  # batches: bin b's rows per GPU batch -> rows per shard
+        out, prior = [[] for _ in range(S)], 0
+        for rows in batches:
+            n = batch_shard_counts([prior], [len(rows)], S)[:, 0]
+            o = 0
+            for k in range(S):
+                out[k] += rows[o:o + n[k]]
+                o += n[k]
+            prior += len(rows)
+        return out
     import logging
     from lddl_amd.torch import get_bert_pretrain_data_loader
     from lddl_amd.dask.bert import pretrain as P
@@ -305,19 +318,24 @@ def test_pretrain_cli_num_shards_balanced(tmp_path, binned, masking):
         ['--sink', 'x', '--gpu-batch-bytes', '1', '--shuffle-group-bytes', '1']),
         P.plan_partitions(args))) == n_part  # one batch per partition in shards_b
     ns = json.loads((tmp_path / 'shards' / '.num_samples.json').read_text())
-    assert ns == json.loads((tmp_path / 'shards_b' / '.num_samples.json').read_text())
+    ns_b = json.loads((tmp_path / 'shards_b' / '.num_samples.json').read_text())
+    assert ns == ns_b  # the same counts per shard (N / N+1 after every batch)
     assert len(ns) == 4 * nb
     for b in range(nb):
         sfx = '_{}'.format(b) if binned else ''
-        glob = [r for p in range(n_part)
-                for r in pq.read_table(tmp_path / 'parts' / 'part.{}.parquet{}'.format(p, sfx)).to_pylist()]
+        per_part = [pq.read_table(tmp_path / 'parts' / 'part.{}.parquet{}'.format(p, sfx)).to_pylist()
+                    for p in range(n_part)]
+        one = dealt([[r for rows in per_part for r in rows]], 4)
+        each = dealt(per_part, 4)
         counts = []
         for s in range(4):
             fn = 'shard-{}.parquet{}'.format(s, sfx)
             t = pq.read_table(tmp_path / 'shards' / fn)
             assert ns[fn] == t.num_rows
-            assert t.to_pylist() == glob[s::4]
-            assert pq.read_table(tmp_path / 'shards_b' / fn).to_pylist() == glob[s::4]
+            assert t.to_pylist() == one[s]
+            tb = pq.read_table(tmp_path / 'shards_b' / fn)
+            assert tb.to_pylist() == each[s]
+            assert ns_b[fn] == tb.num_rows
             counts.append(t.num_rows)
         assert max(counts) - min(counts) <= 1
     dl = get_bert_pretrain_data_loader(
@@ -347,3 +365,71 @@ def test_pretrain_cli_num_shards_reference_plan(tmp_path):
         if '.parquet' in n:
             assert pq.read_table(got / n).to_pylist() == pq.read_table(ref / n).to_pylist()
     assert (got / '.num_samples.json').read_text() == (ref / '.num_samples.json').read_text()
+
+
+def test_pretrain_cli_num_shards_piece_mode(tmp_path):
+    """--max-open-files below the (shard, bin) file count: each batch is written as a piece and
+    the pieces are merged at close — the same files as with every writer open (the
+    reference example's 4096 shards x 8 bins exceed the usual 1024-descriptor soft limit)."""
+    extra = ['--bin-size', '32', '--shuffle-group-bytes', '1', '--gpu-batch-bytes', '1',
+             '--num-shards', '4']
+    _cli(tmp_path, tmp_path / 'open', extra)
+    _cli(tmp_path, tmp_path / 'pieces', extra + ['--max-open-files', '3'])
+    names = sorted(x for x in os.listdir(tmp_path / 'open') if x.startswith('shard-'))
+    assert len(names) == 16
+    assert sorted(x for x in os.listdir(tmp_path / 'pieces') if not x.startswith('.')) == \
+        sorted(x for x in os.listdir(tmp_path / 'open') if not x.startswith('.'))
+    for fn in names:
+        a = pq.read_table(tmp_path / 'open' / fn)
+        b = pq.read_table(tmp_path / 'pieces' / fn)
+        assert a.equals(b), fn
+        assert pq.ParquetFile(tmp_path / 'pieces' / fn).num_row_groups == \
+            pq.ParquetFile(tmp_path / 'open' / fn).num_row_groups
+
+
+def _cli_world2(tmp_path, sink, extra, env_extra=None):
+    import socket
+    import subprocess
+    import sys
+    src = tmp_path / 'source'
+    if not src.exists():
+        _write_source(str(src))
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, LDDL_SHARE_DEVICE='1', **(env_extra or {}))
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env['PYTHONPATH'] = repo + os.pathsep + env.get('PYTHONPATH', '')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), '-m',
+           'lddl_amd.dask.bert.pretrain', '--schedule', 'local', '--wikipedia', str(src),
+           '--sink', str(sink), '--target-seq-length', '128', '--num-blocks', '3', '--seed', '7',
+           '--vocab-file', VOCAB_UNCASED, '--local-n-workers', '1', '--duplicate-factor', '2',
+           '--masking'] + extra
+    r = subprocess.run(cmd, env=env, cwd=repo, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_pretrain_cli_num_shards_world2_unequal_batches(tmp_path):
+    """Two ranks (sharing the one GPU, gloo collectives staged through host memory) with
+    different numbers of GPU batches (3 partitions, one batch each): the collective balance loop
+    ends on the batch iterators themselves, the rank that runs out keeps taking part with empty
+    batches, and the shards hold exactly the rows of the same run's part files, N or N+1 per
+    shard and bin (termination no longer depends on a second count of the batches)."""
+    extra = ['--bin-size', '32', '--shuffle-group-bytes', '1', '--gpu-batch-bytes', '1']
+    _cli_world2(tmp_path, tmp_path / 'parts', extra)
+    _cli_world2(tmp_path, tmp_path / 'shards', extra + ['--num-shards', '3'])
+    n_part = len([x for x in os.listdir(tmp_path / 'parts') if x.endswith('.parquet_0')])
+    assert n_part == 3
+    ns = json.loads((tmp_path / 'shards' / '.num_samples.json').read_text())
+    for b in range(4):
+        parts = sorted(str(r) for p in range(n_part) for r in pq.read_table(
+            tmp_path / 'parts' / 'part.{}.parquet_{}'.format(p, b)).to_pylist())
+        shards, counts = [], []
+        for s in range(3):
+            t = pq.read_table(tmp_path / 'shards' / 'shard-{}.parquet_{}'.format(s, b))
+            assert ns['shard-{}.parquet_{}'.format(s, b)] == t.num_rows
+            shards += [str(r) for r in t.to_pylist()]
+            counts.append(t.num_rows)
+        assert sorted(shards) == parts
+        assert max(counts) - min(counts) <= 1
