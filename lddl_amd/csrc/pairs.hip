@@ -826,10 +826,12 @@ __global__ void __launch_bounds__(64, 6) plan_replay_kernel(PlanArgs A) {
 // walk and every pair's masking runs in its own lane. A stream is keyed by
 // (native_seed, part_seed[p]) and counted by the unit's or pair's index inside its partition, so
 // a partition's output does not depend on how partitions are batched or sharded.
-// Distributions are those of the reference: randint / _randbelow by the same bit-length
-// rejection, random() < p on the same 53-bit integer, each truncation side a fair coin, the
-// masked set a uniform num_to_predict-subset of the candidates (Floyd's algorithm: the shuffled
-// prefix of pretrain.py:197-207 is a uniform subset), 80/10/10 decisions per masked token.
+// Distributions are those of the reference: in the walk, randint / _randbelow by the same
+// bit-length rejection and random() < p on the same 53-bit integer, each truncation side a fair
+// coin; in the masking, the masked set a uniform num_to_predict-subset of the candidates (Floyd's
+// algorithm: the shuffled prefix of pretrain.py:197-207 is a uniform subset) and 80/10/10
+// decisions per masked token, both from one 32-bit draw each (exact uniform integers by Lemire's
+// multiply-shift with rejection).
 // ---------------------------------------------------------------------------------------------
 __device__ inline uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
   x ^= x >> 30;
@@ -843,7 +845,7 @@ __device__ inline uint64_t part_key(uint64_t native_seed, int64_t part_seed) {
   return mix64(native_seed ^ mix64((uint64_t)part_seed + 0x9E3779B97F4A7C15ull));
 }
 
-enum : uint32_t { kStreamWalk = 1, kStreamMask = 2, kStreamOrder = 3 };
+enum : uint32_t { kStreamWalk = 1, kStreamMask = 2, kStreamOrder = 3, kStreamDecide = 4 };
 
 struct CtrRng {
   uint2 key;
@@ -915,117 +917,227 @@ __device__ inline int32_t win_token(const NativeArgs& A, int64_t k, int32_t fron
   return A.dense[A.kscan[k] + front + t];
 }
 
-// Unit u = (duplicate dp, document d) of partition p, numbered dup * kp_off[p] + dp * nd + d_local
-// (the reference's `for _ in range(dup): for doc in docs` order). EMIT = false counts the unit's
-// pairs; EMIT = true replays the identical draws and writes them at uoff[u].
-template <bool EMIT>
-__global__ void __launch_bounds__(256) plan_native_kernel(NativeArgs A) {
-  const int64_t ul = (int64_t)blockIdx.x * 256 + threadIdx.x;  // unit, counted from partition 0
-  if (ul >= A.n_units) return;
-  const int64_t u = ul + A.unit0;
-  int64_t lo = 0, hi = A.n_part;  // largest p with dup * kp_off[p] <= u
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if ((int64_t)A.dup * A.kp_off[mid] <= u) lo = mid;
-    else hi = mid;
+// One partition's walk tables: cumulative kept-sentence lengths and document starts, both
+// partition-relative. Staged in LDS when the partition fits (every length sum and search of the
+// walk is then an LDS read), else read from the global prefix `g_pre` (int64 over all kept
+// sentences) and kd_off. The branch is uniform over the workgroup.
+struct WalkTab {
+  const int32_t* s_pre;  // [nsp + 1]
+  const int32_t* s_doc;  // [nd + 1]
+  const int64_t* g_pre;
+  const int64_t* g_doc;  // kd_off + d0
+  int64_t sb, pre_sb;    // the partition's first kept sentence, g_pre[sb]
+  bool lds;
+  __device__ int64_t pre(int64_t i) const { return lds ? (int64_t)s_pre[i] : g_pre[sb + i] - pre_sb; }
+  __device__ int32_t doc(int64_t d) const { return lds ? s_doc[d] : (int32_t)(g_doc[d] - sb); }
+};
+
+// Smallest e in [i, end) whose sentences i..e reach `need` = pre(i) + target (pre(e + 1) >= need),
+// else end - 1: the chunk / random-B loops of create_pairs_from_document (pretrain.py:276-280,
+// 300-304) as a galloping search over the cumulative lengths (pre(i) < need on entry).
+__device__ inline int32_t first_reaching(const WalkTab& W, int32_t i, int32_t end, int64_t need) {
+  int32_t a = i, b = i + 1;
+  for (int32_t step = 1;; step <<= 1) {
+    b = a + step;
+    if (b >= end) {
+      b = end;
+      break;
+    }
+    if (W.pre(b) >= need) break;
+    a = b;
   }
-  const int64_t p = lo;
+  if (b == end && W.pre(end) < need) return end - 1;
+  while (b - a > 1) {  // pre(a) < need <= pre(b)
+    const int32_t m = (a + b) >> 1;
+    if (W.pre(m) >= need) b = m;
+    else a = m;
+  }
+  return b - 1;
+}
+
+// Literal [CLS]/[SEP] among kept sentences [x, y) of the partition (rare: only partitions that
+// hold one at all look).
+__device__ inline int32_t range_flags(const NativeArgs& A, bool has_flags, int64_t sb, int32_t x,
+                                      int32_t y) {
+  int32_t f = 0;
+  if (has_flags)
+    for (int32_t j = x; j < y; ++j) f |= A.ks_len[sb + j];
+  return f & kLenHasClsSep;
+}
+
+constexpr int kNativeThreads = 256;
+
+// Unit r = (duplicate dp, document dl) of partition p is r = dp * nd + dl (the reference's
+// `for _ in range(dup): for doc in docs` order); its global index is dup * (kp_off[p] -
+// kp_off[0]) + r. One workgroup per partition: the partition's cumulative sentence lengths and
+// document starts are staged in LDS, then every lane walks units, one chunk (pair) per loop
+// iteration, taking the partition's next unit from an LDS counter when its unit ends - so a lane
+// whose document is short does not idle while another lane's runs on. Chunk ends, A/B lengths and
+// the random-next B span are LDS searches over the cumulative lengths (no per-sentence loop).
+// EMIT = false counts each unit's pairs; EMIT = true replays the identical draws and writes them
+// at uoff[unit].
+template <bool EMIT>
+__global__ void __launch_bounds__(kNativeThreads) plan_native_kernel(NativeArgs A, const int64_t* g_pre,
+                                                                     int32_t lds_words) {
+  extern __shared__ int32_t s_tab[];
+  __shared__ int32_t s_next;
+  const int64_t p = blockIdx.x;
   const int64_t d0 = A.kp_off[p], nd = A.kp_off[p + 1] - d0;
-  const int64_t r = u - (int64_t)A.dup * d0;
-  const int64_t dl = r % nd;
-  CtrRng rng(part_key(A.native_seed, A.part_seed[p]), r, kStreamWalk);
-  const int64_t s0 = A.kd_off[d0 + dl];
-  const int ns = (int)(A.kd_off[d0 + dl + 1] - s0);
+  const int64_t sb = A.kd_off[d0], nsp = A.kd_off[d0 + nd] - sb;
+  WalkTab W{s_tab, s_tab + nsp + 1, g_pre, A.kd_off + d0, sb, 0,
+            nsp + nd + 2 <= (int64_t)lds_words};
+  bool flag_any = false;
+  if (W.lds) {
+    int32_t* pre = s_tab;
+    int32_t* dst = s_tab + nsp + 1;
+    for (int64_t i = threadIdx.x; i < nsp; i += kNativeThreads) {
+      const int32_t v = A.ks_len[sb + i];
+      pre[i + 1] = v & kLenMask;
+      flag_any |= (v & kLenHasClsSep) != 0;
+    }
+    for (int64_t d = threadIdx.x; d <= nd; d += kNativeThreads) dst[d] = (int32_t)(A.kd_off[d0 + d] - sb);
+    if (threadIdx.x == 0) {
+      pre[0] = 0;
+      s_next = kNativeThreads;
+    }
+    __syncthreads();
+    // in-place inclusive scan of pre[1 .. nsp]: a contiguous run per thread, then the runs' sums
+    const int32_t per = (int32_t)((nsp + kNativeThreads - 1) / kNativeThreads);
+    const int32_t x0 = 1 + (int32_t)threadIdx.x * per;
+    const int32_t x1 = min(x0 + per, (int32_t)nsp + 1);
+    int32_t run = 0;
+    for (int32_t x = x0; x < x1; ++x) run += pre[x];
+    __shared__ int32_t s_wsum[kNativeThreads / 64];
+    const int32_t inc = wave_incl_scan(run);
+    if ((threadIdx.x & 63) == 63) s_wsum[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    int32_t off = inc - run;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += s_wsum[w];
+    for (int32_t x = x0; x < x1; ++x) {
+      off += pre[x];
+      pre[x] = off;
+    }
+  } else {
+    W.pre_sb = g_pre[sb];
+    for (int64_t i = threadIdx.x; i < nsp; i += kNativeThreads)
+      flag_any |= (A.ks_len[sb + i] & kLenHasClsSep) != 0;
+    if (threadIdx.x == 0) s_next = kNativeThreads;
+  }
+  const bool has_flags = __syncthreads_or(flag_any) != 0;
+  const int64_t nu = (int64_t)A.dup * nd;
+  const int64_t ug0 = (int64_t)A.dup * (d0 - A.kp_off[0]);  // global index of the partition's unit 0
+  const uint64_t key = part_key(A.native_seed, A.part_seed[p]);
   const int32_t max_num = A.seq - 3;
-  int32_t target = max_num;
-  if (rng.rand53() < A.k_short) target = (int32_t)rng.randint(2, max_num);
-  const int64_t base = EMIT ? A.uoff[ul] : 0;
-  int64_t np = 0;
-  int chunk0 = 0, chunk_n = 0;
-  int64_t cur_len = 0;
-  for (int i = 0; i < ns; ++i) {
-    if (chunk_n == 0) chunk0 = i;
-    ++chunk_n;
-    cur_len += A.ks_len[s0 + i] & kLenMask;
-    if (!(i == ns - 1 || cur_len >= target)) continue;
-    const int a_end = chunk_n >= 2 ? (int)rng.randint(1, chunk_n - 1) : 1;
-    int64_t la = 0;
-    int32_t flags = 0;
-    for (int j = chunk0; j < chunk0 + a_end; ++j) {
-      const int32_t wd = A.ks_len[s0 + j];
-      la += wd & kLenMask;
-      flags |= wd;
-    }
-    int64_t lb = 0, b_ks;
-    int32_t rn = 0;
-    if (chunk_n == 1 || rng.coin()) {
-      rn = 1;
-      const int64_t target_b = target - la;
-      int64_t rd = 0;
-      for (int t = 0; t < 10; ++t) {
-        rd = rng.randint(0, nd - 1);
-        if (rd != dl) break;
+  int64_t r = threadIdx.x;
+  bool fresh = true;
+  CtrRng rng(key, 0, kStreamWalk);
+  int32_t s0 = 0, ns = 0, i = 0, target = 0, dl = 0;
+  int64_t np = 0, base = 0;
+  while (__builtin_amdgcn_ballot_w64(r < nu)) {
+    if (r < nu) {
+      if (fresh) {  // a new unit: its document and target length (pretrain.py:259-262)
+        fresh = false;
+        dl = (int32_t)(r % nd);
+        rng = CtrRng(key, r, kStreamWalk);
+        s0 = W.doc(dl);
+        ns = W.doc(dl + 1) - s0;
+        i = 0;
+        np = 0;
+        if (EMIT) base = A.uoff[ug0 + r];
+        target = max_num;
+        if (rng.rand53() < A.k_short) target = (int32_t)rng.randint(2, max_num);
       }
-      if (rd == dl) rn = 0;
-      const int64_t r0 = A.kd_off[d0 + rd];
-      const int rns = (int)(A.kd_off[d0 + rd + 1] - r0);
-      const int rstart = (int)rng.randint(0, rns - 1);
-      b_ks = r0 + rstart;
-      for (int j = rstart; j < rns; ++j) {
-        const int32_t wd = A.ks_len[r0 + j];
-        lb += wd & kLenMask;
-        flags |= wd;
-        if (lb >= target_b) break;
-      }
-      i -= chunk_n - a_end;
-    } else {
-      b_ks = s0 + chunk0 + a_end;
-      for (int j = chunk0 + a_end; j < chunk0 + chunk_n; ++j) {
-        const int32_t wd = A.ks_len[s0 + j];
-        lb += wd & kLenMask;
-        flags |= wd;
-      }
-    }
-    // _truncate_seq_pair: which side each trim hits is fixed (see WaveRng::trunc_draws); front or
-    // back is a fair coin per trim
-    int32_t na = (int32_t)la, nb = (int32_t)lb, a_front = 0, b_front = 0;
-    const int32_t T = na + nb - max_num;
-    if (T > 0) {
-      const int32_t dd = na - nb, ad = dd < 0 ? -dd : dd;
-      const int32_t nA = (dd > 0 ? min(dd, T) : 0) + (T > ad ? (T - ad) / 2 : 0);
-      a_front = rng.heads(nA);
-      b_front = rng.heads(T - nA);
-      na -= nA;
-      nb -= T - nA;
-    }
-    if (EMIT) {
-      const int64_t q = base + np;
-      A.desc[q] = PairDesc{s0 + chunk0, b_ks, a_front, na, b_front,
-                           nb | (int32_t)((uint32_t)rn << 31)};
-      A.ppart[q] = (int32_t)p;
-      if (A.masking) {
-        int32_t nc = na + nb;
-        if (flags & kLenHasClsSep) {  // literal [CLS]/[SEP] in the text are not candidates
-          nc = 0;
-          for (int32_t t = 0; t < na + nb; ++t) {
-            const int32_t tok = t < na ? win_token(A, s0 + chunk0, a_front, t)
-                                       : win_token(A, b_ks, b_front, t - na);
-            nc += tok != A.cls_id && tok != A.sep_id;
+      if (i < ns) {  // one chunk -> one pair
+        const int64_t c_pre = W.pre(s0 + i);
+        const int32_t e = first_reaching(W, s0 + i, s0 + ns, c_pre + target) - s0;
+        const int32_t chunk0 = i, chunk_n = e - i + 1;
+        const int32_t a_end = chunk_n >= 2 ? (int32_t)rng.randint(1, chunk_n - 1) : 1;
+        const int64_t la = W.pre(s0 + chunk0 + a_end) - c_pre;
+        int64_t lb, b_ks;
+        int32_t rn = 0, flags = 0;
+        if (chunk_n == 1 || rng.coin()) {  // random next (pretrain.py:291-321)
+          rn = 1;
+          const int64_t target_b = target - la;
+          int64_t rd = 0;
+          for (int t = 0; t < 10; ++t) {
+            rd = rng.randint(0, nd - 1);
+            if (rd != dl) break;
+          }
+          if (rd == dl) rn = 0;
+          const int32_t r0 = W.doc(rd), rns = W.doc(rd + 1) - r0;
+          const int32_t rstart = (int32_t)rng.randint(0, rns - 1);
+          const int64_t b_pre = W.pre(r0 + rstart);
+          const int32_t be = first_reaching(W, r0 + rstart, r0 + rns, b_pre + target_b);
+          lb = W.pre(be + 1) - b_pre;
+          b_ks = sb + r0 + rstart;
+          if (EMIT && A.masking)
+            flags = range_flags(A, has_flags, sb, s0 + chunk0, s0 + chunk0 + a_end) |
+                    range_flags(A, has_flags, sb, r0 + rstart, be + 1);
+          i = chunk0 + a_end;  // the unused segments are put back (pretrain.py:320-321)
+        } else {
+          lb = W.pre(s0 + e + 1) - W.pre(s0 + chunk0 + a_end);
+          b_ks = sb + s0 + chunk0 + a_end;
+          if (EMIT && A.masking) flags = range_flags(A, has_flags, sb, s0 + chunk0, s0 + e + 1);
+          i = e + 1;
+        }
+        // _truncate_seq_pair: which side each trim hits is fixed (see WaveRng::trunc_draws); front
+        // or back is a fair coin per trim
+        int32_t na = (int32_t)la, nb = (int32_t)lb, a_front = 0, b_front = 0;
+        const int32_t T = na + nb - max_num;
+        if (T > 0) {
+          const int32_t dd = na - nb, ad = dd < 0 ? -dd : dd;
+          const int32_t nA = (dd > 0 ? min(dd, T) : 0) + (T > ad ? (T - ad) / 2 : 0);
+          a_front = rng.heads(nA);
+          b_front = rng.heads(T - nA);
+          na -= nA;
+          nb -= T - nA;
+        }
+        if (EMIT) {
+          const int64_t q = base + np;
+          const int64_t a_ks = sb + s0 + chunk0;
+          A.desc[q] = PairDesc{a_ks, b_ks, a_front, na, b_front, nb | (int32_t)((uint32_t)rn << 31)};
+          A.ppart[q] = (int32_t)p;
+          if (A.masking) {
+            int32_t nc = na + nb;
+            if (flags) {  // literal [CLS]/[SEP] in the text are not candidates
+              nc = 0;
+              for (int32_t t = 0; t < na + nb; ++t) {
+                const int32_t tok = t < na ? win_token(A, a_ks, a_front, t)
+                                           : win_token(A, b_ks, b_front, t - na);
+                nc += tok != A.cls_id && tok != A.sep_id;
+              }
+            }
+            int32_t num = (int32_t)rint((double)(na + nb + 3) * A.ratio);
+            if (num < 1) num = 1;
+            if (num > nc) num = nc;
+            A.nmask[q] = num;
+            A.ncand[q] = nc;
           }
         }
-        int32_t num = (int32_t)rint((double)(na + nb + 3) * A.ratio);
-        if (num < 1) num = 1;
-        if (num > nc) num = nc;
-        A.nmask[q] = num;
-        A.ncand[q] = nc;
+        ++np;
+      }
+      if (i >= ns) {  // the unit is done: take the partition's next one
+        if (!EMIT) A.ucnt[ug0 + r] = np;
+        r = atomicAdd(&s_next, 1);
+        fresh = true;
       }
     }
-    ++np;
-    chunk_n = 0;
-    cur_len = 0;
   }
-  if (!EMIT) A.ucnt[ul] = np;
 }
+
+// LDS words one partition's walk tables take; the largest over all partitions
+__global__ void native_part_need_kernel(const int64_t* kp_off, const int64_t* kd_off, int64_t n_part,
+                                        unsigned long long* need_max) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_part) return;
+  const int64_t d0 = kp_off[p], d1 = kp_off[p + 1];
+  atomicMax(need_max, (unsigned long long)(kd_off[d1] - kd_off[d0] + (d1 - d0) + 2));
+}
+
+struct KeptLenOnly {
+  const int32_t* v;
+  __device__ int64_t operator()(int64_t i) const { return v[i] & kLenMask; }
+};
 
 __global__ void native_part_base_kernel(const int64_t* kp_off, int64_t n_part, int32_t dup,
                                         const int64_t* uoff, int64_t* part_base) {
@@ -1033,38 +1145,76 @@ __global__ void native_part_base_kernel(const int64_t* kp_off, int64_t n_part, i
   if (p <= n_part) part_base[p] = uoff[(int64_t)dup * (kp_off[p] - kp_off[0])];
 }
 
-// Masked positions of pair q (one lane per pair): Floyd's sampling of num candidate indices out of
-// nc into a lane-private LDS bitmap, then the set bits in ascending order (= sorted(masked_lms,
-// key=index)) each with an 80/10/10 decision.
-__global__ void __launch_bounds__(256) mask_native_kernel(NativeArgs A) {
-  extern __shared__ uint32_t s_bm[];  // [wave][word][lane]
-  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  uint32_t* bm = s_bm + (size_t)(threadIdx.x >> 6) * A.words * 64 + lane;
-  if (q >= A.n_pairs) return;
-  const int32_t num = A.nmask[q];
-  if (num <= 0) return;
-  const int32_t nc = A.ncand[q];
-  const PairDesc d = A.desc[q];
-  const int32_t na = d.na, nb = d.nb_rn & 0x7FFFFFFF;
-  const int64_t p = A.ppart[q];
-  CtrRng rng(part_key(A.native_seed, A.part_seed[p]), q - A.part_base[p], kStreamMask);
-  const int nw = (nc + 31) >> 5;
-  for (int i = 0; i < nw; ++i) bm[i * 64] = 0u;
-  for (int32_t j = nc - num; j < nc; ++j) {
-    const uint32_t t = rng.randbelow((uint32_t)j + 1);
-    const uint32_t wt = bm[(t >> 5) * 64];
-    const uint32_t pick = (wt >> (t & 31)) & 1u ? (uint32_t)j : t;
-    bm[(pick >> 5) * 64] |= 1u << (pick & 31);
+// Uniform integer in [0, n) from a 32-bit draw: Lemire's multiply-shift with the exact rejection
+// (taken with probability < n / 2^32, so the lanes of a wave stay in step).
+__device__ inline uint32_t lemire_below(uint32_t x, uint32_t n, CtrRng& rng) {
+  uint64_t m = (uint64_t)x * n;
+  if ((uint32_t)m < n) {
+    const uint32_t t = (0u - n) % n;
+    while ((uint32_t)m < t) m = (uint64_t)rng.u32() * n;
   }
+  return (uint32_t)(m >> 32);
+}
+
+// 80 / 10 / 10 of create_masked_lm_predictions (pretrain.py:214-229) on one 32-bit draw:
+// [MASK] below ceil(0.8 * 2^32), the original token below ceil(0.9 * 2^32), else a random token.
+constexpr uint32_t kNat80 = 3435973837u, kNat90 = 3865470567u;
+
+// Masked positions of 64 consecutive pairs per wave (one lane per pair), in lock step so that
+// every lane's Philox refill comes at the same iteration:
+//  1. Floyd's sampling of num candidate indices out of nc (a uniform num-subset: the shuffled
+//     prefix of pretrain.py:197-207), one draw per step, into a lane-private LDS bitmap;
+//  2. the set bits in ascending order (= sorted(masked_lms, key=index)), each with an 80/10/10
+//     decision from its own stream (two draws per mask, whatever the decision), staged in LDS;
+//  3. the wave's masks are one contiguous run of the pool (moff is the planner-order scan), copied
+//     out with coalesced stores.
+// Every draw's stream position depends on the pair alone (the sampling and the decisions use
+// separate streams), so a pair's masks do not depend on the pairs that share its wave.
+__global__ void __launch_bounds__(256) mask_native_kernel(NativeArgs A, int32_t stage_cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_mn[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int64_t q0 = ((int64_t)blockIdx.x * nw + w) * 64;
+  if (q0 >= A.n_pairs) return;
+  uint32_t* bm = reinterpret_cast<uint32_t*>(s_mn) + (size_t)w * A.words * 64 + lane;
+  int32_t* stok = reinterpret_cast<int32_t*>(s_mn + (size_t)nw * A.words * 64 * 4) + (size_t)w * stage_cap;
+  uint16_t* spos = reinterpret_cast<uint16_t*>(s_mn + (size_t)nw * A.words * 64 * 4 +
+                                                (size_t)nw * stage_cap * 4) + (size_t)w * stage_cap;
+  const int64_t q = q0 + lane;
+  const bool valid = q < A.n_pairs;
+  const int64_t qv = valid ? q : q0;
+  const int64_t qe = q0 + 64 < A.n_pairs ? q0 + 64 : A.n_pairs;
+  const int64_t m0 = A.moff[q0];
+  const int32_t mend = (int32_t)(A.moff[qe] - m0);
+  const int32_t num = valid ? A.nmask[qv] : 0;
+  const int32_t nc = A.ncand[qv];
+  const int32_t mb = (int32_t)(A.moff[qv] - m0);
+  const PairDesc d = A.desc[qv];
+  const int32_t na = d.na, nb = d.nb_rn & 0x7FFFFFFF;
+  const int64_t p = A.ppart[qv];
+  const uint64_t key = part_key(A.native_seed, A.part_seed[p]);
+  const int64_t idx = qv - A.part_base[p];
+  for (int i = 0; i < A.words; ++i) bm[i * 64] = 0u;
+  CtrRng rng(key, idx, kStreamMask);
+  for (int32_t s = 0; __builtin_amdgcn_ballot_w64(s < num); ++s) {
+    const uint32_t u = rng.u32();
+    if (s < num) {
+      const uint32_t j = (uint32_t)(nc - num + s);
+      const uint32_t t = lemire_below(u, j + 1u, rng);
+      const uint32_t wt = bm[(t >> 5) * 64];
+      const uint32_t pick = (wt >> (t & 31)) & 1u ? j : t;
+      bm[(pick >> 5) * 64] |= 1u << (pick & 31);
+    }
+  }
+  CtrRng drng(key, idx, kStreamDecide);
   const bool fast = nc == na + nb;
-  const int64_t mb = A.moff[q];
-  int32_t m = 0, tcur = 0, ccur = 0;  // slow path: token / candidate cursor
-  for (int i = 0; i < nw; ++i) {
-    uint32_t bits = bm[i * 64];
-    while (bits) {
-      const int32_t ci = i * 32 + __ffs(bits) - 1;
-      bits &= bits - 1;
+  int32_t wi = 0, tcur = 0, ccur = 0;  // bitmap word; slow path: token / candidate cursor
+  uint32_t bits = num > 0 ? bm[0] : 0u;
+  for (int32_t m = 0; __builtin_amdgcn_ballot_w64(m < num); ++m) {
+    const uint32_t x = drng.u32(), y = drng.u32();
+    if (m < num) {
+      while (bits == 0u) bits = bm[++wi * 64];
+      const int32_t ci = wi * 32 + __ffs(bits) - 1;
+      bits &= bits - 1u;
       int32_t t = ci;
       if (!fast) {  // walk to the ci-th non-[CLS]/[SEP] token
         while (true) {
@@ -1079,14 +1229,17 @@ __global__ void __launch_bounds__(256) mask_native_kernel(NativeArgs A) {
         t = tcur++;
         ++ccur;
       }
-      int32_t tok;
-      if (rng.rand53() < kLt08) tok = A.mask_id;
-      else if (rng.coin()) tok = kKeep;
-      else tok = (int32_t)rng.randbelow((uint32_t)A.vocab_size);
-      A.mpos[mb + m] = (uint16_t)(t < na ? t + 1 : t + 2);
-      A.mtok[mb + m] = tok;
-      ++m;
+      const int32_t tok = x < kNat80 ? A.mask_id
+                          : x < kNat90 ? kKeep
+                                       : (int32_t)lemire_below(y, (uint32_t)A.vocab_size, drng);
+      spos[mb + m] = (uint16_t)(t < na ? t + 1 : t + 2);
+      stok[mb + m] = tok;
     }
+  }
+  wave_sync();
+  for (int32_t i = lane; i < mend; i += 64) {
+    A.mpos[m0 + i] = spos[i];
+    A.mtok[m0 + i] = stok[i];
   }
 }
 
@@ -1465,7 +1618,6 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, sl = lane & 31;
   const int64_t wg = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
   const int64_t q0 = (wg * kGWaves + w) * 2 * K;  // pairs q0 + 2k + h
-  const uint64_t hm = h ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
   const int W = Lg.W;
 
   int64_t tof[K], aoff[K], boff[K], po[K], mb[K];
@@ -1671,8 +1823,16 @@ static int plan_native(lddl_pairs* P, lddl_ctx* c, const lddl_pair_params* prm,
   A.part_seed = d_part_seed;
   A.n_part = n_part;
   int64_t kp_ends[2] = {0, 0};  // kept documents covered by the partitions
+  unsigned long long need_max = 0, *d_need;
+  int rc;
+  if ((rc = P->alloc(&d_need, 1, st))) return rc;
+  LDDL_HIP(hipMemsetAsync(d_need, 0, 8, st));
+  if (n_part)
+    hipLaunchKernelGGL(native_part_need_kernel, dim3((unsigned)((n_part + 255) / 256)), dim3(256), 0, st,
+                       P->kp_off, P->kd_off, n_part, d_need);
   LDDL_HIP(hipMemcpyAsync(&kp_ends[0], P->kp_off, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipMemcpyAsync(&kp_ends[1], P->kp_off + n_part, 8, hipMemcpyDeviceToHost, st));
+  LDDL_HIP(hipMemcpyAsync(&need_max, d_need, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
   A.unit0 = (int64_t)prm->dup * kp_ends[0];
   A.n_units = (int64_t)prm->dup * (kp_ends[1] - kp_ends[0]);
@@ -1687,14 +1847,22 @@ static int plan_native(lddl_pairs* P, lddl_ctx* c, const lddl_pair_params* prm,
   A.vocab_size = c->vocab_size;
   A.ratio = prm->masked_lm_ratio;
   const int64_t nu = A.n_units;
-  int64_t *uoff, *scr;
-  int rc;
+  // walk tables in LDS up to 96 KB per workgroup; larger partitions read a global prefix
+  constexpr int64_t kLdsWordsCap = 24576;
+  const int32_t lds_words = (int32_t)std::min<int64_t>((int64_t)need_max, kLdsWordsCap);
+  int64_t *uoff, *scr, *g_pre = nullptr;
   if ((rc = P->alloc(&A.ucnt, nu, st)) || (rc = P->alloc(&uoff, nu + 1, st)) ||
-      (rc = P->alloc(&scr, scan_scratch_elems(nu + 1), st)))
+      (rc = P->alloc(&scr, scan_scratch_elems(std::max(nu, P->n_kept_sent) + 1), st)))
     return rc;
+  if ((int64_t)need_max > kLdsWordsCap) {
+    if ((rc = P->alloc(&g_pre, P->n_kept_sent + 1, st))) return rc;
+    LDDL_HIP(scan_exclusive(KeptLenOnly{P->ks_len}, P->n_kept_sent, g_pre, scr, st));
+  }
   LDDL_HIP(hipEventRecord(P->ev[0], st));
-  const unsigned gu = (unsigned)((nu + 255) / 256);
-  if (nu) hipLaunchKernelGGL(plan_native_kernel<false>, dim3(gu), dim3(256), 0, st, A);
+  const size_t lds_bytes = (size_t)4 * lds_words;
+  if (n_part && nu)
+    hipLaunchKernelGGL(plan_native_kernel<false>, dim3((unsigned)n_part), dim3(kNativeThreads), lds_bytes,
+                       st, A, g_pre, lds_words);
   LDDL_HIP(hipGetLastError());
   LDDL_HIP(scan_exclusive(Identity{A.ucnt}, nu, uoff, scr, st));
   LDDL_HIP(hipMemcpyAsync(&P->n_pairs, uoff + nu, 8, hipMemcpyDeviceToHost, st));
@@ -1714,7 +1882,9 @@ static int plan_native(lddl_pairs* P, lddl_ctx* c, const lddl_pair_params* prm,
   A.part_base = P->part_base;
   A.desc = P->desc;
   A.nmask = P->nmask;
-  if (nu) hipLaunchKernelGGL(plan_native_kernel<true>, dim3(gu), dim3(256), 0, st, A);
+  if (n_part && nu)
+    hipLaunchKernelGGL(plan_native_kernel<true>, dim3((unsigned)n_part), dim3(kNativeThreads), lds_bytes,
+                       st, A, g_pre, lds_words);
   LDDL_HIP(hipGetLastError());
   const unsigned gp = (unsigned)((n + 255) / 256);
   if (prm->masking) {
@@ -1727,9 +1897,14 @@ static int plan_native(lddl_pairs* P, lddl_ctx* c, const lddl_pair_params* prm,
     A.mpos = P->mpos;
     A.mtok = P->mtok;
     A.words = (prm->seq + 31) / 32;
+    // per wave: the 64 lanes' bitmaps + the staged masks of its 64 pairs (<= max_pred each);
+    // up to 4 waves per workgroup within 64 KB of LDS
+    const int32_t stage_cap = 64 * std::max(P->max_pred, 1);
+    const size_t per_wave = (size_t)A.words * 64 * 4 + (size_t)stage_cap * 6;
+    const int nwv = (int)std::max<size_t>(1, std::min<size_t>(4, 65536 / per_wave));
     if (n)
-      hipLaunchKernelGGL(mask_native_kernel, dim3(gp), dim3(256), (size_t)4 * 64 * 4 * A.words, st,
-                         A);
+      hipLaunchKernelGGL(mask_native_kernel, dim3((unsigned)((n + 64 * nwv - 1) / (64 * nwv))),
+                         dim3(64 * nwv), per_wave * nwv, st, A, stage_cap);
     LDDL_HIP(hipGetLastError());
   }
   A.src = P->src;

@@ -220,4 +220,6 @@ def test_stream_virtual_gpu_balanced_moves_nothing(gpu_tables):
     moved = sum(o.moved_rows for o in outs[0])
     check_stream([[p.to_host() for p in parts]], [[_to_host_out(o, ops) for o in outs[0]]], 8, nb,
                  W, moved=[[o.moved_rows for o in outs[0]]])
-    assert moved <= (W - 1) * nb and moved < 0.05 * pb.n_pairs
+    # per bin, each rank holds floor or ceil of its share and so does its quota: at most W - 1
+    # rows move per bin (the round-robin deal of round 3 moved (W - 1) / W of all rows)
+    assert moved <= (W - 1) * nb and moved < 0.2 * pb.n_pairs

@@ -403,7 +403,7 @@ def _cli_world2(tmp_path, sink, extra, env_extra=None):
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
            '--master-addr', '127.0.0.1', '--master-port', str(port), '-m',
            'lddl_amd.dask.bert.pretrain', '--schedule', 'local', '--wikipedia', str(src),
-           '--sink', str(sink), '--target-seq-length', '128', '--num-blocks', '3', '--seed', '7',
+           '--sink', str(sink), '--target-seq-length', '128', '--num-blocks', '2', '--seed', '7',
            '--vocab-file', VOCAB_UNCASED, '--local-n-workers', '1', '--duplicate-factor', '2',
            '--masking'] + extra
     r = subprocess.run(cmd, env=env, cwd=repo, capture_output=True, text=True, timeout=300)
@@ -412,7 +412,7 @@ def _cli_world2(tmp_path, sink, extra, env_extra=None):
 
 def test_pretrain_cli_num_shards_world2_unequal_batches(tmp_path):
     """Two ranks (sharing the one GPU, gloo collectives staged through host memory) with
-    different numbers of GPU batches (3 partitions, one batch each): the collective balance loop
+    different numbers of GPU batches (3 partitions, one batch each: 2 and 1): the collective loop
     ends on the batch iterators themselves, the rank that runs out keeps taking part with empty
     batches, and the shards hold exactly the rows of the same run's part files, N or N+1 per
     shard and bin (termination no longer depends on a second count of the batches)."""
