@@ -96,6 +96,9 @@ int lddl_ctx_create(int device, const uint8_t* norm_table, int64_t table_len, co
 int lddl_ctx_destroy(lddl_ctx* ctx);
 int lddl_ctx_info(const lddl_ctx* ctx, int32_t* vocab_size, int32_t* special_ids,
                   int32_t* max_piece_bytes);
+/* Bytes per token id in the pair tables (lddl_pairs_emit tokens and labels, the render inputs):
+ * 2 (uint16) when vocab_size <= 65536, else 4 (int32). */
+int lddl_ctx_id_bytes(const lddl_ctx* ctx);
 /* device pointers to the vocab strings (for rendering ' '.join(tokens)): token i is
  * bytes[off[i] .. off[i+1]) */
 int lddl_ctx_render_table(const lddl_ctx* ctx, const uint8_t** d_bytes, const int64_t** d_off);
@@ -197,8 +200,8 @@ int lddl_pairs_plan(lddl_ctx* ctx, void* stream, const lddl_pair_params* params,
                     int64_t n_sent, const int64_t* d_doc_sent_off, int64_t n_doc,
                     const int64_t* d_part_doc_off, const int64_t* d_part_seed, int64_t n_part,
                     lddl_pairs** out, int64_t* counts);
-int lddl_pairs_emit(lddl_pairs* plan, void* stream, int32_t* d_tokens, int64_t* d_tok_off,
-                    int32_t* d_len_a, uint8_t* d_is_rn, uint16_t* d_pos, int32_t* d_lab,
+int lddl_pairs_emit(lddl_pairs* plan, void* stream, void* d_tokens, int64_t* d_tok_off,
+                    int32_t* d_len_a, uint8_t* d_is_rn, uint16_t* d_pos, void* d_lab,
                     int64_t* d_pos_off);
 int lddl_pairs_destroy(lddl_pairs* plan, void* stream);
 /* d_part_pair_off[n_part + 1]: first output pair of each partition (pairs are emitted in
@@ -240,14 +243,14 @@ int lddl_bin_stable(lddl_ctx* ctx, void* stream, const int32_t* d_num_tokens,
  * It also writes the rows' num_tokens (uint16, len(A) + len(B) + 3) and, from d_is_rn,
  * is_random_next in output order (each output pointer may be NULL).
  * ------------------------------------------------------------------------------------------- */
-int lddl_render_lengths(lddl_ctx* ctx, void* stream, const int32_t* d_tokens,
-                        const int64_t* d_tok_off, const int32_t* d_len_a, const int32_t* d_lab,
+int lddl_render_lengths(lddl_ctx* ctx, void* stream, const void* d_tokens,
+                        const int64_t* d_tok_off, const int32_t* d_len_a, const void* d_lab,
                         const int64_t* d_pos_off, const int64_t* d_rows, int64_t n_rows,
                         int64_t* d_a_len, int64_t* d_b_len, int64_t* d_l_len, int64_t* d_npy_len,
                         const uint8_t* d_is_rn, uint16_t* d_num_tokens_out, uint8_t* d_is_rn_out);
-int lddl_render_write(lddl_ctx* ctx, void* stream, const int32_t* d_tokens,
+int lddl_render_write(lddl_ctx* ctx, void* stream, const void* d_tokens,
                       const int64_t* d_tok_off, const int32_t* d_len_a, const uint16_t* d_pos,
-                      const int32_t* d_lab, const int64_t* d_pos_off, const int64_t* d_rows,
+                      const void* d_lab, const int64_t* d_pos_off, const int64_t* d_rows,
                       int64_t n_rows, const int64_t* d_a_off, const int64_t* d_b_off,
                       const int64_t* d_l_off, const int64_t* d_npy_off, uint8_t* d_a_bytes,
                       uint8_t* d_b_bytes, uint8_t* d_l_bytes, uint8_t* d_npy_bytes);

@@ -36,6 +36,7 @@ SIGNATURES = {
                                        ctypes.POINTER(c_vp)]),
     'lddl_ctx_destroy': (ctypes.c_int, [c_vp]),
     'lddl_ctx_info': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
+    'lddl_ctx_id_bytes': (ctypes.c_int, [c_vp]),
     'lddl_ctx_render_table': (ctypes.c_int, [c_vp, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp)]),
     'lddl_synth_doc_text': (c_i64, [c_u64, c_i64, c_i64, c_dbl, c_vp, c_i64, c_vp, c_i64, c_vp,
                                     ctypes.c_int]),

@@ -273,8 +273,9 @@ class RankBalance:
         self.dev = pb.tok_off.device
         self.masking = pb.pos is not None
         if self.masking:
-            assert pb.pos.element_size() == 2 and pb.labels.element_size() == 4
-        assert pb.tokens.element_size() == 4
+            assert pb.pos.element_size() == 2
+            assert pb.labels.element_size() == pb.tokens.element_size()
+        assert pb.tokens.element_size() in (2, 4)  # uint16 or int32 ids (Context.id_dtype)
         self.perm, self.local_counts = ops.bin_stable(pb, bin_size, nbins)
 
     # plan ----------------------------------------------------------------------------------

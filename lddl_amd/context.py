@@ -82,6 +82,10 @@ class Context:
         self.vocab_size = vs.value
         self.special_ids = dict(zip(SPECIALS, list(sp)))
         self.max_piece_bytes = mp.value
+        # token ids of the pair tables (PairBatch.tokens / labels): uint16 when the vocab fits
+        # (held in int16 tensors), else int32 (lddl_ctx_id_bytes)
+        self.id_bytes = lib.lddl_ctx_id_bytes(h)
+        self.id_dtype = torch.int16 if self.id_bytes == 2 else torch.int32
 
     @property
     def handle(self):

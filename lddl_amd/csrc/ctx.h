@@ -78,8 +78,19 @@ class DevArena {
   }
   void give(Block b, hipStream_t st) {
     if (!b.p) return;
-    if (b.ext) {  // stream-ordered external pool: reusable by later work on `st`
-      if (free_fn_) free_fn_(b.p, (void*)st, user_);
+    if (b.ext) {
+      // a stream-ordered external pool (torch's caching allocator) reuses the block on the stream
+      // it was allocated on: when the last use was on another stream, that stream is ordered
+      // after it first, so no later allocation there can overwrite the block while it is in use
+      if (st != b.st) {
+        hipEvent_t ev;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
+          (void)hipEventRecord(ev, st);
+          (void)hipStreamWaitEvent(b.st, ev, 0);
+          (void)hipEventDestroy(ev);
+        }
+      }
+      if (free_fn_) free_fn_(b.p, (void*)b.st, user_);
       return;
     }
     if (!b.ev) (void)hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
@@ -142,6 +153,9 @@ struct lddl_ctx {
   uint32_t* d_bloom = nullptr;
   uint64_t* d_vlong = nullptr;
   int32_t vocab_size = 0;
+  // bytes per token id in the pair tables (dense kept tokens, sample tokens, labels): 2 when every
+  // id fits uint16 (vocab_size <= 65536: BERT's uncased 30,522 and cased 28,996), else 4
+  int32_t id_bytes() const { return vocab_size <= 65536 ? 2 : 4; }
   size_t lds_per_block = 0;         // hipDeviceAttributeMaxSharedMemoryPerBlock of `device`
   std::vector<std::string> tokens;  // host copy of the vocab lines
   lddl::DevArena arena;             // per-call temporaries (pair plans)

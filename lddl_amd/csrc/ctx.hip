@@ -217,6 +217,11 @@ extern "C" int lddl_ctx_info(const lddl_ctx* c, int32_t* vocab_size, int32_t* sp
   return 0;
 }
 
+extern "C" int lddl_ctx_id_bytes(const lddl_ctx* c) {
+  if (!c) LDDL_FAIL(-1, "null ctx");
+  return c->id_bytes();
+}
+
 extern "C" int lddl_ctx_render_table(const lddl_ctx* c, const uint8_t** d_bytes,
                                      const int64_t** d_off) {
   if (!c) LDDL_FAIL(-1, "null ctx");

@@ -176,35 +176,42 @@ __global__ void bin_totals_kernel(const int64_t* __restrict__ tile_base, int64_t
 struct RenderArgs {
   const uint8_t* rbytes;  // vocab render table
   const int64_t* roff;
-  const int32_t* tokens;
+  const void* tokens;  // ids of lddl_ctx::id_bytes bytes each (uint16 or int32)
   const int64_t* tok_off;
   const int32_t* len_a;
   const uint16_t* pos;
-  const int32_t* lab;
+  const void* lab;     // as tokens
   const int64_t* pos_off;
   const int64_t* rows;  // output row -> pair (NULL: identity)
   int64_t n_rows;
+  int32_t ib;           // bytes per id
 };
+
+// id i of an id array of R.ib-byte entries
+__device__ inline int32_t id_at(const RenderArgs& R, const void* ids, int64_t i) {
+  return R.ib == 2 ? (int32_t)static_cast<const uint16_t*>(ids)[i] : static_cast<const int32_t*>(ids)[i];
+}
 
 __device__ inline int32_t tok_len(const RenderArgs& R, int32_t id) {
   return (int32_t)(R.roff[id + 1] - R.roff[id]);
 }
 
-// total bytes of ' '.join(strings of ids[0..n))
-__device__ int64_t joined_len(const RenderArgs& R, const int32_t* ids, int64_t n) {
+// total bytes of ' '.join(strings of ids[i0 .. i0 + n))
+__device__ int64_t joined_len(const RenderArgs& R, const void* ids, int64_t i0, int64_t n) {
   int64_t acc = 0;
   for (int64_t c0 = 0; c0 < n; c0 += 64) {
     const int64_t j = c0 + lane_id();
-    acc += j < n ? tok_len(R, ids[j]) : 0;
+    acc += j < n ? tok_len(R, id_at(R, ids, i0 + j)) : 0;
   }
   return wave_sum(acc) + (n > 0 ? n - 1 : 0);
 }
 
-__device__ void joined_write(const RenderArgs& R, const int32_t* ids, int64_t n, uint8_t* out) {
+__device__ void joined_write(const RenderArgs& R, const void* ids, int64_t i0, int64_t n,
+                             uint8_t* out) {
   int64_t base = 0;
   for (int64_t c0 = 0; c0 < n; c0 += 64) {
     const int64_t j = c0 + lane_id();
-    const int32_t id = j < n ? ids[j] : 0;
+    const int32_t id = j < n ? id_at(R, ids, i0 + j) : 0;
     const int64_t l = j < n ? tok_len(R, id) + 1 : 0;  // string + separator
     const int64_t incl = wave_incl_scan(l);
     if (j < n) {
@@ -227,12 +234,12 @@ __global__ void __launch_bounds__(256) render_lengths_kernel(RenderArgs R, int64
   const int64_t q = R.rows ? R.rows[row] : row;
   const int64_t t0 = R.tok_off[q], t1 = R.tok_off[q + 1];
   const int32_t na = R.len_a[q];
-  const int64_t la = joined_len(R, R.tokens + t0, na);
-  const int64_t lb = joined_len(R, R.tokens + t0 + na, t1 - t0 - na);
+  const int64_t la = joined_len(R, R.tokens, t0, na);
+  const int64_t lb = joined_len(R, R.tokens, t0 + na, t1 - t0 - na);
   int64_t ll = 0, np = 0;
   if (R.pos_off) {
     const int64_t p0 = R.pos_off[q], p1 = R.pos_off[q + 1];
-    ll = joined_len(R, R.lab + p0, p1 - p0);
+    ll = joined_len(R, R.lab, p0, p1 - p0);
     np = p1 - p0;
   }
   if (lane_id() == 0) {
@@ -280,11 +287,11 @@ __global__ void __launch_bounds__(256) render_write_kernel(RenderArgs R, const i
   const int64_t q = R.rows ? R.rows[row] : row;
   const int64_t t0 = R.tok_off[q], t1 = R.tok_off[q + 1];
   const int32_t na = R.len_a[q];
-  joined_write(R, R.tokens + t0, na, a_bytes + a_off[row]);
-  joined_write(R, R.tokens + t0 + na, t1 - t0 - na, b_bytes + b_off[row]);
+  joined_write(R, R.tokens, t0, na, a_bytes + a_off[row]);
+  joined_write(R, R.tokens, t0 + na, t1 - t0 - na, b_bytes + b_off[row]);
   if (R.pos_off) {
     const int64_t p0 = R.pos_off[q], p1 = R.pos_off[q + 1];
-    if (l_bytes) joined_write(R, R.lab + p0, p1 - p0, l_bytes + l_off[row]);
+    if (l_bytes) joined_write(R, R.lab, p0, p1 - p0, l_bytes + l_off[row]);
     if (npy_bytes) put_npy(npy_bytes + npy_off[row], R.pos + p0, p1 - p0);
   }
 }
@@ -544,16 +551,16 @@ extern "C" int lddl_bin_stable(lddl_ctx* c, void* stream, const int32_t* d_num_t
   return 0;
 }
 
-static RenderArgs make_render(const lddl_ctx* c, const int32_t* d_tokens, const int64_t* d_tok_off,
-                              const int32_t* d_len_a, const uint16_t* d_pos, const int32_t* d_lab,
+static RenderArgs make_render(const lddl_ctx* c, const void* d_tokens, const int64_t* d_tok_off,
+                              const int32_t* d_len_a, const uint16_t* d_pos, const void* d_lab,
                               const int64_t* d_pos_off, const int64_t* d_rows, int64_t n_rows) {
   return RenderArgs{c->d_render, c->d_render_off, d_tokens, d_tok_off, d_len_a, d_pos, d_lab,
-                    d_pos_off, d_rows, n_rows};
+                    d_pos_off, d_rows, n_rows, c->id_bytes()};
 }
 
-extern "C" int lddl_render_lengths(lddl_ctx* c, void* stream, const int32_t* d_tokens,
+extern "C" int lddl_render_lengths(lddl_ctx* c, void* stream, const void* d_tokens,
                                    const int64_t* d_tok_off, const int32_t* d_len_a,
-                                   const int32_t* d_lab, const int64_t* d_pos_off,
+                                   const void* d_lab, const int64_t* d_pos_off,
                                    const int64_t* d_rows, int64_t n_rows, int64_t* d_a_len,
                                    int64_t* d_b_len, int64_t* d_l_len, int64_t* d_npy_len,
                                    const uint8_t* d_is_rn, uint16_t* d_num_tokens_out,
@@ -570,9 +577,9 @@ extern "C" int lddl_render_lengths(lddl_ctx* c, void* stream, const int32_t* d_t
   return 0;
 }
 
-extern "C" int lddl_render_write(lddl_ctx* c, void* stream, const int32_t* d_tokens,
+extern "C" int lddl_render_write(lddl_ctx* c, void* stream, const void* d_tokens,
                                  const int64_t* d_tok_off, const int32_t* d_len_a,
-                                 const uint16_t* d_pos, const int32_t* d_lab,
+                                 const uint16_t* d_pos, const void* d_lab,
                                  const int64_t* d_pos_off, const int64_t* d_rows, int64_t n_rows,
                                  const int64_t* d_a_off, const int64_t* d_b_off,
                                  const int64_t* d_l_off, const int64_t* d_npy_off,

@@ -455,6 +455,21 @@ struct WaveRng {
 
 };
 
+// Token ids of the pair tables (the dense kept tokens, the sample tokens and labels): 2 bytes each
+// when the vocab fits uint16 (lddl_ctx::id_bytes), else 4. The hot reader (gather_kernel) is
+// templated on the type; the rare paths read through this runtime-width view.
+struct IdPtr {
+  void* p;
+  int32_t ib;
+  __device__ int32_t ld(int64_t i) const {
+    return ib == 2 ? (int32_t)static_cast<const uint16_t*>(p)[i] : static_cast<const int32_t*>(p)[i];
+  }
+  __device__ void st(int64_t i, int32_t v) const {
+    if (ib == 2) static_cast<uint16_t*>(p)[i] = (uint16_t)v;
+    else static_cast<int32_t*>(p)[i] = v;
+  }
+};
+
 struct PlanArgs {
   // kept corpus
   const int64_t* kscan;  // dense token offset of each kept sentence
@@ -463,7 +478,7 @@ struct PlanArgs {
   const int64_t* kp_off;
   const int64_t* ks_start;  // kept sentence k's pieces at ids[ks_start[k] ...]: the tokenizer's
   const int32_t* ids;       // layout (`dense` is filled by this launch's tail workgroups)
-  int32_t* dense;           // out: kept tokens, packed (densify_group)
+  IdPtr dense;              // out: kept tokens, packed (densify_group)
   int64_t n_kept_sent;
   int32_t n_part, n_dense_wg;  // workgroups >= n_part fill `dense`
   const int64_t* part_seed;
@@ -569,7 +584,7 @@ __device__ int32_t span_token(const PlanArgs& A, int64_t k0, int64_t j) {
 __device__ inline void densify_group(int64_t k0, const int64_t* __restrict__ ks_start,
                                      const int32_t* __restrict__ ks_len,
                                      const int64_t* __restrict__ kscan, int64_t n,
-                                     const int32_t* __restrict__ ids, int32_t* __restrict__ dense) {
+                                     const int32_t* __restrict__ ids, IdPtr dense) {
   const int lane = threadIdx.x & 63;
   const int64_t k = k0 + lane;
   const bool ok = k < n;
@@ -592,7 +607,7 @@ __device__ inline void densify_group(int64_t k0, const int64_t* __restrict__ ks_
       if (x >= b && x < e) src = s + (x - b);
       if (e > hi) break;
     }
-    if (x < total) dense[base + x] = ids[src];
+    if (x < total) dense.st(base + x, ids[src]);
   }
 }
 
@@ -891,7 +906,7 @@ struct NativeArgs {
   const int64_t* kd_off;
   const int64_t* kp_off;
   const int64_t* kscan;
-  const int32_t* dense;
+  IdPtr dense;
   const int64_t* part_seed;
   int64_t n_part, n_units, unit0;  // units dup * (kp_off[0] .. kp_off[n_part])
   uint64_t native_seed, k_short;
@@ -914,7 +929,7 @@ struct NativeArgs {
 
 // token t of the window [front, front + n) of the span starting at kept sentence k
 __device__ inline int32_t win_token(const NativeArgs& A, int64_t k, int32_t front, int32_t t) {
-  return A.dense[A.kscan[k] + front + t];
+  return A.dense.ld(A.kscan[k] + front + t);
 }
 
 // One partition's walk tables: cumulative kept-sentence lengths and document starts, both
@@ -1431,7 +1446,7 @@ __global__ void __launch_bounds__(256) densify_kernel(const int64_t* __restrict_
                                                       const int32_t* __restrict__ ks_len,
                                                       const int64_t* __restrict__ kscan, int64_t n,
                                                       const int32_t* __restrict__ ids,
-                                                      int32_t* __restrict__ dense) {
+                                                      IdPtr dense) {
   const int64_t k0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
   if (k0 >= n) return;
   densify_group(k0, ks_start, ks_len, kscan, n, ids, dense);
@@ -1443,7 +1458,7 @@ struct KeptLen {
 };
 
 struct GatherArgs {
-  const int32_t* dense;  // kept tokens, packed
+  const void* dense;     // kept tokens, packed (IdT)
   const GatherRec* rec;  // per output pair (pair_prep_kernel)
   // masks: positions + replacements at rec.moff (any order; ranks are taken from the bitmap)
   const uint16_t* mpos;
@@ -1452,11 +1467,11 @@ struct GatherArgs {
   int64_t n_pairs;
   const int64_t* tok_off;
   const int64_t* pos_off;
-  int32_t* out_tok;
+  void* out_tok;  // IdT
   int32_t* len_a;
   uint8_t* is_rn;
   uint16_t* out_pos;
-  int32_t* out_lab;
+  void* out_lab;  // IdT
 };
 
 constexpr int kMaxSeqGather = 4096;
@@ -1483,7 +1498,7 @@ struct ResolveArgs {
   const void* jpool;   // 1- or 2-byte draws (the kernel's D)
   uint16_t* mpos;
   const int64_t* kscan;
-  const int32_t* dense;
+  IdPtr dense;
   int32_t cls_id, sep_id;
 };
 
@@ -1594,7 +1609,7 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
     const int64_t ao = R.kscan[d.a_ks] + d.a_front, bo = R.kscan[d.b_ks] + d.b_front;
     int k = 0;
     for (int t = 0; t < na + nb; ++t) {
-      const int32_t tok = t < na ? R.dense[ao + t] : R.dense[bo + (t - na)];
+      const int32_t tok = t < na ? R.dense.ld(ao + t) : R.dense.ld(bo + (t - na));
       if (tok != R.cls_id && tok != R.sep_id) x.set(k++, (uint32_t)(t < na ? t + 1 : t + 2));
     }
     uint16_t* m16 = R.mpos + mb;
@@ -1610,10 +1625,22 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
 // order in the pool) go to a per-pair LDS bitmap + position-indexed decision table; a masked
 // token's rank (its place in the position-sorted masked_lm_positions / labels) is the count of
 // masked tokens before it in the half-wave, from four ballots.
-typedef int32_t tok4_t __attribute__((ext_vector_type(4), aligned(4)));
+// 4 consecutive token ids (one lane's share of a pass): 16 bytes of int32 ids, 8 of uint16 ids
+template <typename IdT>
+struct Tok4;
+template <>
+struct Tok4<int32_t> {
+  typedef int32_t type __attribute__((ext_vector_type(4), aligned(4)));
+};
+template <>
+struct Tok4<uint16_t> {
+  typedef uint16_t type __attribute__((ext_vector_type(4), aligned(2)));
+};
 
-template <int K>
+template <int K, typename IdT>
 __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, GatherLds Lg) {
+  using tok4_t = typename Tok4<IdT>::type;
+  const IdT* __restrict__ dense = static_cast<const IdT*>(G.dense);
   extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, sl = lane & 31;
   const int64_t wg = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
@@ -1655,8 +1682,8 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
     for (int k = 0; k < K; ++k) {
       const int32_t n = na[k] + nb[k];
       tok4_t a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
-      if (x < na[k]) a = *reinterpret_cast<const tok4_t*>(G.dense + aoff[k] + x);
-      if (x + 3 >= na[k] && x < n) b = *reinterpret_cast<const tok4_t*>(G.dense + boff[k] + (x - na[k]));
+      if (x < na[k]) a = *reinterpret_cast<const tok4_t*>(dense + aoff[k] + x);
+      if (x + 3 >= na[k] && x < n) b = *reinterpret_cast<const tok4_t*>(dense + boff[k] + (x - na[k]));
       const int32_t ra = na[k] - x;
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[k][e] = e < ra ? a[e] : b[e];
@@ -1712,16 +1739,16 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
           if (mk[e]) {
             const int32_t xe = x + e, pos = xe < na[k] ? xe + 1 : xe + 2;
             G.out_pos[po[k] + rank] = (uint16_t)pos;
-            G.out_lab[po[k] + rank] = v[k][e];
+            static_cast<IdT*>(G.out_lab)[po[k] + rank] = v[k][e];
             const int32_t d = dec[k][pos];
-            if (d != kKeep) v[k][e] = d;
+            if (d != kKeep) v[k][e] = (IdT)d;
             ++rank;
           }
         }
         rk[k] += tot;
       }
       // non-temporal: the output is streamed, never re-read by this step
-      int32_t* out = G.out_tok + tof[k];
+      IdT* out = static_cast<IdT*>(G.out_tok) + tof[k];
       if (x + 3 < n) {
         __builtin_nontemporal_store(v[k], reinterpret_cast<tok4_t*>(out + x));
       } else {
@@ -1750,7 +1777,7 @@ struct lddl_pairs {
   // views
   int64_t *ks_start = nullptr, *kd_off = nullptr, *kp_off = nullptr, *kscan = nullptr;
   int32_t* ks_len = nullptr;
-  int32_t* dense = nullptr;  // kept tokens, packed in kept-sentence order
+  IdPtr dense{nullptr, 4};  // kept tokens, packed in kept-sentence order (id_bytes each)
   PairDesc* desc = nullptr;
   int32_t *order = nullptr, *nmask = nullptr, *mtok = nullptr;
   uint16_t* mpos = nullptr;
@@ -1984,8 +2011,12 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   LDDL_HIP(hipMemcpyAsync(&max_docs, d_max_docs, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
   // 4 tokens of padding on both sides: the gather's 16-byte loads may overhang a window
-  TRY(P->alloc(&P->dense, n_kept_tok + 8, st));
-  P->dense += 4;
+  {
+    const int32_t ib = c->id_bytes();
+    uint8_t* raw;
+    TRY(P->alloc(&raw, (n_kept_tok + 8) * ib, st));
+    P->dense = IdPtr{raw + 4 * ib, ib};
+  }
   // replay mode: the planner launch's tail workgroups pack `dense` (plan_replay_kernel)
   const bool dense_in_plan = prm->rng == LDDL_RNG_REPLAY && n_part > 0 && !getenv("LDDL_DENSIFY_INLINE");
   if (P->n_kept_sent && !dense_in_plan)
@@ -2285,14 +2316,14 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   return 0;
 }
 
-extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, int64_t* d_tok_off,
-                               int32_t* d_len_a, uint8_t* d_is_rn, uint16_t* d_pos, int32_t* d_lab,
+extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, void* d_tokens, int64_t* d_tok_off,
+                               int32_t* d_len_a, uint8_t* d_is_rn, uint16_t* d_pos, void* d_lab,
                                int64_t* d_pos_off) {
   if (!P) LDDL_FAIL(-1, "null plan");
   hipStream_t st = as_stream(stream);
   if (P->n_pairs == 0) return 0;
   GatherArgs G{};
-  G.dense = P->dense;
+  G.dense = P->dense.p;
   G.rec = P->rec;
   G.mpos = P->mpos;
   G.mtok = P->mtok;
@@ -2314,8 +2345,14 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, int32_t* d_tokens, i
     hipLaunchKernelGGL(kern, dim3((unsigned)gx, (unsigned)((nwg + gx - 1) / gx)), dim3(64 * kGWaves),
                        lds, st, G, Lg);
   };
-  if (P->seq <= 600) launch(gather_kernel<2>, 2);
-  else launch(gather_kernel<1>, 1);  // (LDS: seq-entry decision tables)
+  const bool i16 = P->dense.ib == 2;
+  if (P->seq <= 600) {
+    if (i16) launch(gather_kernel<2, uint16_t>, 2);
+    else launch(gather_kernel<2, int32_t>, 2);
+  } else {  // (LDS: seq-entry decision tables)
+    if (i16) launch(gather_kernel<1, uint16_t>, 1);
+    else launch(gather_kernel<1, int32_t>, 1);
+  }
   LDDL_HIP(hipGetLastError());
   if (d_tok_off)
     LDDL_HIP(hipMemcpyAsync(d_tok_off, P->tok_off, 8 * (P->n_pairs + 1), hipMemcpyDeviceToDevice, st));

@@ -310,7 +310,9 @@ def process_batch(ctx, args, partitions, corpus, outdir, timer=None, executor=No
         return write_txt(outdir, rd, part_rows, index, args.masking, nbins, counts,
                          getattr(args, 'n_partitions', len(part_rows) - 1))
     if copier is not None and args.output_format == 'parquet':
-        return copier.submit(finish, _copy_stream(ctx))
+        fut = copier.submit(finish, _copy_stream(ctx))
+        fut.render_bytes = drd.nbytes  # pinned host bytes until the batch is written
+        return fut
     paths = finish()
     tm('write')
     return paths
@@ -412,9 +414,11 @@ class ShardWriters:
     and closed at once, and close() appends the pieces of each shard, in batch order, into its
     file (the same files, one more pass over the data)."""
 
-    def __init__(self, outdir, nbins, binned, masking, pool, n_local_shards=None, max_open=None):
+    def __init__(self, outdir, nbins, binned, masking, pool, n_local_shards=None, max_open=None,
+                 max_inflight_bytes=8 << 30):
         self.outdir, self.nbins, self.binned, self.masking, self.pool = (outdir, nbins, binned,
                                                                          masking, pool)
+        self.max_inflight_bytes = max_inflight_bytes  # pinned bytes of rendered batches
         self.writers, self.pending, self.shards, self.jobs = {}, [], set(), []
         needed = (n_local_shards or 0) * nbins
         self.pieces = None  # {(shard, bin): [piece paths]} in piece mode
@@ -485,16 +489,18 @@ class ShardWriters:
         if copier is None:
             job()
             return
-        while len(self.jobs) >= 2:
-            self.jobs.pop(0).result()
-        self.jobs.append(copier.submit(job, _copy_stream(ctx)))
+        nb = drd.nbytes
+        while self.jobs and (len(self.jobs) >= 2 or
+                             sum(b for _, b in self.jobs) + nb > self.max_inflight_bytes):
+            self.jobs.pop(0)[0].result()
+        self.jobs.append((copier.submit(job, _copy_stream(ctx)), nb))
 
     def close(self):
         """Finish the writes; shards of a bin that received no rows get an empty file (every bin
         has all shards, as the loader requires)."""
         import pyarrow.parquet as pq
         from ... import output
-        for j in self.jobs:
+        for j, _ in self.jobs:
             j.result()
         self.jobs = []
         for f in self.pending:
@@ -533,6 +539,15 @@ def num_samples_of_shards(shard_counts, binned):
     return out
 
 
+def _default_inflight_bytes():
+    """1/8 of the host's memory, clamped to 2-16 GiB."""
+    try:
+        total = os.sysconf('SC_PAGE_SIZE') * os.sysconf('SC_PHYS_PAGES')
+    except (ValueError, OSError):
+        total = 64 << 30
+    return int(max(2 << 30, min(16 << 30, total // 8)))
+
+
 def _any_rank(flag, device):
     """True when `flag` holds on any rank (all-reduce MAX: RCCL on a device tensor, gloo on the
     host)."""
@@ -550,12 +565,12 @@ def _empty_pairs(ctx, masking):
     from ...pairs import PairBatch
     dev = ctx.device
     e64 = torch.zeros(1, dtype=torch.int64, device=dev)
-    pb = PairBatch(torch.zeros(0, dtype=torch.int32, device=dev), e64,
+    pb = PairBatch(torch.zeros(0, dtype=ctx.id_dtype, device=dev), e64,
                    torch.zeros(0, dtype=torch.int32, device=dev),
                    torch.zeros(0, dtype=torch.uint8, device=dev))
     if masking:
         pb.pos = torch.zeros(0, dtype=torch.int16, device=dev)
-        pb.labels = torch.zeros(0, dtype=torch.int32, device=dev)
+        pb.labels = torch.zeros(0, dtype=ctx.id_dtype, device=dev)
         pb.pos_off = e64.clone()
     return pb
 
@@ -687,7 +702,8 @@ def main(args):
         from ...balance import shard_owner
         writers = ShardWriters(outdir, nbins, binned, args.masking, pool,
                                n_local_shards=int((shard_owner(args.num_shards, world) == rank).sum()),
-                               max_open=args.max_open_files)
+                               max_open=args.max_open_files,
+                               max_inflight_bytes=args.max_inflight_render_bytes)
     copier = ThreadPoolExecutor(max_workers=1)  # device -> host copies of rendered batches
     inflight = []  # (copy future, write futures) of the batches not yet written
     batch_it = iter(batches)
@@ -712,7 +728,10 @@ def main(args):
             if isinstance(job, list):
                 n_files += len(job)
             inflight.append((job, futs))
-            while len(inflight) > 2:  # at most two rendered batches in memory besides this one
+            # at most two rendered batches in host memory besides this one, and no more pinned
+            # bytes than --max-inflight-render-bytes (the newest batch always proceeds)
+            while len(inflight) > 2 or (len(inflight) > 1 and sum(
+                    getattr(j, 'render_bytes', 0) for j, _ in inflight) > args.max_inflight_render_bytes):
                 j, fs = inflight.pop(0)
                 if not isinstance(j, list):
                     n_files += len(j.result())
@@ -762,6 +781,9 @@ def main(args):
         if args.profile_stages:
             print('stage seconds (rank 0): ' + json.dumps(
                 {k: round(v, 3) for k, v in timer.acc.items()}))
+            hs = torch.cuda.host_memory_stats()  # torch's pinned host allocator
+            print('pinned host memory peak (rank 0): {:.2f} GB'.format(max(
+                [v for k, v in hs.items() if 'bytes' in k and k.endswith('peak')] or [0]) / 1e9))
     if world > 1:
         dist.barrier()
     return n_files
@@ -846,6 +868,10 @@ def attach_args(parser=None):
                              "the shards, RCCL exchange; one batch resident); 'reference' writes "
                              "the part files and runs balance_dask_output over them, the "
                              "reference's exact shard layout")
+    parser.add_argument('--max-inflight-render-bytes', type=int, default=_default_inflight_bytes(),
+                        help='pinned host bytes of rendered batches waiting for their parquet '
+                             'writes (default: 1/8 of host memory, 2-16 GiB); the GPU waits for '
+                             'the writes beyond it')
     parser.add_argument('--max-open-files', type=int, default=None,
                         help='--num-shards: most shard files kept open at once (default: as many '
                              'as RLIMIT_NOFILE allows, raised to its hard limit); above it, each '

@@ -119,6 +119,11 @@ class DeviceRendered:
     masking: bool
     event: object = None
 
+    @property
+    def nbytes(self):
+        """Host bytes to_host() pins for this batch."""
+        return sum(t.numel() * t.element_size() for t in (self.cols or {}).values() if t is not None)
+
     def to_host(self, stream=None):
         st = stream if stream is not None else torch.cuda.current_stream()
         if self.event is not None:
@@ -155,6 +160,9 @@ def render_device(ctx, pb, rows=None, bin_id=None):
     dev = ctx.device
     n = pb.n_pairs if rows is None else rows.numel()
     masking = pb.pos is not None
+    if pb.tokens.element_size() != ctx.id_bytes or (masking and pb.labels.element_size() != ctx.id_bytes):
+        raise ValueError('pair table ids are {}-byte, the context renders {}-byte ids'.format(
+            pb.tokens.element_size(), ctx.id_bytes))
     st = _stream()
     a_len = torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n]
     b_len = torch.empty_like(a_len)

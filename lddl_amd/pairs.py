@@ -12,12 +12,20 @@ from ._native import lib, check, PairParams, RNG_REPLAY, RNG_NATIVE
 from .context import _ptr, _stream
 
 
+def _ids(t):
+    """Host copy of an id tensor: int16 storage holds uint16 ids."""
+    a = t.cpu().numpy()
+    return a.view(np.uint16) if a.dtype == np.int16 else a
+
+
 @dataclass
 class PairBatch:
     """Pairs of one batch of partitions, in output order (partition order, then the reference's
     per-partition shuffle). Pair q: tokens[tok_off[q]:tok_off[q]+len_a[q]] is A (after masking),
     the rest up to tok_off[q+1] is B. With static masking, pos[pos_off[q]:pos_off[q+1]] are the
-    masked positions in [CLS] A [SEP] B [SEP] coordinates (sorted) and labels the original ids."""
+    masked positions in [CLS] A [SEP] B [SEP] coordinates (sorted) and labels the original ids.
+    Token ids and labels are uint16 held in int16 tensors when the vocab fits (ctx.id_dtype),
+    else int32; to_host() returns them as uint16 / int32 numpy arrays."""
     tokens: torch.Tensor
     tok_off: torch.Tensor
     len_a: torch.Tensor
@@ -41,7 +49,7 @@ class PairBatch:
         return (self.tok_off[1:] - self.tok_off[:-1]) + 3
 
     def to_host(self):
-        out = dict(tokens=self.tokens.cpu().numpy(), tok_off=self.tok_off.cpu().numpy(),
+        out = dict(tokens=_ids(self.tokens), tok_off=self.tok_off.cpu().numpy(),
                    len_a=self.len_a.cpu().numpy(),
                    is_random_next=self.is_random_next.cpu().numpy().astype(bool))
         out['num_tokens'] = np.diff(out['tok_off']) + 3
@@ -49,7 +57,7 @@ class PairBatch:
             out['part_off'] = self.part_off.cpu().numpy()
         if self.pos is not None:
             out['pos'] = self.pos.cpu().numpy().view(np.uint16)
-            out['labels'] = self.labels.cpu().numpy()
+            out['labels'] = _ids(self.labels)
             out['pos_off'] = self.pos_off.cpu().numpy()
         return out
 
@@ -75,14 +83,14 @@ def make_pairs(ctx, sent_off, ids, sent_len, doc_sent_off, part_doc_off, part_se
                               _ptr(part_seed), n_part, ctypes.byref(h), counts.ctypes.data))
     try:
         n_pairs, n_tok, n_mask = int(counts[0]), int(counts[1]), int(counts[2])
-        tokens = torch.empty(max(n_tok, 1), dtype=torch.int32, device=dev)[:n_tok]
+        tokens = torch.empty(max(n_tok, 1), dtype=ctx.id_dtype, device=dev)[:n_tok]
         tok_off = torch.empty(n_pairs + 1, dtype=torch.int64, device=dev)
         len_a = torch.empty(n_pairs, dtype=torch.int32, device=dev)
         is_rn = torch.empty(n_pairs, dtype=torch.uint8, device=dev)
         pos = labels = pos_off = None
         if masking:
             pos = torch.empty(max(n_mask, 1), dtype=torch.int16, device=dev)[:n_mask]
-            labels = torch.empty(max(n_mask, 1), dtype=torch.int32, device=dev)[:n_mask]
+            labels = torch.empty(max(n_mask, 1), dtype=ctx.id_dtype, device=dev)[:n_mask]
             pos_off = torch.empty(n_pairs + 1, dtype=torch.int64, device=dev)
         check(lib.lddl_pairs_emit(h, st, _ptr(tokens), _ptr(tok_off), _ptr(len_a), _ptr(is_rn),
                                   _ptr(pos), _ptr(labels), _ptr(pos_off)))

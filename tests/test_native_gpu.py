@@ -87,7 +87,7 @@ def test_native_pairs_valid(ctx, seq):
     for p in range(len(part) - 1):
         pdocs = [i for i in range(part[p], part[p + 1]) if len(docs[i])]
         for q in range(po[p], min(po[p + 1], po[p] + 40)):
-            toks = out['tokens'][tok_off[q]:tok_off[q + 1]].copy()
+            toks = out['tokens'][tok_off[q]:tok_off[q + 1]].astype(np.int32)
             na = int(len_a[q])
             nb = len(toks) - na
             assert na >= 1 and nb >= 1 and na + nb <= seq - 3
