@@ -815,7 +815,7 @@ __global__ void __launch_bounds__(64, 6) plan_replay_kernel(PlanArgs A) {
     }
   }
   // random.shuffle(partition_pairs) (pretrain.py:401): record the draws j_i, i = np-1 .. 1
-  // (64 at a time through writelane); apply_shuffle_kernel performs the swaps.
+  // (64 at a time through writelane); shuffle_resolve_kernel resolves the swaps.
   STAMP_ADD(0, st_t);
   {
     int32_t* js = A.jseq + base;
@@ -1294,68 +1294,95 @@ __global__ void __launch_bounds__(256) sum_tokens_kernel(const int32_t* __restri
   if (lane_id() == 0) atomicAdd(out, (unsigned long long)acc);
 }
 
-// Perform the final per-partition Fisher-Yates swaps (draws from plan_replay_kernel). One
-// workgroup per partition: the permutation lives in LDS (Idx = uint16_t when every partition has
-// <= 65536 pairs, else int32_t; cap = the largest partition) and the draws are staged through LDS
-// in coalesced blocks, top down, so the one swapping lane only ever waits on LDS. Partitions
-// beyond `cap` (never, as launched) would use global memory.
-constexpr int kShufStage = 2048;
+// The final per-partition Fisher-Yates swaps (draws from plan_replay_kernel) for partitions too
+// large for shuffle_resolve_kernel's LDS tables: one lane swaps in global memory.
+constexpr int kShufStage = 2048;  // draws staged in LDS per block (shuffle_resolve_kernel)
 
-template <typename Idx>
 __global__ void __launch_bounds__(64) apply_shuffle_kernel(const int64_t* kd_off, const int64_t* kp_off,
                                                           int32_t dup, const int64_t* part_npairs,
-                                                          const int32_t* jseq, int32_t* order,
-                                                          int64_t cap) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sh_smem[];
-  Idx* s_ord = reinterpret_cast<Idx*>(sh_smem);
-  Idx* s_js = s_ord + cap;
+                                                          const int32_t* jseq, int32_t* order) {
   const int p = blockIdx.x;
   const int64_t base = (int64_t)dup * kd_off[kp_off[p]];
   const int64_t np = part_npairs[p];
   const int32_t* js = jseq + base;
   int32_t* ord = order + base;
-  if (np <= cap) {
-    for (int64_t k = threadIdx.x; k < np; k += 64) s_ord[k] = (Idx)k;
-    for (int64_t hi = np - 1; hi > 0; hi -= kShufStage) {
-      const int64_t lo = hi - kShufStage + 1 > 1 ? hi - kShufStage + 1 : 1;
-      __syncthreads();
-      for (int64_t k = lo + threadIdx.x; k <= hi; k += 64) s_js[k - lo] = (Idx)js[k];
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        // the draws of 8 steps are read into registers first (s_js is not written here), so
-        // each swap waits on one LDS round trip (x[i], x[j] together) instead of two
-        int64_t i = hi;
-        for (; i - 7 >= lo; i -= 8) {
-          int32_t jr[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) jr[u] = (int32_t)s_js[i - u - lo];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const Idx t = s_ord[i - u];
-            const Idx v = s_ord[jr[u]];
-            s_ord[jr[u]] = t;
-            s_ord[i - u] = v;
-          }
-        }
-        for (; i >= lo; --i) {
-          const int32_t j = (int32_t)s_js[i - lo];
-          const Idx t = s_ord[i];
-          const Idx v = s_ord[j];
-          s_ord[j] = t;
-          s_ord[i] = v;
-        }
-      }
-    }
-    __syncthreads();
-    for (int64_t k = threadIdx.x; k < np; k += 64) ord[k] = (int32_t)s_ord[k];
-  } else if (threadIdx.x == 0) {
-    for (int64_t k = 0; k < np; ++k) ord[k] = (int32_t)k;
+  for (int64_t k = threadIdx.x; k < np; k += 64) ord[k] = (int32_t)k;
+  __syncthreads();
+  if (threadIdx.x == 0) {
     for (int64_t i = np - 1; i > 0; --i) {
       const int32_t j = js[i];
       const int32_t t = ord[i];
       ord[i] = ord[j];
       ord[j] = t;
     }
+  }
+}
+
+// The same permutation without a sequential swap chain (one workgroup of 256 per partition, for
+// partitions whose tables fit LDS). The backward Fisher-Yates x[i] <-> x[j_i], i = n-1 .. 1, on
+// x = identity leaves, with succ(i) = the next step k > i drawing the same j (j_k = j_i) and
+// first(v) = the first step drawing v:
+//   x[i] = succ(i) ? R(succ(i)) : j_i  (i >= 1),   x[0] = first(0) ? R(first(0)) : 0,
+// where R(k) follows f(k) = (j_k == k ? succ(k) : first(k)) to the end of its chain (the value
+// step k moved out of position k is the one the last earlier-executed step wrote there, and so
+// on). succ / first come from one descending pass (a lane-0 loop whose LDS writes never wait on
+// a read: 4 LDS operations per step instead of two dependent read-write round trips), R by
+// pointer jumping over all threads, the outputs in parallel. apply_shuffle_kernel remains the
+// path for partitions beyond the LDS budget.
+template <typename Idx>
+__global__ void __launch_bounds__(256) shuffle_resolve_kernel(const int64_t* kd_off, const int64_t* kp_off,
+                                                             int32_t dup, const int64_t* part_npairs,
+                                                             const int32_t* jseq, int32_t* order,
+                                                             int64_t cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sr_smem[];
+  constexpr Idx kNone = (Idx)~(Idx)0;
+  Idx* s_succ = reinterpret_cast<Idx*>(sr_smem);
+  Idx* s_r = s_succ + cap;  // last(v) during the pass, then first(v), then f / R
+  Idx* s_js = s_r + cap;    // staged draws (kShufStage)
+  const int p = blockIdx.x;
+  const int64_t base = (int64_t)dup * kd_off[kp_off[p]];
+  const int32_t n = (int32_t)part_npairs[p];
+  const int32_t* js = jseq + base;
+  int32_t* ord = order + base;
+  for (int32_t k = threadIdx.x; k < n; k += 256) s_r[k] = kNone;
+  // descending pass: succ(i) = last(j_i); last(j_i) = i
+  for (int32_t hi = n - 1; hi > 0; hi -= kShufStage) {
+    const int32_t lo = hi - kShufStage + 1 > 1 ? hi - kShufStage + 1 : 1;
+    __syncthreads();
+    for (int32_t k = lo + threadIdx.x; k <= hi; k += 256) s_js[k - lo] = (Idx)js[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int32_t i = hi; i >= lo; --i) {
+        const Idx v = s_js[i - lo];
+        s_succ[i] = s_r[v];
+        s_r[v] = (Idx)i;
+      }
+    }
+  }
+  __syncthreads();
+  // f(k) = j_k == k ? succ(k) : first(k); R(k) = k at a chain's end (in place over first())
+  for (int32_t k = threadIdx.x; k < n; k += 256) {
+    const Idx fk = k == 0 ? kNone : (js[k] == k ? s_succ[k] : s_r[k]);
+    const Idx first0 = k == 0 ? s_r[0] : kNone;  // (read before it is overwritten)
+    if (k == 0) s_succ[0] = first0;  // succ(0) is unused: it keeps first(0)
+    s_r[k] = fk == kNone ? (Idx)k : fk;
+  }
+  __syncthreads();
+  // pointer jumping: R(k) = R(R(k)) until every chain is collapsed
+  for (;;) {
+    int changed = 0;
+    for (int32_t k = threadIdx.x; k < n; k += 256) {
+      const Idx a = s_r[k], b = s_r[a];
+      if (b != a) {
+        s_r[k] = b;
+        changed = 1;
+      }
+    }
+    if (!__syncthreads_or(changed)) break;
+  }
+  for (int32_t k = threadIdx.x; k < n; k += 256) {
+    const Idx sc = s_succ[k];  // (k = 0: first(0))
+    ord[k] = sc != kNone ? (int32_t)s_r[sc] : (k == 0 ? 0 : js[k]);
   }
 }
 
@@ -1875,8 +1902,10 @@ static int plan_native(lddl_pairs* P, lddl_ctx* c, const lddl_pair_params* prm,
   A.ratio = prm->masked_lm_ratio;
   const int64_t nu = A.n_units;
   // walk tables in LDS up to 96 KB per workgroup; larger partitions read a global prefix
-  constexpr int64_t kLdsWordsCap = 24576;
-  const int32_t lds_words = (int32_t)std::min<int64_t>((int64_t)need_max, kLdsWordsCap);
+  int64_t kLdsWordsCap = 24576;
+  if (const char* e = getenv("LDDL_NATIVE_LDS_WORDS")) kLdsWordsCap = atoll(e);  // tests: global path
+  const int32_t lds_words = (int32_t)std::max<int64_t>(
+      1, std::min<int64_t>((int64_t)need_max, kLdsWordsCap));
   int64_t *uoff, *scr, *g_pre = nullptr;
   if ((rc = P->alloc(&A.ucnt, nu, st)) || (rc = P->alloc(&uoff, nu + 1, st)) ||
       (rc = P->alloc(&scr, scan_scratch_elems(std::max(nu, P->n_kept_sent) + 1), st)))
@@ -2034,6 +2063,29 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   }
   P->max_pred = max_pred;
   SlotPool* spool_out = nullptr;  // replay masking: per-slot pool record (pair_prep reads it)
+  // the gather records + output-order scans (tok_off, pos_off) of the plan's pairs
+  int2* pcnt = nullptr;
+  int64_t* scr2 = nullptr;
+  auto alloc_layout = [&](int64_t npairs) -> int {
+    int rc;
+    if ((rc = P->alloc(&P->tok_off, npairs + 1, st)) || (rc = P->alloc(&P->rec, npairs, st)) ||
+        (rc = P->alloc(&pcnt, npairs, st)) || (rc = P->alloc(&scr2, scan_scratch_elems(npairs), st)))
+      return rc;
+    if (prm->masking && (rc = P->alloc(&P->pos_off, npairs + 1, st))) return rc;
+    return 0;
+  };
+  auto prep_and_scan = [&](hipStream_t s, const SlotPool* spool_rec) -> int {
+    const int64_t npairs = P->n_pairs;
+    if (npairs)
+      hipLaunchKernelGGL(pair_prep_kernel, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, s,
+                         P->src, npairs, P->desc, P->kscan, prm->masking ? P->nmask : nullptr,
+                         P->moff, prm->masking && prm->rng != LDDL_RNG_NATIVE ? spool_rec : nullptr,
+                         P->rec, pcnt);
+    LDDL_HIP(hipGetLastError());
+    LDDL_HIP(scan_exclusive(PairTokens{pcnt}, npairs, P->tok_off, scr2, s));
+    if (prm->masking) LDDL_HIP(scan_exclusive(PairMasks{pcnt}, npairs, P->pos_off, scr2, s));
+    return 0;
+  };
   if (prm->rng == LDDL_RNG_NATIVE) {
     TRY(plan_native(P, c, prm, d_part_seed, n_part, st));
   } else {
@@ -2185,22 +2237,19 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
                                                                ? c->lds_per_block - 10 * 1024 : 0);
     const bool force_global = getenv("LDDL_SHUFFLE_GLOBAL") != nullptr;  // tests: the large-partition path
     if (force_global)
-      hipLaunchKernelGGL(apply_shuffle_kernel<int32_t>, dim3((unsigned)n_part), dim3(64),
-                         4 * (size_t)kShufStage, sst, P->kd_off, P->kp_off, prm->dup, part_npairs,
-                         jseq, P->order, (int64_t)0);
-    else if (cap <= 65536 && 2 * (size_t)(cap + kShufStage) <= kLdsBudget)
-      hipLaunchKernelGGL(apply_shuffle_kernel<uint16_t>, dim3((unsigned)n_part), dim3(64),
-                         2 * (size_t)(cap + kShufStage), sst, P->kd_off, P->kp_off, prm->dup,
+      hipLaunchKernelGGL(apply_shuffle_kernel, dim3((unsigned)n_part), dim3(64), 0, sst, P->kd_off,
+                         P->kp_off, prm->dup, part_npairs, jseq, P->order);
+    else if (cap < 65535 && 2 * (size_t)(2 * cap + kShufStage) <= kLdsBudget)
+      hipLaunchKernelGGL(shuffle_resolve_kernel<uint16_t>, dim3((unsigned)n_part), dim3(256),
+                         2 * (size_t)(2 * cap + kShufStage), sst, P->kd_off, P->kp_off, prm->dup,
                          part_npairs, jseq, P->order, cap);
-    else if (4 * (size_t)(cap + kShufStage) <= kLdsBudget)
-      hipLaunchKernelGGL(apply_shuffle_kernel<int32_t>, dim3((unsigned)n_part), dim3(64),
-                         4 * (size_t)(cap + kShufStage), sst, P->kd_off, P->kp_off, prm->dup,
+    else if (4 * (size_t)(2 * cap + kShufStage) <= kLdsBudget)
+      hipLaunchKernelGGL(shuffle_resolve_kernel<int32_t>, dim3((unsigned)n_part), dim3(256),
+                         4 * (size_t)(2 * cap + kShufStage), sst, P->kd_off, P->kp_off, prm->dup,
                          part_npairs, jseq, P->order, cap);
     else  // partitions too large for LDS: swaps in global memory
-      hipLaunchKernelGGL(apply_shuffle_kernel<int32_t>, dim3((unsigned)n_part), dim3(64),
-                         4 * (size_t)kShufStage, sst, P->kd_off, P->kp_off, prm->dup, part_npairs,
-                         jseq, P->order, (int64_t)0);
-    LDDL_HIP(hipEventRecord(ev_shuf, sst));
+      hipLaunchKernelGGL(apply_shuffle_kernel, dim3((unsigned)n_part), dim3(64), 0, sst, P->kd_off,
+                         P->kp_off, prm->dup, part_npairs, jseq, P->order);
   }
   LDDL_HIP(hipGetLastError());
 #ifdef LDDL_STAMPS
@@ -2254,7 +2303,10 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     fprintf(stderr, "\n");
   }
 #endif
-  // layout (part_base and n_pairs came with the planner's sync)
+  // layout (part_base and n_pairs came with the planner's sync): the main stream replays the
+  // masks (fy_resolve, planner order) while the side stream, after the partition shuffle, maps
+  // the output order and builds the gather records and the two output-order scans
+  TRY(alloc_layout(P->n_pairs));
   TRY(P->alloc(&P->src, P->n_pairs, st));
   int64_t* slots = nullptr;  // planner-order slots for the mask replay
   if (prm->masking) TRY(P->alloc(&slots, P->n_pairs, st));
@@ -2275,35 +2327,24 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
                          (size_t)2 * 64 * (size_t)prm->seq, st, RA);
     LDDL_HIP(hipGetLastError());
   }
-  if (n_part) {  // the output order: after the partition shuffle on the side stream
-    LDDL_HIP(hipStreamWaitEvent(st, ev_shuf, 0));
-    hipLaunchKernelGGL(map_pairs_kernel, dim3((unsigned)n_part), dim3(256), 0, st, P->kd_off,
+  hipStream_t lst = n_part ? sst : st;  // the layout's stream
+  if (n_part)  // the output order: after the partition shuffle (side stream)
+    hipLaunchKernelGGL(map_pairs_kernel, dim3((unsigned)n_part), dim3(256), 0, lst, P->kd_off,
                        P->kp_off, prm->dup, part_base, (const int32_t*)P->order, P->src, (int64_t*)nullptr);
-    LDDL_HIP(hipGetLastError());
+  LDDL_HIP(hipGetLastError());
+  TRY(prep_and_scan(lst, spool_out));
+  if (n_part) {
+    LDDL_HIP(hipEventRecord(ev_shuf, sst));
+    LDDL_HIP(hipStreamWaitEvent(st, ev_shuf, 0));
   }
   }  // replay
-  const int64_t npairs = P->n_pairs;
-  TRY(P->alloc(&P->tok_off, npairs + 1, st));
-  TRY(P->alloc(&P->rec, npairs, st));
-  int2* pcnt;
-  TRY(P->alloc(&pcnt, npairs, st));
-  if (npairs)
-    hipLaunchKernelGGL(pair_prep_kernel, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, st,
-                       P->src, npairs, P->desc, P->kscan, prm->masking ? P->nmask : nullptr,
-                       P->moff, prm->masking && prm->rng != LDDL_RNG_NATIVE ? spool_out : nullptr,
-                       P->rec, pcnt);
-  LDDL_HIP(hipGetLastError());
-  int64_t* scr2;
-  TRY(P->alloc(&scr2, scan_scratch_elems(npairs), st));
-  if (scan_exclusive(PairTokens{pcnt}, npairs, P->tok_off, scr2, st) != hipSuccess)
-    TRY(-100);
-  LDDL_HIP(hipMemcpyAsync(&P->n_tokens, P->tok_off + npairs, 8, hipMemcpyDeviceToHost, st));
-  if (prm->masking) {
-    TRY(P->alloc(&P->pos_off, npairs + 1, st));
-    if (scan_exclusive(PairMasks{pcnt}, npairs, P->pos_off, scr2, st) != hipSuccess)
-      TRY(-100);
-    LDDL_HIP(hipMemcpyAsync(&P->n_masked, P->pos_off + npairs, 8, hipMemcpyDeviceToHost, st));
+  if (prm->rng == LDDL_RNG_NATIVE) {
+    TRY(alloc_layout(P->n_pairs));
+    TRY(prep_and_scan(st, nullptr));
   }
+  LDDL_HIP(hipMemcpyAsync(&P->n_tokens, P->tok_off + P->n_pairs, 8, hipMemcpyDeviceToHost, st));
+  if (prm->masking)
+    LDDL_HIP(hipMemcpyAsync(&P->n_masked, P->pos_off + P->n_pairs, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
   if (counts) {
     counts[0] = P->n_pairs;

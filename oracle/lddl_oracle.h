@@ -62,6 +62,16 @@ int64_t orc_partition_pairs(const orc_pair_params* p, int64_t seed, const int64_
                             int32_t* len_a, uint8_t* is_rn, int64_t pair_cap, uint16_t* out_pos,
                             int32_t* out_lab, int64_t pos_cap, int64_t* out_pos_off);
 
+/* The same partition through lddl_amd's native-RNG mode (oracle/native_oracle.c): the reference's
+ * algorithm drawing from Philox4x32-10 streams keyed by (native_seed, part_seed); outputs as
+ * orc_partition_pairs. */
+int64_t orc_partition_pairs_native(const orc_pair_params* p, uint64_t native_seed, int64_t part_seed,
+                                   const int64_t* doc_sent, int64_t n_docs, const int64_t* tok_off,
+                                   const int32_t* ids, int32_t* out_tok, int64_t tok_cap,
+                                   int64_t* out_tok_off, int32_t* len_a, uint8_t* is_rn,
+                                   int64_t pair_cap, uint16_t* out_pos, int32_t* out_lab,
+                                   int64_t pos_cap, int64_t* out_pos_off);
+
 /* Binning (binning.py:63-93): bin id per sample and the stable by-bin row order. */
 /* nltk Punkt sentence spans (PunktSentenceTokenizer.span_tokenize), oracle/punkt_oracle.c.
  * table = lddl_amd/assets/punkt_props.bin; params = records (u8 kind 1 abbrev / 2 sentence

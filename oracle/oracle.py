@@ -41,6 +41,8 @@ def _load():
         'orc_tokenize': (i64, [P, P, P, i64, i32, P, i64, P]),
         'orc_partition_pairs': (i64, [ctypes.POINTER(PairParams), i64, P, i64, P, P, P, i64, P, P,
                                       P, i64, P, P, i64, P]),
+        'orc_partition_pairs_native': (i64, [ctypes.POINTER(PairParams), ctypes.c_uint64, i64, P,
+                                             i64, P, P, P, i64, P, P, P, i64, P, P, i64, P]),
         'orc_bin': (None, [P, i64, i32, i32, P, P, P]),
         'orc_punkt_create': (P, [P, i64, P, i64]),
         'orc_punkt_destroy': (None, [P]),
@@ -142,6 +144,43 @@ def partition_pairs(doc_sent, tok_off, ids, seed, dup, seq, masking, vocab_size,
     n = lib.orc_partition_pairs(ctypes.byref(pp), seed, _p(doc_sent), n_docs, _p(tok_off), _p(ids),
                                 _p(out_tok), tok_cap, _p(out_off), _p(len_a), _p(is_rn), pair_cap,
                                 _p(pos), _p(lab), pos_cap, _p(pos_off) if masking else None)
+    assert n >= 0
+    out = dict(tokens=out_tok[:out_off[n]].copy(), tok_off=out_off[:n + 1].copy(),
+               len_a=len_a[:n].copy(), is_random_next=is_rn[:n].astype(bool))
+    out['num_tokens'] = np.diff(out['tok_off']) + 3
+    if masking:
+        out['pos'] = pos[:pos_off[n]].copy()
+        out['labels'] = lab[:pos_off[n]].copy()
+        out['pos_off'] = pos_off[:n + 1].copy()
+    return out
+
+
+def partition_pairs_native(doc_sent, tok_off, ids, native_seed, part_seed, dup, seq, masking,
+                           vocab_size, cls_id, sep_id, mask_id, short_seq_prob=0.1,
+                           masked_lm_ratio=0.15):
+    """One partition through lddl_amd's native-RNG mode (oracle/native_oracle.c): the reference's
+    algorithm on Philox streams keyed by (native_seed, part_seed); a dict as partition_pairs."""
+    doc_sent = np.ascontiguousarray(doc_sent, np.int64)
+    tok_off = np.ascontiguousarray(tok_off, np.int64)
+    ids = np.ascontiguousarray(ids, np.int32)
+    n_docs = len(doc_sent) - 1
+    n_sent = int(doc_sent[-1] - doc_sent[0])
+    pp = PairParams(dup, seq, int(masking), vocab_size, cls_id, sep_id, mask_id, short_seq_prob,
+                    masked_lm_ratio)
+    pair_cap = dup * max(n_sent, 1) + 16
+    tok_cap = pair_cap * (seq - 3)
+    pos_cap = pair_cap * seq if masking else 0
+    out_tok = np.empty(tok_cap, np.int32)
+    out_off = np.empty(pair_cap + 1, np.int64)
+    len_a = np.empty(pair_cap, np.int32)
+    is_rn = np.empty(pair_cap, np.uint8)
+    pos = np.empty(max(pos_cap, 1), np.uint16)
+    lab = np.empty(max(pos_cap, 1), np.int32)
+    pos_off = np.empty(pair_cap + 1, np.int64)
+    n = lib.orc_partition_pairs_native(
+        ctypes.byref(pp), native_seed & ((1 << 64) - 1), part_seed, _p(doc_sent), n_docs,
+        _p(tok_off), _p(ids), _p(out_tok), tok_cap, _p(out_off), _p(len_a), _p(is_rn), pair_cap,
+        _p(pos), _p(lab), pos_cap, _p(pos_off) if masking else None)
     assert n >= 0
     out = dict(tokens=out_tok[:out_off[n]].copy(), tok_off=out_off[:n + 1].copy(),
                len_a=len_a[:n].copy(), is_random_next=is_rn[:n].astype(bool))

@@ -30,9 +30,20 @@ def ctx():
     return Context(VOCAB_UNCASED, True)
 
 
-def batch(ctx, n_bytes, part_bytes, seed=77):
+def batch(ctx, n_bytes, part_bytes, seed=77, specials_every=0):
+    """specials_every > 0: every that many bytes, a run of 5 lowercase letters in the text is
+    overwritten with a literal [CLS] or [SEP] (sentence boundaries unchanged)."""
     from lddl_amd import synth
     corp = synth.generate(seed=seed, n_bytes=n_bytes, nonascii_frac=0.01, threads=16)
+    if specials_every:
+        t = np.array(corp.text, copy=True)
+        low = (t >= ord('a')) & (t <= ord('z'))
+        for k, at in enumerate(range(0, len(t) - 5, specials_every)):
+            while at < len(t) - 5 and not low[at:at + 5].all():
+                at += 1
+            if at < len(t) - 5:
+                t[at:at + 5] = np.frombuffer(b'[CLS]' if k % 2 else b'[SEP]', np.uint8)
+        corp.text = t
     part = partition_docs(corp, part_bytes)
     seeds = np.arange(len(part) - 1, dtype=np.int64) * 7919 + 12345
     dev = ctx.device
@@ -172,3 +183,51 @@ def test_native_masking_stream_is_separate(ctx):
     np.testing.assert_array_equal(m['len_a'], u['len_a'])
     np.testing.assert_array_equal(m['tok_off'], u['tok_off'])
     assert u.get('pos') is None
+
+
+def _oracle_inputs(b):
+    """The GPU tokenizer's output as the oracle's per-sentence token runs (tokenization parity is
+    tested in test_tokenize_gpu.py)."""
+    ids = b['ids'].cpu().numpy()
+    lens = (b['sent_len'].cpu().numpy() & LEN_MASK).astype(np.int64)
+    so = b['corp'].sent_off
+    tok_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    flat = np.concatenate([ids[so[s]:so[s] + lens[s]] for s in range(len(lens))]
+                          or [np.zeros(0, np.int32)]).astype(np.int32)
+    return tok_off, flat
+
+
+@pytest.mark.parametrize('seq,masking,lds_words', [(128, True, None), (512, True, None),
+                                                   (128, False, None), (128, True, '64')])
+def test_native_bit_exact_vs_oracle(ctx, seq, masking, lds_words, monkeypatch):
+    """rng='native' against the C restatement of the same algorithm and streams
+    (oracle/native_oracle.c): pair windows, truncation, random-next choice, masked positions and
+    decisions and the partition order, bit for bit, partition by partition — with literal
+    [CLS] / [SEP] in the text (the candidate walk) and, with LDDL_NATIVE_LDS_WORDS=64, every
+    partition through the planner's global-prefix path instead of the LDS tables."""
+    from oracle import oracle as O
+    if lds_words:
+        monkeypatch.setenv('LDDL_NATIVE_LDS_WORDS', lds_words)
+    b = batch(ctx, 1_500_000, 200_000, seed=33, specials_every=3000)
+    tok_off, flat = _oracle_inputs(b)
+    assert ((b['sent_len'].cpu().numpy() & (1 << 30)) != 0).sum() > 50  # literal specials kept
+    out = run(ctx, b, seq=seq, masking=masking, native_seed=987654321)
+    part, seeds = b['part'], b['seeds']
+    po = out['part_off']
+    cls_id, sep_id, mask_id = (ctx.vocab[t] for t in ('[CLS]', '[SEP]', '[MASK]'))
+    for p in range(len(part) - 1):
+        ds = b['corp'].doc_sent_off[part[p]:part[p + 1] + 1]
+        exp = O.partition_pairs_native(ds, tok_off, flat, 987654321, int(seeds[p]), 5, seq, masking,
+                                       len(ctx), cls_id, sep_id, mask_id)
+        q0, q1 = po[p], po[p + 1]
+        assert q1 - q0 == len(exp['len_a']), p
+        t0, t1 = out['tok_off'][q0], out['tok_off'][q1]
+        np.testing.assert_array_equal(out['tokens'][t0:t1], exp['tokens'], err_msg=str(p))
+        np.testing.assert_array_equal(np.diff(out['tok_off'][q0:q1 + 1]), np.diff(exp['tok_off']))
+        np.testing.assert_array_equal(out['len_a'][q0:q1], exp['len_a'])
+        np.testing.assert_array_equal(out['is_random_next'][q0:q1], exp['is_random_next'])
+        if masking:
+            m0, m1 = out['pos_off'][q0], out['pos_off'][q1]
+            np.testing.assert_array_equal(out['pos'][m0:m1], exp['pos'])
+            np.testing.assert_array_equal(out['labels'][m0:m1], exp['labels'])
+            np.testing.assert_array_equal(np.diff(out['pos_off'][q0:q1 + 1]), np.diff(exp['pos_off']))
