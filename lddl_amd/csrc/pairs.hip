@@ -815,7 +815,7 @@ __global__ void __launch_bounds__(64, 6) plan_replay_kernel(PlanArgs A) {
     }
   }
   // random.shuffle(partition_pairs) (pretrain.py:401): record the draws j_i, i = np-1 .. 1
-  // (64 at a time through writelane); shuffle_resolve_kernel resolves the swaps.
+  // (64 at a time through writelane); shuffle_sort_kernel resolves the swaps.
   STAMP_ADD(0, st_t);
   {
     int32_t* js = A.jseq + base;
@@ -1295,15 +1295,17 @@ __global__ void __launch_bounds__(256) sum_tokens_kernel(const int32_t* __restri
 }
 
 // The final per-partition Fisher-Yates swaps (draws from plan_replay_kernel) for partitions too
-// large for shuffle_resolve_kernel's LDS tables: one lane swaps in global memory.
-constexpr int kShufStage = 2048;  // draws staged in LDS per block (shuffle_resolve_kernel)
+// large for shuffle_sort_kernel's LDS tables (more than min_np pairs): one lane swaps in global
+// memory.
 
 __global__ void __launch_bounds__(64) apply_shuffle_kernel(const int64_t* kd_off, const int64_t* kp_off,
                                                           int32_t dup, const int64_t* part_npairs,
-                                                          const int32_t* jseq, int32_t* order) {
+                                                          const int32_t* jseq, int32_t* order,
+                                                          int64_t min_np) {
   const int p = blockIdx.x;
   const int64_t base = (int64_t)dup * kd_off[kp_off[p]];
   const int64_t np = part_npairs[p];
+  if (np <= min_np) return;  // (shuffle_sort_kernel's)
   const int32_t* js = jseq + base;
   int32_t* ord = order + base;
   for (int64_t k = threadIdx.x; k < np; k += 64) ord[k] = (int32_t)k;
@@ -1318,71 +1320,111 @@ __global__ void __launch_bounds__(64) apply_shuffle_kernel(const int64_t* kd_off
   }
 }
 
-// The same permutation without a sequential swap chain (one workgroup of 256 per partition, for
-// partitions whose tables fit LDS). The backward Fisher-Yates x[i] <-> x[j_i], i = n-1 .. 1, on
-// x = identity leaves, with succ(i) = the next step k > i drawing the same j (j_k = j_i) and
-// first(v) = the first step drawing v:
+// The same permutation with no sequential chain at all (one workgroup of 1024 per partition of at
+// most `cap` pairs; larger ones go to apply_shuffle_kernel). The backward Fisher-Yates
+// x[i] <-> x[j_i], i = n-1 .. 1, on x = identity leaves, with succ(i) = the next step k > i that
+// drew the same j (j_k = j_i) and first(v) = the first step that drew v:
 //   x[i] = succ(i) ? R(succ(i)) : j_i  (i >= 1),   x[0] = first(0) ? R(first(0)) : 0,
 // where R(k) follows f(k) = (j_k == k ? succ(k) : first(k)) to the end of its chain (the value
 // step k moved out of position k is the one the last earlier-executed step wrote there, and so
-// on). succ / first come from one descending pass (a lane-0 loop whose LDS writes never wait on
-// a read: 4 LDS operations per step instead of two dependent read-write round trips), R by
-// pointer jumping over all threads, the outputs in parallel. apply_shuffle_kernel remains the
-// path for partitions beyond the LDS budget.
-template <typename Idx>
-__global__ void __launch_bounds__(256) shuffle_resolve_kernel(const int64_t* kd_off, const int64_t* kp_off,
-                                                             int32_t dup, const int64_t* part_npairs,
-                                                             const int32_t* jseq, int32_t* order,
-                                                             int64_t cap) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sr_smem[];
-  constexpr Idx kNone = (Idx)~(Idx)0;
-  Idx* s_succ = reinterpret_cast<Idx*>(sr_smem);
-  Idx* s_r = s_succ + cap;  // last(v) during the pass, then first(v), then f / R
-  Idx* s_js = s_r + cap;    // staged draws (kShufStage)
+// on). succ and first come from a bucket sort of the steps by their draw (LDS counters, a block
+// scan, a scatter, then each bucket - a few steps on average - sorted by step), R from pointer
+// jumping, everything over 1024 threads. LDS: three 16-bit arrays of n (the draws are read from
+// global memory once, coalesced, into the one that later holds f and R).
+__device__ inline uint32_t lds_add16(uint32_t* words, uint32_t v) {  // 16-bit counters, packed
+  const uint32_t sh = 16u * (v & 1u);
+  return (atomicAdd(&words[v >> 1], 1u << sh) >> sh) & 0xFFFFu;
+}
+
+constexpr int kShufThreads = 1024;  // one block per CU (its LDS): 16 waves hide the latencies
+__global__ void __launch_bounds__(kShufThreads) shuffle_sort_kernel(const int64_t* kd_off, const int64_t* kp_off,
+                                                          int32_t dup, const int64_t* part_npairs,
+                                                          const int32_t* __restrict__ jseq,
+                                                          int32_t* __restrict__ order, int32_t cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t ss_smem[];
   const int p = blockIdx.x;
-  const int64_t base = (int64_t)dup * kd_off[kp_off[p]];
   const int32_t n = (int32_t)part_npairs[p];
-  const int32_t* js = jseq + base;
-  int32_t* ord = order + base;
-  for (int32_t k = threadIdx.x; k < n; k += 256) s_r[k] = kNone;
-  // descending pass: succ(i) = last(j_i); last(j_i) = i
-  for (int32_t hi = n - 1; hi > 0; hi -= kShufStage) {
-    const int32_t lo = hi - kShufStage + 1 > 1 ? hi - kShufStage + 1 : 1;
+  if (n > cap) return;  // (apply_shuffle_kernel's)
+  const int32_t capw = (cap + 2) & ~1;
+  uint32_t* cntw = reinterpret_cast<uint32_t*>(ss_smem);        // bucket counters -> ends
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(ss_smem);
+  uint16_t* srt = reinterpret_cast<uint16_t*>(ss_smem) + capw;  // steps by bucket
+  uint16_t* r = srt + capw;                                     // j, then f, then R
+  const int64_t base = (int64_t)dup * kd_off[kp_off[p]];
+  const int32_t* __restrict__ js = jseq + base;
+  // succ(i) (or ~j_i when step i is the last to draw j_i), then the permutation
+  int32_t* __restrict__ ord = order + base;
+  const int tid = threadIdx.x;
+  for (int32_t w = tid; w < capw / 2; w += kShufThreads) cntw[w] = 0u;
+  for (int32_t i = tid; i < n; i += kShufThreads) r[i] = (uint16_t)js[i];
+  __syncthreads();
+  for (int32_t i = 1 + tid; i < n; i += kShufThreads) (void)lds_add16(cntw, r[i]);
+  __syncthreads();
+  {  // exclusive scan of the counts: a run per thread, then the runs' sums
+    __shared__ int32_t s_w[kShufThreads / 64];
+    const int32_t per = (n + kShufThreads - 1) / kShufThreads;
+    const int32_t x0 = tid * per, x1 = min(x0 + per, n);
+    int32_t run = 0;
+    for (int32_t x = x0; x < x1; ++x) run += cnt[x];
+    const int32_t inc = wave_incl_scan(run);
+    if ((tid & 63) == 63) s_w[tid >> 6] = inc;
     __syncthreads();
-    for (int32_t k = lo + threadIdx.x; k <= hi; k += 256) s_js[k - lo] = (Idx)js[k];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int32_t i = hi; i >= lo; --i) {
-        const Idx v = s_js[i - lo];
-        s_succ[i] = s_r[v];
-        s_r[v] = (Idx)i;
-      }
+    int32_t off = inc - run;
+    for (int w = 0; w < (tid >> 6); ++w) off += s_w[w];
+    for (int32_t x = x0; x < x1; ++x) {
+      const int32_t c = cnt[x];
+      cnt[x] = (uint16_t)off;
+      off += c;
     }
   }
   __syncthreads();
-  // f(k) = j_k == k ? succ(k) : first(k); R(k) = k at a chain's end (in place over first())
-  for (int32_t k = threadIdx.x; k < n; k += 256) {
-    const Idx fk = k == 0 ? kNone : (js[k] == k ? s_succ[k] : s_r[k]);
-    const Idx first0 = k == 0 ? s_r[0] : kNone;  // (read before it is overwritten)
-    if (k == 0) s_succ[0] = first0;  // succ(0) is unused: it keeps first(0)
-    s_r[k] = fk == kNone ? (Idx)k : fk;
+  for (int32_t i = 1 + tid; i < n; i += kShufThreads) srt[lds_add16(cntw, r[i])] = (uint16_t)i;
+  __syncthreads();  // cnt[v] = the end of bucket v now
+  // each bucket sorted by step (insertion sort: a few entries), succ along it
+  for (int32_t v = tid; v < n; v += kShufThreads) {
+    const int32_t lo = v ? cnt[v - 1] : 0, hi = cnt[v];
+    for (int32_t m = lo + 1; m < hi; ++m) {
+      const uint16_t e = srt[m];
+      int32_t y = m - 1;
+      while (y >= lo && srt[y] > e) {
+        srt[y + 1] = srt[y];
+        --y;
+      }
+      srt[y + 1] = e;
+    }
+    for (int32_t m = lo; m < hi; ++m) ord[srt[m]] = m + 1 < hi ? (int32_t)srt[m + 1] : ~v;
   }
   __syncthreads();
-  // pointer jumping: R(k) = R(R(k)) until every chain is collapsed
-  for (;;) {
+  // f(k) = j_k == k ? succ(k) : first(k); R(k) = k at a chain's end (each thread reads the
+  // draws it overwrites)
+  for (int32_t k = tid; k < n; k += kShufThreads) {
+    int32_t f = -1;
+    if (k > 0) {
+      if (r[k] == k) {
+        f = ord[k];
+      } else {
+        const int32_t lo = cnt[k - 1], hi = cnt[k];
+        f = lo < hi ? (int32_t)srt[lo] : -1;
+      }
+    }
+    r[k] = (uint16_t)(f < 0 ? k : f);
+  }
+  __syncthreads();
+  for (;;) {  // pointer jumping: R(k) = R(R(k)) until every chain is collapsed
     int changed = 0;
-    for (int32_t k = threadIdx.x; k < n; k += 256) {
-      const Idx a = s_r[k], b = s_r[a];
+    for (int32_t k = tid; k < n; k += kShufThreads) {
+      const uint16_t a = r[k], b = r[a];
       if (b != a) {
-        s_r[k] = b;
+        r[k] = b;
         changed = 1;
       }
     }
     if (!__syncthreads_or(changed)) break;
   }
-  for (int32_t k = threadIdx.x; k < n; k += 256) {
-    const Idx sc = s_succ[k];  // (k = 0: first(0))
-    ord[k] = sc != kNone ? (int32_t)s_r[sc] : (k == 0 ? 0 : js[k]);
+  const int32_t first0 = n > 1 && cnt[0] > 0 ? (int32_t)srt[0] : -1;
+  for (int32_t k = tid; k < n; k += kShufThreads) {
+    const int32_t sc = k == 0 ? first0 : ord[k];
+    ord[k] = sc >= 0 ? (int32_t)r[sc] : (k == 0 ? 0 : ~sc);
   }
 }
 
@@ -2216,9 +2258,9 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     cap = (int64_t)ctl[0] + 1024;
     jcap = (int64_t)ctl[2] + 1024;
   }
-  // random.shuffle(partition_pairs): the swaps run on the context's side stream, beside the mask
-  // replay (fy_resolve_kernel needs only the planner-order slots); the main stream waits for them
-  // before the output order (src) is built
+  // random.shuffle(partition_pairs), alone on the main stream (its blocks need 16 waves and
+  // ~90 KB of LDS per CU: beside fy_resolve's small blocks they waited for CUs to drain, 10.3 ms
+  // against ~2 alone); then the layout forks onto the context's side stream
   hipStream_t sst = nullptr;
   hipEvent_t ev_plan = nullptr, ev_shuf = nullptr;
   if (n_part) {
@@ -2228,28 +2270,24 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
             ? 0 : (set_error("side stream"), -100));
     ev_plan = P->ev[2];
     ev_shuf = P->ev[3];
-    LDDL_HIP(hipEventRecord(ev_plan, st));
-    LDDL_HIP(hipStreamWaitEvent(sst, ev_plan, 0));
     const int64_t cap = max_np;
     // dynamic-LDS budget of the swap kernel: what the device grants a block (160 KiB on
     // gfx950), minus headroom for the kernel's static LDS
     const size_t kLdsBudget = std::min<size_t>(150 * 1024, c->lds_per_block > 10 * 1024
                                                                ? c->lds_per_block - 10 * 1024 : 0);
     const bool force_global = getenv("LDDL_SHUFFLE_GLOBAL") != nullptr;  // tests: the large-partition path
-    if (force_global)
-      hipLaunchKernelGGL(apply_shuffle_kernel, dim3((unsigned)n_part), dim3(64), 0, sst, P->kd_off,
-                         P->kp_off, prm->dup, part_npairs, jseq, P->order);
-    else if (cap < 65535 && 2 * (size_t)(2 * cap + kShufStage) <= kLdsBudget)
-      hipLaunchKernelGGL(shuffle_resolve_kernel<uint16_t>, dim3((unsigned)n_part), dim3(256),
-                         2 * (size_t)(2 * cap + kShufStage), sst, P->kd_off, P->kp_off, prm->dup,
-                         part_npairs, jseq, P->order, cap);
-    else if (4 * (size_t)(2 * cap + kShufStage) <= kLdsBudget)
-      hipLaunchKernelGGL(shuffle_resolve_kernel<int32_t>, dim3((unsigned)n_part), dim3(256),
-                         4 * (size_t)(2 * cap + kShufStage), sst, P->kd_off, P->kp_off, prm->dup,
-                         part_npairs, jseq, P->order, cap);
-    else  // partitions too large for LDS: swaps in global memory
-      hipLaunchKernelGGL(apply_shuffle_kernel, dim3((unsigned)n_part), dim3(64), 0, sst, P->kd_off,
-                         P->kp_off, prm->dup, part_npairs, jseq, P->order);
+    // partitions of <= cap_lds pairs: the parallel bucket-sort resolve (three 16-bit LDS tables);
+    // larger ones: one lane swapping in global memory
+    const int64_t cap_lds = force_global ? 0 : std::min<int64_t>({cap, 65534, (int64_t)(kLdsBudget / 6) - 2});
+    if (cap_lds > 0)
+      hipLaunchKernelGGL(shuffle_sort_kernel, dim3((unsigned)n_part), dim3(kShufThreads),
+                         (size_t)6 * (size_t)((cap_lds + 2) & ~1), st, P->kd_off, P->kp_off,
+                         prm->dup, part_npairs, jseq, P->order, (int32_t)cap_lds);
+    if (cap > cap_lds)
+      hipLaunchKernelGGL(apply_shuffle_kernel, dim3((unsigned)n_part), dim3(64), 0, st, P->kd_off,
+                         P->kp_off, prm->dup, part_npairs, jseq, P->order, cap_lds);
+    LDDL_HIP(hipEventRecord(ev_plan, st));
+    LDDL_HIP(hipStreamWaitEvent(sst, ev_plan, 0));
   }
   LDDL_HIP(hipGetLastError());
 #ifdef LDDL_STAMPS
@@ -2304,8 +2342,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   }
 #endif
   // layout (part_base and n_pairs came with the planner's sync): the main stream replays the
-  // masks (fy_resolve, planner order) while the side stream, after the partition shuffle, maps
-  // the output order and builds the gather records and the two output-order scans
+  // masks (fy_resolve, planner order) while the side stream maps the output order and builds the
+  // gather records and the two output-order scans
   TRY(alloc_layout(P->n_pairs));
   TRY(P->alloc(&P->src, P->n_pairs, st));
   int64_t* slots = nullptr;  // planner-order slots for the mask replay

@@ -274,19 +274,6 @@ __device__ inline bool tail_match(const Tables& T, int32_t id, const B32& a, int
 
 // Vocab probe of the first `len` (1..32) bytes of a: exact key for <= 12 bytes (k0 = bytes 0..7,
 // k1 = bytes 8..11), longer pieces confirmed against their 32-byte copies.
-__device__ inline int32_t probe32(const Tables& T, const B32& a, int len, uint32_t cont) {
-  const uint64_t k0 = keep_bytes(a.w0, len);
-  const uint32_t k1 = (uint32_t)keep_bytes(a.w1, len - 8 < 4 ? len - 8 : 4);
-  const uint32_t want = kMetaValid | (cont ? kMetaCont : 0u) | (len > 12 ? kMetaLong : 0u) |
-                        ((uint32_t)len << 21);
-  for (uint32_t slot = (uint32_t)vhash(k0, k1, len, cont) & T.vmask;; slot = (slot + 1) & T.vmask) {
-    const VEnt e = T.vhash[slot];
-    if (!(e.meta & kMetaValid)) return -1;
-    if (e.k0 == k0 && e.k1 == k1 && (e.meta & ~0x1FFFFFu) == want &&
-        (len <= 12 || tail_match(T, meta_id(e.meta), a, len)))
-      return meta_id(e.meta);
-  }
-}
 
 // probe32 split in two, so that several probes' first table loads are in flight together:
 // probe_first computes the key and issues the load of the home slot, probe_finish examines it
@@ -339,8 +326,11 @@ __device__ inline uint32_t bloom_candidates32(const uint32_t* bloom, const B32& 
 // Greedy longest-match WordPiece (HF WordPiece::tokenize) of a normalised word of nb <= 32 bytes
 // held in registers. ends: bit e set iff a piece may end at byte e (a UTF-8 character boundary;
 // all bits for ASCII). Returns the piece count written to pc, or -1 if more than kPcs pieces.
-// The longest candidate is probed first (most words are one piece); when it misses, the Bloom
-// filter (LDS) rules out the shorter lengths that cannot be pieces.
+// Per piece, the Bloom filter (LDS) gives the lengths that may be pieces (every vocab piece is in
+// it: the longest candidate that hits is the greedy match), and the two longest candidates' home
+// slots are loaded together: a lane waits on ONE table round trip per piece in the common case.
+// (Round 3 probed the full length alone first, then two candidates per round trip: 21.9 ms per
+// 2 GiB against 20.7 now; three candidates per trip spilled VGPRs and took 22.1 ms, r04o.)
 __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v, int nb,
                            uint64_t ends, Pcs& pc, bool first_probe_missed = false) {
   int n = 0, start = 0;
@@ -353,33 +343,29 @@ __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v,
       const uint64_t okl = (e >> 1) & ((1ull << len) - 1ull);
       len = okl ? 64 - __clzll(okl) : 0;
     }
+    uint32_t cand = len > 0 ? bloom_candidates32(bloom, a, len, cont) & (uint32_t)(e >> 1) : 0u;
     // (the caller may already know that the whole word is not one piece)
-    int32_t id = len > 0 && !(first_probe_missed && start == 0 && len == nb) ? probe32(T, a, len, cont)
-                                                                              : -1;
-    if (id < 0 && len > 1) {
-      uint32_t cand = bloom_candidates32(bloom, a, len - 1, cont) & (uint32_t)(e >> 1);
-      // the two longest remaining candidates' home slots are loaded together (the chain of
-      // dependent table loads per piece is what a lane waits on), the longer one decides first
-      while (cand) {
-        const int l1 = 32 - __clz(cand);
-        const uint32_t rest = cand & ~(1u << (l1 - 1));
-        const int l2 = rest ? 32 - __clz(rest) : 0;
-        const Probe q1 = probe_first(T, a, l1, cont);
-        const Probe q2 = probe_first(T, a, l2 ? l2 : l1, cont);
-        id = probe_finish(T, a, l1, q1);
+    if (first_probe_missed && start == 0 && len == nb) cand &= ~(1u << (len - 1));
+    int32_t id = -1;
+    while (cand) {
+      const int l1 = 32 - __clz(cand);
+      const uint32_t r1 = cand & ~(1u << (l1 - 1));
+      const int l2 = r1 ? 32 - __clz(r1) : 0;
+      const Probe q1 = probe_first(T, a, l1, cont);
+      const Probe q2 = probe_first(T, a, l2 ? l2 : l1, cont);
+      id = probe_finish(T, a, l1, q1);
+      if (id >= 0) {
+        len = l1;
+        break;
+      }
+      if (l2) {
+        id = probe_finish(T, a, l2, q2);
         if (id >= 0) {
-          len = l1;
+          len = l2;
           break;
         }
-        if (l2) {
-          id = probe_finish(T, a, l2, q2);
-          if (id >= 0) {
-            len = l2;
-            break;
-          }
-        }
-        cand = l2 ? rest & ~(1u << (l2 - 1)) : 0u;
       }
+      cand = l2 ? r1 & ~(1u << (l2 - 1)) : 0u;
     }
     if (id < 0) {  // no piece: the whole word is [UNK]
       pc.put(0, T.special_id[kUnk]);
