@@ -145,6 +145,16 @@ struct Philox {
 // directly (HIP's __ballot(int) re-materialises it through a compare against zero).
 __device__ inline uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
+// Workgroup b of a launch of nb as the logical block that keeps each XCD's share contiguous:
+// the dispatcher deals workgroups round-robin over the 8 XCDs (b and b + 8 share one XCD and its
+// L2; MI355X_MICROARCH.md, workgroup dispatch), so consecutive logical blocks - e.g. the pairs
+// of one partition, which re-read the same dense tokens and mask pool lines - meet in one L2
+// instead of eight. A bijection on [0, nb); placement only, never correctness.
+__device__ inline int64_t xcd_block(int64_t b, int64_t nb) {
+  const int64_t per = nb >> 3, rem = nb & 7, x = b & 7;
+  return x * per + (x < rem ? x : rem) + (b >> 3);
+}
+
 // Set bits of m below the calling lane (v_mbcnt).
 __device__ inline uint32_t popc_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));

@@ -1478,7 +1478,8 @@ __global__ void __launch_bounds__(256) pair_prep_kernel(const int64_t* __restric
                                                         const SlotPool* __restrict__ spool,
                                                         GatherRec* __restrict__ rec,
                                                         int2* __restrict__ cnt) {
-  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // (XCD-contiguous blocks: a partition's pairs share one L2 for its descriptors and offsets)
+  const int64_t q = xcd_block(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
   if (q >= n) return;
   const int64_t slot = src[q];
   const PairDesc d = desc[slot];
@@ -1541,16 +1542,20 @@ struct GatherArgs {
   uint8_t* is_rn;
   uint16_t* out_pos;
   void* out_lab;  // IdT
+  int64_t* out_tok_off;  // the caller's copies of tok_off / pos_off (may be null)
+  int64_t* out_pos_off;
 };
 
 constexpr int kMaxSeqGather = 4096;
 constexpr int kGWaves = 4;
 
-// LDS of the gather per pair in flight: the masked-position bitmap (W words, bit = position - 1)
-// and the decisions indexed by position.
+// LDS of the gather per pair in flight: the decision table indexed by output token x (seqp =
+// seq rounded up to 128 entries of int32, kNoMask where x is not masked) and the staging rows
+// of one pass's masked positions and labels by rank (128 each).
+constexpr int32_t kNoMask = INT32_MIN;
 struct GatherLds {
-  int32_t W, seq;
-  __host__ __device__ size_t per_pair() const { return ((size_t)4 * W + (size_t)4 * seq + 15) & ~(size_t)15; }
+  int32_t seqp;
+  __host__ __device__ size_t per_pair() const { return (size_t)4 * seqp + 128 * 2 + 128 * 4; }
 };
 
 // Replay masks, off the planner's sequential chain: one LANE per pair replays the recorded swaps
@@ -1689,11 +1694,16 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
 // Gather: each half-wave emits K output pairs, 4 consecutive tokens per lane (128 per pass), so
 // a wave has 2K pairs in flight with all their parameters in vector registers. Per pair:
 // A = dense[kscan[a_ks] + a_front ..+ na), B likewise; output token x < na + nb comes from A
-// (x < na, position x + 1) or B (position x + 2); a lane's 4 tokens are one 16-byte load and one
-// 16-byte non-temporal store except where they straddle A/B or the end. The pair's masks (any
-// order in the pool) go to a per-pair LDS bitmap + position-indexed decision table; a masked
-// token's rank (its place in the position-sorted masked_lm_positions / labels) is the count of
-// masked tokens before it in the half-wave, from four ballots.
+// (x < na, position x + 1) or B (position x + 2); a lane's 4 tokens are one 8- or 16-byte load
+// and one non-temporal store except where they straddle A/B or the end. The pair's masks (pool,
+// any order) fill a per-pair LDS decision table indexed by x (one plain LDS store per mask);
+// each lane reads its 4 entries with one 16-byte LDS load. A masked token's rank (its place in
+// the position-sorted masked_lm_positions / labels) is the half-wave's exclusive scan of the
+// lanes' masked counts (one DPP scan for all K pairs, counts packed 16 bits apart) plus the
+// masked elements before it in the lane; (position, label) go to an LDS staging row by rank and
+// leave as two coalesced stores per pass (round 3 issued eight lane-masked 2-byte stores per
+// pass from four ballots per element: that mask path was half the kernel, profiles/r04t_*).
+// The caller's tok_off / pos_off are written here too (no device-to-device copies).
 // 4 consecutive token ids (one lane's share of a pass): 16 bytes of int32 ids, 8 of uint16 ids
 template <typename IdT>
 struct Tok4;
@@ -1708,18 +1718,21 @@ struct Tok4<uint16_t> {
 
 template <int K, typename IdT>
 __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, GatherLds Lg) {
+  static_assert(K == 1 || K == 2, "masked counts of K pairs are packed 16 bits apart");
   using tok4_t = typename Tok4<IdT>::type;
   const IdT* __restrict__ dense = static_cast<const IdT*>(G.dense);
   extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, sl = lane & 31;
-  const int64_t wg = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  // XCD-contiguous blocks: the pairs of one partition (which read its dense tokens dup times over)
+  // and their mask pool lines meet in one L2
+  const int64_t wg = xcd_block((int64_t)blockIdx.y * gridDim.x + blockIdx.x, (int64_t)gridDim.x * gridDim.y);
   const int64_t q0 = (wg * kGWaves + w) * 2 * K;  // pairs q0 + 2k + h
-  const int W = Lg.W;
 
   int64_t tof[K], aoff[K], boff[K], po[K], mb[K];
   int32_t na[K], nb[K], rk[K], nm[K];
-  uint32_t* bm[K];
   int32_t* dec[K];
+  uint16_t* spos[K];
+  IdT* slab[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int64_t q = q0 + 2 * k + h;
@@ -1736,16 +1749,25 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
     po[k] = (G.masking && act) ? G.pos_off[q] : 0;
     rk[k] = 0;
     uint8_t* pb = g_smem + (((size_t)w * K + k) * 2 + h) * Lg.per_pair();
-    bm[k] = reinterpret_cast<uint32_t*>(pb);
-    dec[k] = reinterpret_cast<int32_t*>(pb + 4 * (size_t)W);
+    dec[k] = reinterpret_cast<int32_t*>(pb);
+    spos[k] = reinterpret_cast<uint16_t*>(pb + 4 * (size_t)Lg.seqp);
+    slab[k] = reinterpret_cast<IdT*>(pb + 4 * (size_t)Lg.seqp + 256);
     if (sl == 0 && act) {
       G.len_a[q] = na[k];
       G.is_rn[q] = (uint8_t)((uint32_t)r.nb_rn >> 31);
+      if (G.out_tok_off) {
+        G.out_tok_off[q] = tof[k];
+        if (q + 1 == G.n_pairs) G.out_tok_off[q + 1] = tof[k] + na[k] + nb[k];
+      }
+      if (G.out_pos_off && G.masking) {
+        G.out_pos_off[q] = po[k];
+        if (q + 1 == G.n_pairs) G.out_pos_off[q + 1] = po[k] + nm[k];
+      }
     }
   }
-  // a lane's 4 tokens: one 16-byte load from A (x < na) and/or one from B (x + 3 >= na), each
-  // at the offset of token x in that window (dense is padded by 4 tokens on both sides, so a
-  // load overhanging its window stays in bounds); element e comes from A iff x + e < na
+  // a lane's 4 tokens: one load from A (x < na) and/or one from B (x + 3 >= na), each at the
+  // offset of token x in that window (dense is padded by 4 tokens on both sides, so a load
+  // overhanging its window stays in bounds); element e comes from A iff x + e < na
   auto load_tokens = [&](int32_t x, tok4_t* v) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -1759,18 +1781,18 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
     }
   };
   tok4_t v[K];
-  load_tokens(4 * sl, v);  // the first pass's tokens are in flight while the mask tables fill
+  load_tokens(4 * sl, v);  // the first pass's tokens are in flight while the tables fill
   if (G.masking) {
 #pragma unroll
     for (int k = 0; k < K; ++k)
-      for (int i = sl; i < W; i += 32) bm[k][i] = 0u;
+      for (int i = 4 * sl; i < Lg.seqp; i += 128)
+        *reinterpret_cast<int4*>(dec[k] + i) = make_int4(kNoMask, kNoMask, kNoMask, kNoMask);
     wave_sync();
 #pragma unroll
     for (int k = 0; k < K; ++k)
       for (int j = sl; j < nm[k]; j += 32) {
-        const int p = G.mpos[mb[k] + j];
-        atomicOr(&bm[k][(p - 1) >> 5], 1u << ((p - 1) & 31));
-        dec[k][p] = G.mtok[mb[k] + j];
+        const int p = G.mpos[mb[k] + j];  // position in [CLS] A [SEP] B [SEP]: never a literal
+        dec[k][p <= na[k] ? p - 1 : p - 2] = G.mtok[mb[k] + j];
       }
     wave_sync();
   }
@@ -1778,44 +1800,52 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
     const int32_t x = cb + 4 * sl;
     if (cb > 0) load_tokens(x, v);
     bool more = false;
+    if (G.masking) {
+      int4 d4[K];
+      uint32_t m4[K], packed = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int32_t n = na[k] + nb[k];
-      if (G.masking) {
-        // bits x .. x+4 of the bitmap (x is a multiple of 4: they span words x/32 and x/32 + 1
-        // only when x % 32 == 28); element e is bit x + e (A) or x + e + 1 (B)
-        const int wi = x >> 5;
-        uint32_t win = bm[k][wi] >> (x & 31);
-        if ((x & 31) == 28) win |= (wi + 1 < W ? bm[k][wi + 1] : 0u) << 4;
-        const int32_t ra = na[k] - x, rn_ = n - x;
-        const uint32_t am = ra >= 4 ? 0xFu : ra <= 0 ? 0u : ((1u << ra) - 1u);
-        const uint32_t vm = rn_ >= 4 ? 0xFu : rn_ <= 0 ? 0u : ((1u << rn_) - 1u);
-        const uint32_t m4 = ((win & am) | ((win >> 1) & ~am)) & vm;
-        bool mk[4];
-        int rank = rk[k], tot = 0;
+      for (int k = 0; k < K; ++k) {  // (x < seqp: every pass starts below the longest pair)
+        d4[k] = *reinterpret_cast<const int4*>(dec[k] + x);
+        m4[k] = (d4[k].x != kNoMask ? 1u : 0u) | (d4[k].y != kNoMask ? 2u : 0u) |
+                (d4[k].z != kNoMask ? 4u : 0u) | (d4[k].w != kNoMask ? 8u : 0u);
+        packed |= (uint32_t)__popc(m4[k]) << (16 * k);
+      }
+      // per half-wave exclusive scan of the packed counts (<= 128 per pair and pass)
+      const uint32_t inc = wave_incl_scan(packed);
+      const uint32_t lo_tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 31);
+      const uint32_t all_tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+      const uint32_t excl = inc - packed - (h ? lo_tot : 0u);
+      const uint32_t tots = h ? all_tot - lo_tot : lo_tot;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          mk[e] = (m4 >> e) & 1u;
-          const uint64_t M = ballot(mk[e]);
-          const uint32_t lo = (uint32_t)M, hi = (uint32_t)(M >> 32);
-          const int plo = __popc(lo), phi = __popc(hi);  // wave-uniform
-          // masked elements in the lanes before this one, minus the lower half's for the upper
-          rank += (int)__builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u)) - (h ? plo : 0);
-          tot += h ? phi : plo;
-        }
+      for (int k = 0; k < K; ++k) {
+        int32_t r = (int32_t)((excl >> (16 * k)) & 0xFFFFu);
+        const int32_t dd[4] = {d4[k].x, d4[k].y, d4[k].z, d4[k].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if (mk[e]) {
-            const int32_t xe = x + e, pos = xe < na[k] ? xe + 1 : xe + 2;
-            G.out_pos[po[k] + rank] = (uint16_t)pos;
-            static_cast<IdT*>(G.out_lab)[po[k] + rank] = v[k][e];
-            const int32_t d = dec[k][pos];
-            if (d != kKeep) v[k][e] = (IdT)d;
-            ++rank;
+          if ((m4[k] >> e) & 1u) {
+            const int32_t xe = x + e;
+            spos[k][r] = (uint16_t)(xe < na[k] ? xe + 1 : xe + 2);
+            slab[k][r] = v[k][e];
+            if (dd[e] != kKeep) v[k][e] = (IdT)dd[e];
+            ++r;
           }
+        }
+      }
+      wave_sync();
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int32_t tot = (int32_t)((tots >> (16 * k)) & 0xFFFFu);
+        for (int32_t i = sl; i < tot; i += 32) {
+          G.out_pos[po[k] + rk[k] + i] = spos[k][i];
+          static_cast<IdT*>(G.out_lab)[po[k] + rk[k] + i] = slab[k][i];
         }
         rk[k] += tot;
       }
+      wave_sync();  // (the staging rows are rewritten by the next pass)
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int32_t n = na[k] + nb[k];
       // non-temporal: the output is streamed, never re-read by this step
       IdT* out = static_cast<IdT*>(G.out_tok) + tof[k];
       if (x + 3 < n) {
@@ -2415,7 +2445,9 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, void* d_tokens, int6
   G.is_rn = d_is_rn;
   G.out_pos = d_pos;
   G.out_lab = d_lab;
-  GatherLds Lg{(P->seq + 31) / 32, P->seq};
+  G.out_tok_off = d_tok_off;
+  G.out_pos_off = d_pos_off;
+  GatherLds Lg{(P->seq + 127) / 128 * 128};
   auto launch = [&](auto kern, int K) {
     const int64_t per_wg = (int64_t)2 * K * kGWaves;
     const int64_t nwg = (P->n_pairs + per_wg - 1) / per_wg;
@@ -2433,10 +2465,6 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, void* d_tokens, int6
     else launch(gather_kernel<1, int32_t>, 1);
   }
   LDDL_HIP(hipGetLastError());
-  if (d_tok_off)
-    LDDL_HIP(hipMemcpyAsync(d_tok_off, P->tok_off, 8 * (P->n_pairs + 1), hipMemcpyDeviceToDevice, st));
-  if (d_pos_off && P->masking)
-    LDDL_HIP(hipMemcpyAsync(d_pos_off, P->pos_off, 8 * (P->n_pairs + 1), hipMemcpyDeviceToDevice, st));
   return 0;
 }
 

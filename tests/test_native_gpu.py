@@ -198,12 +198,14 @@ def _oracle_inputs(b):
 
 
 @pytest.mark.parametrize('seq,masking,lds_words', [(128, True, None), (512, True, None),
-                                                   (128, False, None), (128, True, '64')])
+                                                   (1024, True, None), (128, False, None),
+                                                   (128, True, '64')])
 def test_native_bit_exact_vs_oracle(ctx, seq, masking, lds_words, monkeypatch):
     """rng='native' against the C restatement of the same algorithm and streams
     (oracle/native_oracle.c): pair windows, truncation, random-next choice, masked positions and
     decisions and the partition order, bit for bit, partition by partition — with literal
-    [CLS] / [SEP] in the text (the candidate walk) and, with LDDL_NATIVE_LDS_WORDS=64, every
+    [CLS] / [SEP] in the text (the candidate walk), at seq 1024 (the gather's one-pair-per-
+    half-wave instantiation) and, with LDDL_NATIVE_LDS_WORDS=64, every
     partition through the planner's global-prefix path instead of the LDS tables."""
     from oracle import oracle as O
     if lds_words:

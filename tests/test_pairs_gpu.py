@@ -118,3 +118,49 @@ def test_pairs_large_partition_vs_oracle(ctx):
             exp[k].append(out[k])
     for k in exp:
         assert np.array_equal(pb[k], np.concatenate(exp[k])), k
+
+
+@pytest.mark.parametrize('seq,extra', [(128, 40000), (512, 40000)])
+def test_pairs_wide_vs_oracle(tmp_path, seq, extra):
+    """A vocab of more than 65,536 entries against the oracle: 4-byte token ids and labels in
+    the pair tables and the gather, random-token mask decisions above 65,535. The extra vocab
+    lines are bracketed, so no word of the text can produce them and the tokenization is
+    unchanged. (The gather's seq > 600 instantiation runs in test_native_gpu.py: the replay
+    planner stops at seq 512.)"""
+    from lddl_amd import synth
+    from lddl_amd.context import Context
+    from lddl_amd.pairs import make_pairs
+    from oracle import oracle as O
+    vocab = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         'lddl_amd', 'assets', 'vocab_synth_uncased_30522.txt')
+    if extra:
+        big = tmp_path / 'vocab_big.txt'
+        with open(vocab) as f:
+            lines = f.read().splitlines()
+        big.write_text('\n'.join(lines + ['[extra{}]'.format(i) for i in range(extra)]) + '\n')
+        vocab = str(big)
+    ctx = Context(vocab)
+    assert ctx.id_bytes == (4 if extra else 2)
+    corp = synth.generate(seed=91 + seq, n_bytes=600_000, threads=4)
+    part = np.linspace(0, corp.n_doc, 4).astype(np.int64)
+    seeds = np.asarray([11, 12, 13], np.int64)
+    so = torch.from_numpy(corp.sent_off).cuda()
+    ids, sl = ctx.tokenize(torch.from_numpy(corp.text).cuda(), so)
+    pb = make_pairs(ctx, so, ids, sl, torch.from_numpy(corp.doc_sent_off).cuda(),
+                    torch.from_numpy(part).cuda(), torch.from_numpy(seeds).cuda(), seq=seq, dup=2,
+                    masking=True).to_host()
+    tok = O.Tokenizer(vocab)
+    assert tok.vocab_size == 30522 + extra
+    e_ids, e_off = tok.tokenize(corp.text, corp.sent_off)
+    exp = {'tokens': [], 'num_tokens': [], 'len_a': [], 'pos': [], 'labels': []}
+    for p in range(3):
+        ds = corp.doc_sent_off[part[p]:part[p + 1] + 1]
+        out = O.partition_pairs(ds, e_off, e_ids, int(seeds[p]), 2, seq, True, tok.vocab_size,
+                                *(tok.token_id(t) for t in ('[CLS]', '[SEP]', '[MASK]')))
+        for k in exp:
+            exp[k].append(out[k])
+    for k in exp:
+        assert np.array_equal(np.asarray(pb[k]).astype(np.int64),
+                              np.concatenate(exp[k]).astype(np.int64)), k
+    if extra:
+        assert np.concatenate(exp['tokens']).max() > 65535  # random-token decisions reach them
