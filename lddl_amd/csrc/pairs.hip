@@ -1715,6 +1715,18 @@ template <>
 struct Tok4<uint16_t> {
   typedef uint16_t type __attribute__((ext_vector_type(4), aligned(2)));
 };
+// The raw load of 4 ids, and the blend "element e from A iff e < ra" (ra = A elements left)
+__device__ inline uint2 blend4(uint2 a, uint2 b, int32_t ra) {
+  const int32_t bits = ra <= 0 ? 0 : ra >= 4 ? 64 : 16 * ra;
+  const uint32_t mlo = bits >= 32 ? ~0u : (1u << bits) - 1u;
+  const uint32_t mhi = bits >= 64 ? ~0u : bits <= 32 ? 0u : (1u << (bits - 32)) - 1u;
+  return make_uint2((a.x & mlo) | (b.x & ~mlo), (a.y & mhi) | (b.y & ~mhi));
+}
+__device__ inline int4 blend4(int4 a, int4 b, int32_t ra) {
+  return make_int4(0 < ra ? a.x : b.x, 1 < ra ? a.y : b.y, 2 < ra ? a.z : b.z, 3 < ra ? a.w : b.w);
+}
+template <typename IdT>
+using Raw4 = std::conditional_t<sizeof(IdT) == 2, uint2, int4>;
 
 template <int K, typename IdT>
 __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, GatherLds Lg) {
@@ -1733,26 +1745,31 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
   int32_t* dec[K];
   uint16_t* spos[K];
   IdT* slab[K];
+  GatherRec rc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {  // every pair's loads in flight before any is used
+    const int64_t q = q0 + 2 * k + h;
+    const bool act = q < G.n_pairs;
+    rc[k] = act ? G.rec[q] : GatherRec{0, 0, 0, 0, 0, 0, 0};
+    tof[k] = act ? G.tok_off[q] : 0;
+    po[k] = (G.masking && act) ? G.pos_off[q] : 0;
+  }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int64_t q = q0 + 2 * k + h;
-    const bool act = q < G.n_pairs;
-    GatherRec r{0, 0, 0, 0, 0, 0, 0};
-    if (act) r = G.rec[q];
+    const GatherRec& r = rc[k];
     na[k] = r.na;
     nb[k] = r.nb_rn & 0x7FFFFFFF;
     aoff[k] = r.aoff;
     boff[k] = r.boff;
     mb[k] = r.moff;
     nm[k] = G.masking ? r.nm : 0;
-    tof[k] = act ? G.tok_off[q] : 0;
-    po[k] = (G.masking && act) ? G.pos_off[q] : 0;
     rk[k] = 0;
     uint8_t* pb = g_smem + (((size_t)w * K + k) * 2 + h) * Lg.per_pair();
     dec[k] = reinterpret_cast<int32_t*>(pb);
     spos[k] = reinterpret_cast<uint16_t*>(pb + 4 * (size_t)Lg.seqp);
     slab[k] = reinterpret_cast<IdT*>(pb + 4 * (size_t)Lg.seqp + 256);
-    if (sl == 0 && act) {
+    if (sl == 0 && q < G.n_pairs) {
       G.len_a[q] = na[k];
       G.is_rn[q] = (uint8_t)((uint32_t)r.nb_rn >> 31);
       if (G.out_tok_off) {
@@ -1765,23 +1782,28 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
       }
     }
   }
-  // a lane's 4 tokens: one load from A (x < na) and/or one from B (x + 3 >= na), each at the
-  // offset of token x in that window (dense is padded by 4 tokens on both sides, so a load
-  // overhanging its window stays in bounds); element e comes from A iff x + e < na
-  auto load_tokens = [&](int32_t x, tok4_t* v) {
+  // a lane's 4 tokens: one load from A and one from B, each at the offset of token x in that
+  // window (dense is padded by 4 tokens on both sides, so a load overhanging its window stays in
+  // bounds); element e comes from A iff x + e < na. Both loads are issued unconditionally (an
+  // unneeded one reads the window start) and blended only when the pass needs the tokens: a
+  // conditional load made the compiler wait for it inside its branch, before the next pair's
+  // loads were issued.
+  using raw_t = Raw4<IdT>;
+  raw_t ta[K], tb[K];
+  auto issue_tokens = [&](int32_t x) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int32_t n = na[k] + nb[k];
-      tok4_t a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
-      if (x < na[k]) a = *reinterpret_cast<const tok4_t*>(dense + aoff[k] + x);
-      if (x + 3 >= na[k] && x < n) b = *reinterpret_cast<const tok4_t*>(dense + boff[k] + (x - na[k]));
-      const int32_t ra = na[k] - x;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[k][e] = e < ra ? a[e] : b[e];
+      const int32_t n = na[k] + nb[k], bx = x - na[k];
+      ta[k] = *reinterpret_cast<const raw_t*>(dense + aoff[k] + (x < na[k] ? x : 0));
+      tb[k] = *reinterpret_cast<const raw_t*>(dense + boff[k] + (bx >= -3 && x < n ? bx : 0));
     }
   };
+  auto finish_tokens = [&](int32_t x, tok4_t* v) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = __builtin_bit_cast(tok4_t, blend4(ta[k], tb[k], na[k] - x));
+  };
   tok4_t v[K];
-  load_tokens(4 * sl, v);  // the first pass's tokens are in flight while the tables fill
+  issue_tokens(4 * sl);  // the first pass's tokens are in flight while the tables fill
   if (G.masking) {
 #pragma unroll
     for (int k = 0; k < K; ++k)
@@ -1798,7 +1820,8 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
   }
   for (int32_t cb = 0;; cb += 128) {
     const int32_t x = cb + 4 * sl;
-    if (cb > 0) load_tokens(x, v);
+    if (cb > 0) issue_tokens(x);
+    finish_tokens(x, v);
     bool more = false;
     if (G.masking) {
       int4 d4[K];
