@@ -1617,15 +1617,16 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   const int64_t q = (int64_t)blockIdx.x * 64 + lane;
   if (q >= R.n_pairs) return;
   const int64_t slot = R.src[q];
-  const SlotPool sp = R.spool[slot];
-  const int32_t num = sp.nmask;
-  if (num <= 0) return;
-  const int32_t nc = sp.ncand;
-  const int64_t jb = (int64_t)sp.joff16 << 4, mb = (int64_t)sp.moff8 << 3;
+  // the whole 16-byte record and the descriptor in one round trip (a member-wise read split the
+  // record around the early exit below)
+  const uint4 spv = *reinterpret_cast<const uint4*>(R.spool + slot);
   const PairDesc d = R.desc[slot];
+  const SlotPool sp{spv.x, spv.y, (int32_t)spv.z, (int32_t)spv.w};
+  const int32_t num = sp.nmask;
+  const int32_t nc = num > 0 ? sp.ncand : 0;  // (no early exit: it split the loads above)
+  const int64_t jb = (int64_t)sp.joff16 << 4, mb = (int64_t)sp.moff8 << 3;
   const int32_t na = d.na, nb = d.nb_rn & 0x7FFFFFFF;
   const bool fast = nc == na + nb;
-  x.iota(nc);
   const uint4* jp = reinterpret_cast<const uint4*>(static_cast<const D*>(R.jpool) + jb);
   uint4* mp = reinterpret_cast<uint4*>(R.mpos + mb);
   uint4 acc = make_uint4(0u, 0u, 0u, 0u);  // slots [8h, 8h+8) collected from the top down
@@ -1668,18 +1669,20 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
 #pragma unroll
     for (int g = 0; g < NG; ++g)
       if (g < nvec) jv[g] = jp[g];
+    x.iota(nc);  // (after the draws' loads are issued)
 #pragma unroll
     for (int g = NG - 1; g >= 0; --g)
       if (g < nvec) vec(g, jv[g]);
   } else {
     uint4 nxt = jp[nvec - 1];
+    x.iota(nc);
     for (int g = nvec - 1; g >= 0; --g) {
       const uint4 jv = nxt;
       if (g > 0) nxt = jp[g - 1];  // next vector of draws in flight
       vec(g, jv);
     }
   }
-  if (!fast) {  // literal [CLS]/[SEP] in the pair: candidate index -> position via the tokens
+  if (!fast && num > 0) {  // literal [CLS]/[SEP] in the pair: candidate index -> position via the tokens
     const int64_t ao = R.kscan[d.a_ks] + d.a_front, bo = R.kscan[d.b_ks] + d.b_front;
     int k = 0;
     for (int t = 0; t < na + nb; ++t) {
