@@ -128,9 +128,10 @@ def granted_cores():
 def load_pmc(batch_sizes):
     """Per-kernel counters per launch from the committed PMC passes (profiles/pmc_*.json, made by
     tools/prof_counters.sh + tools/make_pmc_json.py) taken on one of `batch_sizes` (requested or
-    actual bytes); the last such file in name order wins. Returns (kernels, file name)."""
+    actual bytes); the last such file in name order wins. Returns (kernels, file name, the pass's
+    build id and git head)."""
     import glob
-    kernels, src = {}, None
+    kernels, src, meta = {}, None, {}
     for pmc in sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_*.json'))):
         try:
             with open(pmc) as f:
@@ -139,7 +140,8 @@ def load_pmc(batch_sizes):
             continue
         if rec.get('batch_bytes') in batch_sizes:
             kernels, src = rec.get('kernels', {}), os.path.basename(pmc)
-    return kernels, src
+            meta = {k: rec.get(k) for k in ('build_id', 'git_head')}
+    return kernels, src, meta
 
 
 def pmc_entry(kernels, kernel):
@@ -674,6 +676,7 @@ def main():
         else:
             torch.cuda.set_device(local)
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    from lddl_amd._native import lib
     from lddl_amd.context import Context
     from lddl_amd.pairs import make_pairs
     from lddl_amd.balance import balance
@@ -937,7 +940,9 @@ def main():
     stage_gbs = stage_bytes / (pair_ms * 1e-3) / 1e9
     # per-kernel counters per launch from the committed PMC passes (profiles/pmc_*.json, made by
     # tools/prof_counters.sh + tools/make_pmc_json.py) when taken on the same batch size
-    pmc_kernels, pmc_src = load_pmc((args.batch_bytes, int(n_bytes)))
+    pmc_kernels, pmc_src, pmc_meta = load_pmc((args.batch_bytes, int(n_bytes)))
+    build_id = lib.lddl_build_id().decode()
+    same_build = pmc_meta.get('build_id') == build_id
 
     def pmc_of(kernel):
         return pmc_entry(pmc_kernels, kernel)
@@ -964,8 +969,10 @@ def main():
                 # the model both hot kernels fit: scalar and vector issue barely
                 # overlap, a SALU instruction costs a SIMD 4 cycles and a VALU one 2
                 'issue_model_frac': (4.0 * (sc or 0) + 2.0 * v) / (256 * 4 * 2.4e9 * ms * 1e-3),
-                'source': pmc_src,
-                'note': 'PMC pass taken on an earlier build of the same batch size'}
+                'source': pmc_src, 'pmc_build_id': pmc_meta.get('build_id'),
+                'pmc_git_head': pmc_meta.get('git_head'), 'same_build': same_build,
+                'note': ('PMC pass of this build (lddl_build_id {})'.format(build_id) if same_build
+                         else 'PMC pass taken on an earlier build of the same batch size')}
 
     plan_roof = {'kernel': 'plan_replay_kernel' if args.rng == 'replay' else
                  'plan_native_kernel x2 + mask_native_kernel + order_native_kernel (HIP events '
@@ -1047,6 +1054,7 @@ def main():
         res['pcie_inclusive'] = pcie_line
     if ref_part is not None:
         res['ref_partitioning'] = ref_part
+    res['build_id'] = build_id  # lddl_build_id(): SHA-256 of the library's sources
     res['torch_alloc_retries'] = int(mem_head.get('num_alloc_retries', 0))  # headline line
     res['torch_alloc_retries_all_lines'] = int(mem.get('num_alloc_retries', 0))
     free_b, total_b = torch.cuda.mem_get_info()

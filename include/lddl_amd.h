@@ -32,6 +32,10 @@ typedef struct lddl_ctx lddl_ctx;
  * ------------------------------------------------------------------------------------------- */
 const char* lddl_last_error(void);
 int lddl_version(void);
+/* Build identity: the first 16 hex digits of a SHA-256 over this library's sources (csrc/ and
+ * include/, as compiled), so that a measurement (bench line, PMC pass) can name the exact build
+ * it ran; no reference counterpart. */
+const char* lddl_build_id(void);
 
 /* ---------------------------------------------------------------------------------------------
  * Synthetic corpus; host-only, no GPU needed.

@@ -22,6 +22,7 @@ c_i64p = ctypes.POINTER(ctypes.c_int64)
 # name -> (restype, argtypes); must mirror include/lddl_amd.h exactly
 SIGNATURES = {
     'lddl_last_error': (ctypes.c_char_p, []),
+    'lddl_build_id': (ctypes.c_char_p, []),
     'lddl_version': (ctypes.c_int, []),
     'lddl_synth_corpus': (c_i64, [c_u64, c_i64, c_i64, c_dbl, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                                   c_i64p, c_i64p, ctypes.c_int]),

@@ -40,10 +40,42 @@ def _run(cmd):
     return r.stdout
 
 
+BUILD_ID_H = os.path.join(CSRC, 'build_id.h')
+
+
+def source_id():
+    """First 16 hex digits of SHA-256 over the library's sources (csrc/ and include/, names and
+    contents, build_id.h itself excluded): the id lddl_build_id() returns."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(CSRC, '*')) + glob.glob(os.path.join(ROOT, 'include', '*.h')))
+    for f in files:
+        if os.path.isfile(f) and f != BUILD_ID_H and f.endswith(('.hip', '.cpp', '.h')):
+            h.update(os.path.relpath(f, ROOT).encode() + b'\0')
+            with open(f, 'rb') as fh:
+                h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def write_build_id():
+    """csrc/build_id.h (generated, not tracked), rewritten only when the id changes so that an
+    unchanged tree rebuilds nothing."""
+    text = '#pragma once\n#define LDDL_BUILD_ID "{}"\n'.format(source_id())
+    try:
+        with open(BUILD_ID_H) as f:
+            if f.read() == text:
+                return
+    except OSError:
+        pass
+    with open(BUILD_ID_H, 'w') as f:
+        f.write(text)
+
+
 def build_product(verbose=False, jobs=8, diag=False, variant=None, defines=()):
     """diag=True builds the stamp-instrumented diagnostic library into lddl_amd/_lib_diag
     (timing shares only; never the shipped library). variant/defines build an experiment library
     into lddl_amd/_lib_<variant> with extra -D flags (A/B measurements only)."""
+    write_build_id()
     suffix = '_diag' if diag else ('_' + variant if variant else '')
     libdir = LIBDIR + suffix
     objdir = OBJDIR + suffix
@@ -85,8 +117,9 @@ def build_host():
     torch (liblddl_amd.so must be loaded after torch: one HIP runtime per process). The same
     sources are also part of liblddl_amd.so."""
     os.makedirs(LIBDIR, exist_ok=True)
+    write_build_id()
     srcs = [os.path.join(CSRC, x) for x in HOST_SRCS]
-    deps = srcs + glob.glob(os.path.join(ROOT, 'include', '*.h')) + [os.path.join(CSRC, 'common.h')]
+    deps = srcs + glob.glob(os.path.join(ROOT, 'include', '*.h')) + [os.path.join(CSRC, 'common.h'), BUILD_ID_H]
     if _newer(HOST_LIB, deps):
         _run(['g++', '-O3', '-std=c++17', '-fPIC', '-shared', '-Wall', '-I' + os.path.join(ROOT, 'include'),
               '-I' + CSRC, '-o', HOST_LIB] + srcs + ['-lpthread'])

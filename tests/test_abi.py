@@ -48,3 +48,11 @@ def test_synth_deterministic_across_threads():
     assert (a.doc_sent_off == b.doc_sent_off).all()
     c = synth.generate(seed=8, n_bytes=300_000, threads=1)
     assert len(c.text) != len(a.text) or (c.text != a.text).any()
+
+
+def test_build_id_matches_sources():
+    """lddl_build_id() of the loaded library is the hash of the sources in this tree (the
+    library is current; bench lines and PMC passes name their build by it)."""
+    from lddl_amd import build
+    from lddl_amd._native import lib
+    assert lib.lddl_build_id().decode() == build.source_id()

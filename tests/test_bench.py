@@ -53,8 +53,8 @@ def test_granted_cores():
 def test_pmc_json_matches_actual_batch_and_template_names():
     """The committed PMC passes are found by the batch's actual byte count and the planner's
     template instantiation is found by its base name (bench.py `traffic` / `issue_roofline`)."""
-    kernels, src = bench.load_pmc((10_000_000_000, 10_000_001_451))
-    assert src is not None and kernels
+    kernels, src, meta = bench.load_pmc((10_000_000_000, 10_000_001_451))
+    assert src is not None and kernels and set(meta) == {'build_id', 'git_head'}
     plan = bench.pmc_entry(kernels, 'plan_replay_kernel')
     assert plan.get('SQ_INSTS_SALU') and plan.get('hbm_bytes_per_launch')
     assert bench.pmc_entry(kernels, 'tokenize_batch_kernel').get('SQ_INSTS_VALU')
