@@ -160,19 +160,6 @@ struct lddl_ctx {
   std::vector<std::string> tokens;  // host copy of the vocab lines
   lddl::DevArena arena;             // per-call temporaries (pair plans)
   void* punkt = nullptr;            // lddl_punkt_state (segment.hip), created by lddl_punkt_set_params
-  // a second stream for work that runs beside the caller's stream inside one call (the planner's
-  // partition shuffle; the call forks and joins it with its own events); created on first use
-  hipStream_t side = nullptr;
-  hipError_t side_stream(hipStream_t* s) {
-    std::lock_guard<std::mutex> g(side_mu);
-    if (!side) {
-      const hipError_t e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
-      if (e != hipSuccess) return e;
-    }
-    *s = side;
-    return hipSuccess;
-  }
-  std::mutex side_mu;
 };
 extern "C" void lddl_punkt_release(lddl_ctx* c);
 

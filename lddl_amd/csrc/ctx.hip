@@ -195,10 +195,6 @@ extern "C" int lddl_ctx_destroy(lddl_ctx* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   lddl_punkt_release(c);
-  if (c->side) {
-    (void)hipStreamSynchronize(c->side);
-    (void)hipStreamDestroy(c->side);
-  }
   for (void* p : {(void*)c->d_l1, (void*)c->d_pages, (void*)c->d_pool, (void*)c->d_vhash,
                   (void*)c->d_vbytes, (void*)c->d_voff, (void*)c->d_render, (void*)c->d_render_off,
                   (void*)c->d_bloom, (void*)c->d_vlong})

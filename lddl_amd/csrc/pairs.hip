@@ -1337,10 +1337,19 @@ __device__ inline uint32_t lds_add16(uint32_t* words, uint32_t v) {  // 16-bit c
 }
 
 constexpr int kShufThreads = 1024;  // one block per CU (its LDS): 16 waves hide the latencies
+// The pair maps of map_pairs_kernel, written by the partition shuffle's last pass (any may be
+// null): src[q] the slot of output pair q, slots[i] the i-th slot in planner order, dstq[i] the
+// output position of the i-th pair in planner order; part_base[p] = the partition's first pair.
+struct PairMaps {
+  const int64_t* part_base;
+  int64_t *src, *slots, *dstq;
+};
+
 __global__ void __launch_bounds__(kShufThreads) shuffle_sort_kernel(const int64_t* kd_off, const int64_t* kp_off,
                                                           int32_t dup, const int64_t* part_npairs,
                                                           const int32_t* __restrict__ jseq,
-                                                          int32_t* __restrict__ order, int32_t cap) {
+                                                          int32_t* __restrict__ order, int32_t cap,
+                                                          PairMaps M) {
   extern __shared__ __attribute__((aligned(16))) uint8_t ss_smem[];
   const int p = blockIdx.x;
   const int32_t n = (int32_t)part_npairs[p];
@@ -1422,9 +1431,14 @@ __global__ void __launch_bounds__(kShufThreads) shuffle_sort_kernel(const int64_
     if (!__syncthreads_or(changed)) break;
   }
   const int32_t first0 = n > 1 && cnt[0] > 0 ? (int32_t)srt[0] : -1;
+  const int64_t q0 = M.part_base ? M.part_base[p] : 0;
   for (int32_t k = tid; k < n; k += kShufThreads) {
     const int32_t sc = k == 0 ? first0 : ord[k];
-    ord[k] = sc >= 0 ? (int32_t)r[sc] : (k == 0 ? 0 : ~sc);
+    const int32_t v = sc >= 0 ? (int32_t)r[sc] : (k == 0 ? 0 : ~sc);
+    ord[k] = v;
+    if (M.src) M.src[q0 + k] = base + v;
+    if (M.slots) M.slots[q0 + k] = base + k;
+    if (M.dstq) M.dstq[q0 + v] = q0 + k;
   }
 }
 
@@ -1434,17 +1448,19 @@ __global__ void __launch_bounds__(kShufThreads) shuffle_sort_kernel(const int64_
 // src[q]: the planner slot of output pair q (partition shuffle applied); slots[q]: the q-th
 // slot in planner order (every partition's slots base .. base + np - 1), so the per-slot passes
 // read the slot-indexed arrays front to back instead of in shuffled order.
-// (either output may be null: the slots do not depend on the partition shuffle, so they are
-// written before it finishes)
+// (any output may be null)
+// dstq[i]: the output position of the i-th pair in planner order (the inverse of src), for the
+// mask replay that also writes each pair's gather record.
 __global__ void map_pairs_kernel(const int64_t* kd_off, const int64_t* kp_off, int32_t dup,
                                  const int64_t* part_pair_base, const int32_t* order, int64_t* src,
-                                 int64_t* slots) {
+                                 int64_t* slots, int64_t* dstq) {
   const int p = blockIdx.x;
   const int64_t base = (int64_t)dup * kd_off[kp_off[p]];
   const int64_t q0 = part_pair_base[p], n = part_pair_base[p + 1] - q0;
   for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
     if (src) src[q0 + k] = base + order[base + k];
     if (slots) slots[q0 + k] = base + k;
+    if (dstq) dstq[q0 + order[base + k]] = q0 + k;
   }
 }
 
@@ -1475,7 +1491,6 @@ __global__ void __launch_bounds__(256) pair_prep_kernel(const int64_t* __restric
                                                         const int64_t* __restrict__ kscan,
                                                         const int32_t* __restrict__ nmask,
                                                         const int64_t* __restrict__ moff,
-                                                        const SlotPool* __restrict__ spool,
                                                         GatherRec* __restrict__ rec,
                                                         int2* __restrict__ cnt) {
   // (XCD-contiguous blocks: a partition's pairs share one L2 for its descriptors and offsets)
@@ -1486,13 +1501,12 @@ __global__ void __launch_bounds__(256) pair_prep_kernel(const int64_t* __restric
   GatherRec r;
   r.aoff = kscan[d.a_ks] + d.a_front;
   r.boff = kscan[d.b_ks] + d.b_front;
-  // masks: the replay planner's per-slot record, or the native path's arrays (none: no masking)
-  SlotPool sp{0u, 0u, 0, 0};
-  if (spool) sp = spool[slot];
-  r.moff = spool ? (int64_t)sp.moff8 << 3 : nmask ? moff[slot] : 0;
+  // masks: the native path's arrays (none: no masking; the replay path's records come from
+  // fy_resolve_kernel)
+  r.moff = nmask ? moff[slot] : 0;
   r.na = d.na;
   r.nb_rn = d.nb_rn;
-  r.nm = spool ? sp.nmask : nmask ? nmask[slot] : 0;
+  r.nm = nmask ? nmask[slot] : 0;
   r.pad = 0;
   rec[q] = r;
   cnt[q] = make_int2(r.na + (r.nb_rn & 0x7FFFFFFF), r.nm);  // compact input of the two scans
@@ -1574,6 +1588,13 @@ struct ResolveArgs {
   const int64_t* kscan;
   IdPtr dense;
   int32_t cls_id, sep_id;
+  // with masking on the replay path, the pair's gather record and scan counts are written here
+  // too, at its output position dstq[i] (what pair_prep_kernel does for the other paths: the
+  // descriptor and slot record are already in registers, and planner order reads them front to
+  // back); null otherwise
+  const int64_t* dstq;
+  GatherRec* rec;
+  int2* cnt;
 };
 
 // A lane's column of LDS entries; 16-bit: x[k * 64 + lane]; 8-bit (seq <= 256): dword k/4 of
@@ -1614,9 +1635,12 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   constexpr int kPerVec = 16 / (int)sizeof(D);  // draws per uint4
   const int lane = threadIdx.x;
   LaneCol<T> x{reinterpret_cast<T*>(s_xb), lane};
-  const int64_t q = (int64_t)blockIdx.x * 64 + lane;
+  // (XCD-contiguous blocks: a partition's pairs, their kept-sentence offsets and records meet
+  // in one L2)
+  const int64_t q = xcd_block(blockIdx.x, gridDim.x) * 64 + lane;
   if (q >= R.n_pairs) return;
   const int64_t slot = R.src[q];
+  const int64_t oq = R.dstq ? R.dstq[q] : 0;
   // the whole 16-byte record and the descriptor in one round trip (a member-wise read split the
   // record around the early exit below)
   const uint4 spv = *reinterpret_cast<const uint4*>(R.spool + slot);
@@ -1627,6 +1651,7 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   const int64_t jb = (int64_t)sp.joff16 << 4, mb = (int64_t)sp.moff8 << 3;
   const int32_t na = d.na, nb = d.nb_rn & 0x7FFFFFFF;
   const bool fast = nc == na + nb;
+  const int64_t ao = R.kscan[d.a_ks] + d.a_front, bo = R.kscan[d.b_ks] + d.b_front;
   const uint4* jp = reinterpret_cast<const uint4*>(static_cast<const D*>(R.jpool) + jb);
   uint4* mp = reinterpret_cast<uint4*>(R.mpos + mb);
   uint4 acc = make_uint4(0u, 0u, 0u, 0u);  // slots [8h, 8h+8) collected from the top down
@@ -1682,8 +1707,19 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
       vec(g, jv);
     }
   }
+  if (R.rec) {
+    GatherRec r;
+    r.aoff = ao;
+    r.boff = bo;
+    r.moff = mb;
+    r.na = na;
+    r.nb_rn = d.nb_rn;
+    r.nm = num;
+    r.pad = 0;
+    R.rec[oq] = r;
+    R.cnt[oq] = make_int2(na + nb, num);
+  }
   if (!fast && num > 0) {  // literal [CLS]/[SEP] in the pair: candidate index -> position via the tokens
-    const int64_t ao = R.kscan[d.a_ks] + d.a_front, bo = R.kscan[d.b_ks] + d.b_front;
     int k = 0;
     for (int t = 0; t < na + nb; ++t) {
       const int32_t tok = t < na ? R.dense.ld(ao + t) : R.dense.ld(bo + (t - na));
@@ -1910,8 +1946,7 @@ struct lddl_pairs {
   int64_t *src = nullptr, *tok_off = nullptr, *pos_off = nullptr;
   GatherRec* rec = nullptr;  // per output pair (pair_prep_kernel)
   int64_t* part_base = nullptr;  // [n_part + 1] first output pair of each partition
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // [0..1] around the last
-  // plan_replay_kernel launch; [2..3] fork / join of the side stream
+  hipEvent_t ev[2] = {nullptr, nullptr};  // around the last plan_replay_kernel launch
 
   template <typename T>
   int alloc(T** p, int64_t n, hipStream_t st) {
@@ -1930,7 +1965,6 @@ struct lddl_pairs {
       }
   }
   void release(hipStream_t st) {
-    if (ev[3]) (void)hipStreamWaitEvent(st, ev[3], 0);  // side-stream work has finished
     for (DevArena::Block& b : allocs) arena->give(b, st);
     allocs.clear();
     for (hipEvent_t& e : ev)
@@ -2160,7 +2194,6 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
 
   }
   P->max_pred = max_pred;
-  SlotPool* spool_out = nullptr;  // replay masking: per-slot pool record (pair_prep reads it)
   // the gather records + output-order scans (tok_off, pos_off) of the plan's pairs
   int2* pcnt = nullptr;
   int64_t* scr2 = nullptr;
@@ -2172,17 +2205,20 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     if (prm->masking && (rc = P->alloc(&P->pos_off, npairs + 1, st))) return rc;
     return 0;
   };
-  auto prep_and_scan = [&](hipStream_t s, const SlotPool* spool_rec) -> int {
+  auto scan_only = [&](hipStream_t s) -> int {
+    LDDL_HIP(scan_exclusive(PairTokens{pcnt}, P->n_pairs, P->tok_off, scr2, s));
+    if (prm->masking) LDDL_HIP(scan_exclusive(PairMasks{pcnt}, P->n_pairs, P->pos_off, scr2, s));
+    return 0;
+  };
+  // gather records from the output order (src): the native path, and replay without masking
+  auto prep_and_scan = [&](hipStream_t s) -> int {
     const int64_t npairs = P->n_pairs;
     if (npairs)
       hipLaunchKernelGGL(pair_prep_kernel, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, s,
                          P->src, npairs, P->desc, P->kscan, prm->masking ? P->nmask : nullptr,
-                         P->moff, prm->masking && prm->rng != LDDL_RNG_NATIVE ? spool_rec : nullptr,
-                         P->rec, pcnt);
+                         P->moff, P->rec, pcnt);
     LDDL_HIP(hipGetLastError());
-    LDDL_HIP(scan_exclusive(PairTokens{pcnt}, npairs, P->tok_off, scr2, s));
-    if (prm->masking) LDDL_HIP(scan_exclusive(PairMasks{pcnt}, npairs, P->pos_off, scr2, s));
-    return 0;
+    return scan_only(s);
   };
   if (prm->rng == LDDL_RNG_NATIVE) {
     TRY(plan_native(P, c, prm, d_part_seed, n_part, st));
@@ -2194,7 +2230,6 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   TRY(P->alloc(&part_npairs, n_part + 1, st));
   SlotPool* spool = nullptr;
   if (prm->masking) TRY(P->alloc(&spool, slots, st));
-  spool_out = spool;
   PlanArgs A{};
   A.kscan = P->kscan;
   A.ks_len = P->ks_len;
@@ -2314,18 +2349,20 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     cap = (int64_t)ctl[0] + 1024;
     jcap = (int64_t)ctl[2] + 1024;
   }
-  // random.shuffle(partition_pairs), alone on the main stream (its blocks need 16 waves and
-  // ~90 KB of LDS per CU: beside fy_resolve's small blocks they waited for CUs to drain, 10.3 ms
-  // against ~2 alone); then the layout forks onto the context's side stream
-  hipStream_t sst = nullptr;
-  hipEvent_t ev_plan = nullptr, ev_shuf = nullptr;
+  // the pair maps (see PairMaps): with masking the planner-order slots and their output
+  // positions (the mask replay writes each pair's gather record there), else the output order
+  PairMaps M{part_base, nullptr, nullptr, nullptr};
+  if (prm->masking) {
+    TRY(P->alloc(&M.slots, P->n_pairs, st));
+    TRY(P->alloc(&M.dstq, P->n_pairs, st));
+  } else {
+    TRY(P->alloc(&P->src, P->n_pairs, st));
+    M.src = P->src;
+  }
+  // random.shuffle(partition_pairs), alone on the stream (its blocks need 16 waves and ~90 KB of
+  // LDS per CU: beside fy_resolve's small blocks on a second stream they waited for CUs to
+  // drain, 10.3 ms against ~2 alone); its last pass writes the pair maps
   if (n_part) {
-    TRY(c->side_stream(&sst) == hipSuccess &&
-                hipEventCreateWithFlags(&P->ev[2], hipEventDisableTiming) == hipSuccess &&
-                hipEventCreateWithFlags(&P->ev[3], hipEventDisableTiming) == hipSuccess
-            ? 0 : (set_error("side stream"), -100));
-    ev_plan = P->ev[2];
-    ev_shuf = P->ev[3];
     const int64_t cap = max_np;
     // dynamic-LDS budget of the swap kernel: what the device grants a block (160 KiB on
     // gfx950), minus headroom for the kernel's static LDS
@@ -2338,12 +2375,14 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     if (cap_lds > 0)
       hipLaunchKernelGGL(shuffle_sort_kernel, dim3((unsigned)n_part), dim3(kShufThreads),
                          (size_t)6 * (size_t)((cap_lds + 2) & ~1), st, P->kd_off, P->kp_off,
-                         prm->dup, part_npairs, jseq, P->order, (int32_t)cap_lds);
-    if (cap > cap_lds)
+                         prm->dup, part_npairs, jseq, P->order, (int32_t)cap_lds, M);
+    if (cap > cap_lds) {  // partitions beyond the LDS tables: swaps in global memory, then the maps
       hipLaunchKernelGGL(apply_shuffle_kernel, dim3((unsigned)n_part), dim3(64), 0, st, P->kd_off,
                          P->kp_off, prm->dup, part_npairs, jseq, P->order, cap_lds);
-    LDDL_HIP(hipEventRecord(ev_plan, st));
-    LDDL_HIP(hipStreamWaitEvent(sst, ev_plan, 0));
+      hipLaunchKernelGGL(map_pairs_kernel, dim3((unsigned)n_part), dim3(256), 0, st, P->kd_off,
+                         P->kp_off, prm->dup, part_base, (const int32_t*)P->order, M.src, M.slots,
+                         M.dstq);
+    }
   }
   LDDL_HIP(hipGetLastError());
 #ifdef LDDL_STAMPS
@@ -2397,44 +2436,36 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     fprintf(stderr, "\n");
   }
 #endif
-  // layout (part_base and n_pairs came with the planner's sync): the main stream replays the
-  // masks (fy_resolve, planner order) while the side stream maps the output order and builds the
-  // gather records and the two output-order scans
+  // layout (part_base and n_pairs came with the planner's sync). With masking, the mask replay
+  // (fy_resolve, planner order) also writes every pair's gather record at its output position
+  // and the two output-order scans follow; without, pair_prep builds the records from the
+  // output order. (Round 4 ran pair_prep beside fy_resolve on a second stream: 15.6 ms for the
+  // section, both kernels slowed by the other; the fused replay reads each slot record once.)
   TRY(alloc_layout(P->n_pairs));
-  TRY(P->alloc(&P->src, P->n_pairs, st));
-  int64_t* slots = nullptr;  // planner-order slots for the mask replay
-  if (prm->masking) TRY(P->alloc(&slots, P->n_pairs, st));
-  if (n_part && slots)
-    hipLaunchKernelGGL(map_pairs_kernel, dim3((unsigned)n_part), dim3(256), 0, st, P->kd_off,
-                       P->kp_off, prm->dup, part_base, (const int32_t*)nullptr, (int64_t*)nullptr, slots);
-  if (prm->masking && P->n_pairs) {
-    ResolveArgs RA{slots, P->n_pairs, P->desc, spool, jpool, P->mpos, P->kscan, P->dense, cls, sep};
-    const dim3 grid((unsigned)((P->n_pairs + 63) / 64));
-    if (prm->seq <= 131)  // nc <= 128: all draws in registers (8 uint4 of 1-byte draws)
-      hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 8>), grid, dim3(64),
-                         (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
-    else if (prm->seq <= 256)  // candidate indices, positions and draws fit a byte
-      hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 0>), grid, dim3(64),
-                         (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
-    else
-      hipLaunchKernelGGL((fy_resolve_kernel<uint16_t, uint16_t, 0>), grid, dim3(64),
-                         (size_t)2 * 64 * (size_t)prm->seq, st, RA);
+  if (prm->masking) {
+    if (P->n_pairs) {
+      ResolveArgs RA{M.slots, P->n_pairs, P->desc, spool, jpool, P->mpos, P->kscan, P->dense, cls,
+                     sep, M.dstq, P->rec, pcnt};
+      const dim3 grid((unsigned)((P->n_pairs + 63) / 64));
+      if (prm->seq <= 131)  // nc <= 128: all draws in registers (8 uint4 of 1-byte draws)
+        hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 8>), grid, dim3(64),
+                           (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
+      else if (prm->seq <= 256)  // candidate indices, positions and draws fit a byte
+        hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 0>), grid, dim3(64),
+                           (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
+      else
+        hipLaunchKernelGGL((fy_resolve_kernel<uint16_t, uint16_t, 0>), grid, dim3(64),
+                           (size_t)2 * 64 * (size_t)prm->seq, st, RA);
+    }
     LDDL_HIP(hipGetLastError());
-  }
-  hipStream_t lst = n_part ? sst : st;  // the layout's stream
-  if (n_part)  // the output order: after the partition shuffle (side stream)
-    hipLaunchKernelGGL(map_pairs_kernel, dim3((unsigned)n_part), dim3(256), 0, lst, P->kd_off,
-                       P->kp_off, prm->dup, part_base, (const int32_t*)P->order, P->src, (int64_t*)nullptr);
-  LDDL_HIP(hipGetLastError());
-  TRY(prep_and_scan(lst, spool_out));
-  if (n_part) {
-    LDDL_HIP(hipEventRecord(ev_shuf, sst));
-    LDDL_HIP(hipStreamWaitEvent(st, ev_shuf, 0));
+    TRY(scan_only(st));
+  } else {
+    TRY(prep_and_scan(st));
   }
   }  // replay
   if (prm->rng == LDDL_RNG_NATIVE) {
     TRY(alloc_layout(P->n_pairs));
-    TRY(prep_and_scan(st, nullptr));
+    TRY(prep_and_scan(st));
   }
   LDDL_HIP(hipMemcpyAsync(&P->n_tokens, P->tok_off + P->n_pairs, 8, hipMemcpyDeviceToHost, st));
   if (prm->masking)

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out/r04z
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/r04z/tests.log 2>&1 || exit 1
+echo tests ok
+bash tools/run_trace_copies.sh r04z/trace || exit 1
