@@ -1516,9 +1516,12 @@ struct PairTokens {
   const int2* c;
   __device__ int64_t operator()(int64_t q) const { return c[q].x; }
 };
-struct PairMasks {
+struct PairCounts {  // both, for scan_exclusive2
   const int2* c;
-  __device__ int64_t operator()(int64_t q) const { return c[q].y; }
+  __device__ Sum2 operator()(int64_t q) const {
+    const int2 v = c[q];
+    return Sum2{v.x, v.y};
+  }
 };
 
 // Kept tokens packed densely in kept-sentence order: kept sentence k's pieces are
@@ -2200,14 +2203,16 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   auto alloc_layout = [&](int64_t npairs) -> int {
     int rc;
     if ((rc = P->alloc(&P->tok_off, npairs + 1, st)) || (rc = P->alloc(&P->rec, npairs, st)) ||
-        (rc = P->alloc(&pcnt, npairs, st)) || (rc = P->alloc(&scr2, scan_scratch_elems(npairs), st)))
+        (rc = P->alloc(&pcnt, npairs, st)) || (rc = P->alloc(&scr2, 2 * scan_scratch_elems(npairs), st)))
       return rc;
     if (prm->masking && (rc = P->alloc(&P->pos_off, npairs + 1, st))) return rc;
     return 0;
   };
-  auto scan_only = [&](hipStream_t s) -> int {
-    LDDL_HIP(scan_exclusive(PairTokens{pcnt}, P->n_pairs, P->tok_off, scr2, s));
-    if (prm->masking) LDDL_HIP(scan_exclusive(PairMasks{pcnt}, P->n_pairs, P->pos_off, scr2, s));
+  auto scan_only = [&](hipStream_t s) -> int {  // tok_off (and pos_off) from the counts
+    if (prm->masking)
+      LDDL_HIP(scan_exclusive2(PairCounts{pcnt}, P->n_pairs, P->tok_off, P->pos_off, scr2, s));
+    else
+      LDDL_HIP(scan_exclusive(PairTokens{pcnt}, P->n_pairs, P->tok_off, scr2, s));
     return 0;
   };
   // gather records from the output order (src): the native path, and replay without masking

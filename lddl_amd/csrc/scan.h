@@ -80,4 +80,78 @@ hipError_t scan_exclusive(F f, int64_t n, int64_t* out, int64_t* scratch, hipStr
   return hipGetLastError();
 }
 
+// Two exclusive scans in one set of passes over a functor returning both values (Sum2): each
+// input element is read once; out_a / out_b as scan_exclusive's out. Scratch: twice
+// scan_scratch_elems(n).
+struct Sum2 {
+  int64_t a, b;
+};
+
+template <typename F>
+__global__ void __launch_bounds__(kScanThreads) scan_reduce2_kernel(F f, int64_t n, int64_t* sa, int64_t* sb) {
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int64_t va = 0, vb = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k)
+    if (base + k < n) {
+      const Sum2 s = f(base + k);
+      va += s.a;
+      vb += s.b;
+    }
+  int64_t ta, tb;
+  block_excl_scan(va, &ta);
+  block_excl_scan(vb, &tb);
+  if (threadIdx.x == 0) {
+    sa[blockIdx.x] = ta;
+    sb[blockIdx.x] = tb;
+  }
+}
+
+// sa (block 0) and sb (block 1) as scan_sums_kernel
+__global__ void __launch_bounds__(kScanThreads) scan_sums2_kernel(int64_t* sa, int64_t* sb, int64_t nb);
+
+template <typename F>
+__global__ void __launch_bounds__(kScanThreads) scan_write2_kernel(F f, int64_t n, const int64_t* sa,
+                                                                  const int64_t* sb, int64_t* oa,
+                                                                  int64_t* ob) {
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  Sum2 vals[kScanItems];
+  int64_t va = 0, vb = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    vals[k] = base + k < n ? f(base + k) : Sum2{0, 0};
+    va += vals[k].a;
+    vb += vals[k].b;
+  }
+  int64_t ta, tb;
+  int64_t offa = block_excl_scan(va, &ta) + sa[blockIdx.x];
+  int64_t offb = block_excl_scan(vb, &tb) + sb[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    if (base + k < n) {
+      oa[base + k] = offa;
+      ob[base + k] = offb;
+    }
+    offa += vals[k].a;
+    offb += vals[k].b;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) {
+    oa[n] = sa[gridDim.x];
+    ob[n] = sb[gridDim.x];
+  }
+}
+
+template <typename F>
+hipError_t scan_exclusive2(F f, int64_t n, int64_t* out_a, int64_t* out_b, int64_t* scratch,
+                           hipStream_t st) {
+  const int64_t nb = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
+  int64_t* sb = scratch + scan_scratch_elems(n);
+  hipLaunchKernelGGL(scan_reduce2_kernel<F>, dim3((unsigned)nb), dim3(kScanThreads), 0, st, f, n,
+                     scratch, sb);
+  hipLaunchKernelGGL(scan_sums2_kernel, dim3(2), dim3(kScanThreads), 0, st, scratch, sb, nb);
+  hipLaunchKernelGGL(scan_write2_kernel<F>, dim3((unsigned)nb), dim3(kScanThreads), 0, st, f, n,
+                     scratch, sb, out_a, out_b);
+  return hipGetLastError();
+}
+
 }  // namespace lddl
