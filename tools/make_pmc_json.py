@@ -2,7 +2,7 @@
 (tools/prof_counters.sh) -> profiles/pmc_<tag>.json, read by bench.py for `roofline.traffic`
 and the VALU-issue roofline when the batch size matches.
 
-    python tools/make_pmc_json.py gpurun_out/<dir> <batch_bytes> <label> [git head] > profiles/pmc.json
+    python tools/make_pmc_json.py gpurun_out/<dir>/pmc <batch_bytes> <label> [git head] > profiles/pmc.json
 
 The library's build id (lddl_build_id, a hash of its sources) is taken from the passes' bench
 JSON lines, so bench.py can tell whether the counters describe the build it runs.
@@ -30,7 +30,8 @@ def short(name):
 
 def bench_build_id(src):
     """lddl_build_id of the library the passes ran (the bench JSON line in the passes' logs)."""
-    for log in sorted(glob.glob(os.path.join(src, '*.log'))):
+    logs = glob.glob(os.path.join(src, '*.log')) + glob.glob(os.path.join(os.path.dirname(src.rstrip('/')), '*.log'))
+    for log in sorted(logs):
         with open(log, errors='replace') as f:
             for ln in f:
                 if ln.startswith('{') and '"build_id"' in ln:
