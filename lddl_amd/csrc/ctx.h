@@ -67,7 +67,6 @@ class DevArena {
     }
     out = Block{};
     out.size = want;
-    if (getenv("LDDL_ARENA_DEBUG")) fprintf(stderr, "[arena] hipMalloc %zu bytes (%zu cached)\n", want, free_.size());
     hipError_t e = hipMalloc(&out.p, want);
     if (e != hipSuccess) {  // release the cached blocks and retry once
       (void)hipGetLastError();

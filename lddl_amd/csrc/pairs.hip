@@ -2182,7 +2182,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
     P->dense = IdPtr{raw + 4 * ib, ib};
   }
   // replay mode: the planner launch's tail workgroups pack `dense` (plan_replay_kernel)
-  const bool dense_in_plan = prm->rng == LDDL_RNG_REPLAY && n_part > 0 && !getenv("LDDL_DENSIFY_INLINE");
+  const bool dense_in_plan = prm->rng == LDDL_RNG_REPLAY && n_part > 0;
   if (P->n_kept_sent && !dense_in_plan)
     hipLaunchKernelGGL(densify_kernel, dim3((unsigned)((P->n_kept_sent + 255) / 256)), dim3(256), 0,
                        st, P->ks_start, P->ks_len, P->kscan, P->n_kept_sent, d_ids, P->dense);
@@ -2245,7 +2245,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   A.dense = P->dense;
   A.n_kept_sent = dense_in_plan ? P->n_kept_sent : 0;
   A.n_part = (int32_t)n_part;
-  A.n_dense_wg = getenv("LDDL_DENSE_WG") ? std::max(1, atoi(getenv("LDDL_DENSE_WG"))) : 4096;
+  A.n_dense_wg = 4096;
   A.part_seed = d_part_seed;
   A.seq = prm->seq;
   A.dup = prm->dup;
