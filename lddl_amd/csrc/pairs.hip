@@ -1568,11 +1568,14 @@ constexpr int kGWaves = 4;
 
 // LDS of the gather per pair in flight: the decision table indexed by output token x (seqp =
 // seq rounded up to 128 entries of int32, kNoMask where x is not masked) and the staging rows
-// of one pass's masked positions and labels by rank (128 each).
+// of one pass's masked positions and labels by rank (128 each, then one trash entry per lane).
 constexpr int32_t kNoMask = INT32_MIN;
+constexpr int kStageRows = 128;  // + 32 trash entries, one per lane of the half-wave
 struct GatherLds {
   int32_t seqp;
-  __host__ __device__ size_t per_pair() const { return (size_t)4 * seqp + 128 * 2 + 128 * 4; }
+  __host__ __device__ size_t per_pair() const {
+    return (size_t)4 * seqp + (kStageRows + 32) * 2 + (kStageRows + 32) * 4;
+  }
 };
 
 // Replay masks, off the planner's sequential chain: one LANE per pair replays the recorded swaps
@@ -1810,7 +1813,7 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
     uint8_t* pb = g_smem + (((size_t)w * K + k) * 2 + h) * Lg.per_pair();
     dec[k] = reinterpret_cast<int32_t*>(pb);
     spos[k] = reinterpret_cast<uint16_t*>(pb + 4 * (size_t)Lg.seqp);
-    slab[k] = reinterpret_cast<IdT*>(pb + 4 * (size_t)Lg.seqp + 256);
+    slab[k] = reinterpret_cast<IdT*>(pb + 4 * (size_t)Lg.seqp + 2 * (kStageRows + 32));
     if (sl == 0 && q < G.n_pairs) {
       G.len_a[q] = na[k];
       G.is_rn[q] = (uint8_t)((uint32_t)r.nb_rn >> 31);
@@ -1886,14 +1889,13 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
         int32_t r = (int32_t)((excl >> (16 * k)) & 0xFFFFu);
         const int32_t dd[4] = {d4[k].x, d4[k].y, d4[k].z, d4[k].w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if ((m4[k] >> e) & 1u) {
-            const int32_t xe = x + e;
-            spos[k][r] = (uint16_t)(xe < na[k] ? xe + 1 : xe + 2);
-            slab[k][r] = v[k][e];
-            if (dd[e] != kKeep) v[k][e] = (IdT)dd[e];
-            ++r;
-          }
+        for (int e = 0; e < 4; ++e) {  // branch-free: an unmasked element writes the lane's trash entry
+          const bool mk = (m4[k] >> e) & 1u;
+          const int32_t xe = x + e, at = mk ? r : kStageRows + sl;
+          spos[k][at] = (uint16_t)(xe < na[k] ? xe + 1 : xe + 2);
+          slab[k][at] = v[k][e];
+          v[k][e] = mk && dd[e] != kKeep ? (IdT)dd[e] : v[k][e];
+          r += mk ? 1 : 0;
         }
       }
       wave_sync();
