@@ -1,5 +1,5 @@
 // Issue-rate probe for gfx950 (diagnostic, not product): SALU vs VALU vs mixed instruction
-// throughput per SIMD at 1, 2, 4 and 8 waves per SIMD. Each wave runs ITER x 32 independent
+// throughput per SIMD at 1, 2, 4 and 8 waves per SIMD, and 32-bit vs 24-bit integer multiplies. Each wave runs ITER x 32 independent
 // adds (8 registers round robin); cycles from s_memtime (shader clock) per wave.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -40,6 +40,28 @@ __global__ void probe(unsigned long long* cyc, int* sink) {
           "v_add_u32 %0, %0, 1\n v_add_u32 %1, %1, 1\n v_add_u32 %2, %2, 1\n v_add_u32 %3, %3, 1\n"
           "v_add_u32 %4, %4, 1\n v_add_u32 %5, %5, 1\n v_add_u32 %6, %6, 1\n v_add_u32 %7, %7, 1\n"
           : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7));
+    } else if (MODE == 3) {  // 32 v_mul_lo_u32 (8 independent chains)
+      asm volatile(
+          "v_mul_lo_u32 %0, %0, %8\n v_mul_lo_u32 %1, %1, %8\n v_mul_lo_u32 %2, %2, %8\n v_mul_lo_u32 %3, %3, %8\n"
+          "v_mul_lo_u32 %4, %4, %8\n v_mul_lo_u32 %5, %5, %8\n v_mul_lo_u32 %6, %6, %8\n v_mul_lo_u32 %7, %7, %8\n"
+          "v_mul_lo_u32 %0, %0, %8\n v_mul_lo_u32 %1, %1, %8\n v_mul_lo_u32 %2, %2, %8\n v_mul_lo_u32 %3, %3, %8\n"
+          "v_mul_lo_u32 %4, %4, %8\n v_mul_lo_u32 %5, %5, %8\n v_mul_lo_u32 %6, %6, %8\n v_mul_lo_u32 %7, %7, %8\n"
+          "v_mul_lo_u32 %0, %0, %8\n v_mul_lo_u32 %1, %1, %8\n v_mul_lo_u32 %2, %2, %8\n v_mul_lo_u32 %3, %3, %8\n"
+          "v_mul_lo_u32 %4, %4, %8\n v_mul_lo_u32 %5, %5, %8\n v_mul_lo_u32 %6, %6, %8\n v_mul_lo_u32 %7, %7, %8\n"
+          "v_mul_lo_u32 %0, %0, %8\n v_mul_lo_u32 %1, %1, %8\n v_mul_lo_u32 %2, %2, %8\n v_mul_lo_u32 %3, %3, %8\n"
+          "v_mul_lo_u32 %4, %4, %8\n v_mul_lo_u32 %5, %5, %8\n v_mul_lo_u32 %6, %6, %8\n v_mul_lo_u32 %7, %7, %8\n"
+          : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7) : "v"(s0 + 3));
+    } else if (MODE == 4) {  // 32 v_mad_u32_u24 (8 independent chains)
+      asm volatile(
+          "v_mad_u32_u24 %0, %0, %8, %8\n v_mad_u32_u24 %1, %1, %8, %8\n v_mad_u32_u24 %2, %2, %8, %8\n v_mad_u32_u24 %3, %3, %8, %8\n"
+          "v_mad_u32_u24 %4, %4, %8, %8\n v_mad_u32_u24 %5, %5, %8, %8\n v_mad_u32_u24 %6, %6, %8, %8\n v_mad_u32_u24 %7, %7, %8, %8\n"
+          "v_mad_u32_u24 %0, %0, %8, %8\n v_mad_u32_u24 %1, %1, %8, %8\n v_mad_u32_u24 %2, %2, %8, %8\n v_mad_u32_u24 %3, %3, %8, %8\n"
+          "v_mad_u32_u24 %4, %4, %8, %8\n v_mad_u32_u24 %5, %5, %8, %8\n v_mad_u32_u24 %6, %6, %8, %8\n v_mad_u32_u24 %7, %7, %8, %8\n"
+          "v_mad_u32_u24 %0, %0, %8, %8\n v_mad_u32_u24 %1, %1, %8, %8\n v_mad_u32_u24 %2, %2, %8, %8\n v_mad_u32_u24 %3, %3, %8, %8\n"
+          "v_mad_u32_u24 %4, %4, %8, %8\n v_mad_u32_u24 %5, %5, %8, %8\n v_mad_u32_u24 %6, %6, %8, %8\n v_mad_u32_u24 %7, %7, %8, %8\n"
+          "v_mad_u32_u24 %0, %0, %8, %8\n v_mad_u32_u24 %1, %1, %8, %8\n v_mad_u32_u24 %2, %2, %8, %8\n v_mad_u32_u24 %3, %3, %8, %8\n"
+          "v_mad_u32_u24 %4, %4, %8, %8\n v_mad_u32_u24 %5, %5, %8, %8\n v_mad_u32_u24 %6, %6, %8, %8\n v_mad_u32_u24 %7, %7, %8, %8\n"
+          : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7) : "v"(s0 + 3));
     } else {  // 16 SALU + 16 VALU interleaved
       asm volatile(
           "s_add_u32 %0, %0, 1\n v_add_u32 %8, %8, 1\n s_add_u32 %1, %1, 1\n v_add_u32 %9, %9, 1\n"
@@ -68,8 +90,8 @@ int main() {
   int* sink;
   hipMalloc(&cyc, sizeof(unsigned long long) * ncu * 32);
   hipMalloc(&sink, 4);
-  const char* names[3] = {"salu32", "valu32", "mix16+16"};
-  for (int mode = 0; mode < 3; ++mode) {
+  const char* names[5] = {"salu32", "valu32", "mix16+16", "mul_lo32", "mad_u24"};
+  for (int mode = 0; mode < 5; ++mode) {
     for (int wps : {1, 2, 4, 8}) {  // waves per SIMD: workgroups of 4 * wps waves, one per CU
       const int threads = 256 * wps > 1024 ? 1024 : 256 * wps;
       const int blocks = ncu * (256 * wps / threads);
@@ -81,6 +103,8 @@ int main() {
         if (mode == 0) hipLaunchKernelGGL(probe<0>, dim3(blocks), dim3(threads), 0, 0, cyc, sink);
         if (mode == 1) hipLaunchKernelGGL(probe<1>, dim3(blocks), dim3(threads), 0, 0, cyc, sink);
         if (mode == 2) hipLaunchKernelGGL(probe<2>, dim3(blocks), dim3(threads), 0, 0, cyc, sink);
+        if (mode == 3) hipLaunchKernelGGL(probe<3>, dim3(blocks), dim3(threads), 0, 0, cyc, sink);
+        if (mode == 4) hipLaunchKernelGGL(probe<4>, dim3(blocks), dim3(threads), 0, 0, cyc, sink);
         hipEventRecord(b);
         hipEventSynchronize(b);
       }
