@@ -1573,8 +1573,9 @@ constexpr int32_t kNoMask = INT32_MIN;
 constexpr int kStageRows = 128;  // + 32 trash entries, one per lane of the half-wave
 struct GatherLds {
   int32_t seqp;
+  int32_t ib;  // bytes per label id (the staging row's width)
   __host__ __device__ size_t per_pair() const {
-    return (size_t)4 * seqp + (kStageRows + 32) * 2 + (kStageRows + 32) * 4;
+    return (size_t)4 * seqp + (size_t)(kStageRows + 32) * (size_t)(2 + ib);
   }
 };
 
@@ -1928,6 +1929,167 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
   }
 }
 
+typedef uint16_t Tok8 __attribute__((ext_vector_type(8), aligned(2)));
+__device__ inline uint4 blend8(uint4 a, uint4 b, int32_t ra) {  // element e from A iff e < ra
+  const int32_t bits = ra <= 0 ? 0 : ra >= 8 ? 128 : 16 * ra;
+  auto m = [&](int d) -> uint32_t {
+    const int32_t t = bits - 32 * d;
+    return t >= 32 ? ~0u : t <= 0 ? 0u : (1u << t) - 1u;
+  };
+  const uint32_t m0 = m(0), m1 = m(1), m2 = m(2), m3 = m(3);
+  return make_uint4((a.x & m0) | (b.x & ~m0), (a.y & m1) | (b.y & ~m1), (a.z & m2) | (b.z & ~m2),
+                    (a.w & m3) | (b.w & ~m3));
+}
+
+// The gather for 16-bit ids: LP = 16 or 8 lanes per output pair (4 or 8 pairs per wave), 128 / LP
+// consecutive tokens per lane (16-byte loads from A and B, 16-byte non-temporal stores). Against
+// gather_kernel<2, uint16_t> (a half-wave per pair, 4 tokens per lane, two pairs per lane) a pair
+// costs fewer lanes and a lane holds one pair's registers, so more pairs are in flight per SIMD
+// while the per-wave load chain (record -> tokens and masks -> stores) stays the same: 33.3 ->
+// 29.5 ms per 10 GB step at LP = 16 (profiles/r04zd_*); LP = 8 needs 95 VGPRs and 37 KB of LDS
+// per 4-wave block, runs at 4 waves/SIMD and took 35.3 ms (r04ze). The mask path is the same
+// decision table by output token (16-byte LDS reads), ranks from an LP-lane DPP scan of the
+// lanes' masked counts, and staged coalesced stores.
+template <int LP>
+struct G16 {
+  static constexpr int kNT = 128 / LP;  // tokens per lane per pass
+  static constexpr int kNV = kNT / 8;   // 16-byte vectors per lane
+};
+
+// inclusive scan of v over LP-lane segments (LP = 8 or 16) and the segment's total
+template <int LP>
+__device__ inline uint32_t seg_scan(uint32_t v, int lane, uint32_t* tot) {
+  uint32_t inc = v;  // 16-lane row scan (row_shr 1, 2, 4, 8)
+  inc = scan_step<0x111, 0xF, true>(inc);
+  inc = scan_step<0x112, 0xF, true>(inc);
+  inc = scan_step<0x114, 0xF, true>(inc);
+  inc = scan_step<0x118, 0xF, true>(inc);
+  const uint32_t r15 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x15F, 0xF, 0xF, false);  // row_share:15
+  if (LP == 16) {
+    *tot = r15;
+    return inc;
+  }
+  const uint32_t r7 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x157, 0xF, 0xF, false);  // row_share:7
+  const bool hi = (lane & 8) != 0;
+  *tot = hi ? r15 - r7 : r7;
+  return hi ? inc - r7 : inc;
+}
+
+template <int LP>
+__global__ void __launch_bounds__(64 * kGWaves, 1) gather16_kernel(GatherArgs G, GatherLds Lg) {
+  constexpr int NT = G16<LP>::kNT, NV = G16<LP>::kNV, PW = 64 / LP;  // PW pairs per wave
+  const uint16_t* __restrict__ dense = static_cast<const uint16_t*>(G.dense);
+  uint16_t* __restrict__ out_tok = static_cast<uint16_t*>(G.out_tok);
+  uint16_t* __restrict__ out_lab = static_cast<uint16_t*>(G.out_lab);
+  extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, qw = lane / LP, ql = lane % LP;
+  // XCD-contiguous blocks (see gather_kernel)
+  const int64_t wg = xcd_block((int64_t)blockIdx.y * gridDim.x + blockIdx.x, (int64_t)gridDim.x * gridDim.y);
+  const int64_t q = (wg * kGWaves + w) * PW + qw;
+  const bool act = q < G.n_pairs;
+  const GatherRec r = act ? G.rec[q] : GatherRec{0, 0, 0, 0, 0, 0, 0};
+  const int64_t tof = act ? G.tok_off[q] : 0;
+  const int64_t po = (G.masking && act) ? G.pos_off[q] : 0;
+  const int32_t na = r.na, nb = r.nb_rn & 0x7FFFFFFF, n = na + nb;
+  const int32_t nm = G.masking ? r.nm : 0;
+  const int64_t mb = r.moff;
+  uint8_t* pb = g_smem + ((size_t)w * PW + qw) * Lg.per_pair();
+  int32_t* dec = reinterpret_cast<int32_t*>(pb);
+  uint16_t* spos = reinterpret_cast<uint16_t*>(pb + 4 * (size_t)Lg.seqp);
+  uint16_t* slab = reinterpret_cast<uint16_t*>(pb + 4 * (size_t)Lg.seqp + 2 * (kStageRows + 32));
+  if (ql == 0 && act) {
+    G.len_a[q] = na;
+    G.is_rn[q] = (uint8_t)((uint32_t)r.nb_rn >> 31);
+    if (G.out_tok_off) {
+      G.out_tok_off[q] = tof;
+      if (q + 1 == G.n_pairs) G.out_tok_off[q + 1] = tof + n;
+    }
+    if (G.out_pos_off && G.masking) {
+      G.out_pos_off[q] = po;
+      if (q + 1 == G.n_pairs) G.out_pos_off[q + 1] = po + nm;
+    }
+  }
+  // both NT-token loads unconditional (an unneeded one reads the window start; dense is padded
+  // by 8 tokens on both sides and a B load starts at most 7 tokens before its window, an A load
+  // overhangs only by the tokens a shorter A leaves, which the next 8-token vector's select
+  // drops), blended when the pass needs them
+  uint4 ta[NV], tb[NV];
+  auto issue = [&](int32_t x) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int32_t xk = x + 8 * k, bx = xk - na;
+      ta[k] = *reinterpret_cast<const uint4*>(dense + r.aoff + (xk < na ? xk : 0));
+      tb[k] = *reinterpret_cast<const uint4*>(dense + r.boff + (bx >= -7 && xk < n ? bx : 0));
+    }
+  };
+  issue(NT * ql);
+  int32_t rk = 0;
+  if (G.masking) {
+    for (int i = 4 * ql; i < Lg.seqp; i += 4 * LP)
+      *reinterpret_cast<int4*>(dec + i) = make_int4(kNoMask, kNoMask, kNoMask, kNoMask);
+    wave_sync();
+    for (int j = ql; j < nm; j += LP) {
+      const int p = G.mpos[mb + j];  // position in [CLS] A [SEP] B [SEP]: never a literal
+      dec[p <= na ? p - 1 : p - 2] = G.mtok[mb + j];
+    }
+    wave_sync();
+  }
+  for (int32_t cb = 0;; cb += 128) {
+    const int32_t x = cb + NT * ql;
+    if (cb > 0) issue(x);
+    Tok8 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = __builtin_bit_cast(Tok8, blend8(ta[k], tb[k], na - x - 8 * k));
+    if (G.masking) {
+      int32_t dd[NT];
+#pragma unroll
+      for (int k = 0; k < NT / 4; ++k) {  // (x < seqp, as in gather_kernel)
+        const int4 d = *reinterpret_cast<const int4*>(dec + x + 4 * k);
+        dd[4 * k] = d.x;
+        dd[4 * k + 1] = d.y;
+        dd[4 * k + 2] = d.z;
+        dd[4 * k + 3] = d.w;
+      }
+      uint32_t mk = 0;
+#pragma unroll
+      for (int e = 0; e < NT; ++e) mk |= dd[e] != kNoMask ? 1u << e : 0u;
+      const uint32_t c = (uint32_t)__popc(mk);
+      uint32_t tot;
+      const uint32_t inc = seg_scan<LP>(c, lane, &tot);
+      int32_t rr = (int32_t)(inc - c);
+#pragma unroll
+      for (int e = 0; e < NT; ++e) {  // branch-free: an unmasked element writes the lane's trash entry
+        const bool m = (mk >> e) & 1u;
+        const int32_t xe = x + e, at = m ? rr : kStageRows + ql;
+        spos[at] = (uint16_t)(xe < na ? xe + 1 : xe + 2);
+        slab[at] = v[e >> 3][e & 7];
+        v[e >> 3][e & 7] = m && dd[e] != kKeep ? (uint16_t)dd[e] : v[e >> 3][e & 7];
+        rr += m ? 1 : 0;
+      }
+      wave_sync();
+      for (int32_t i = ql; i < (int32_t)tot; i += LP) {
+        G.out_pos[po + rk + i] = spos[i];
+        out_lab[po + rk + i] = slab[i];
+      }
+      rk += (int32_t)tot;
+      wave_sync();  // (the staging rows are rewritten by the next pass)
+    }
+    uint16_t* out = out_tok + tof;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int32_t xk = x + 8 * k;
+      if (xk + 7 < n) {
+        __builtin_nontemporal_store(v[k], reinterpret_cast<Tok8*>(out + xk));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (xk + e < n) __builtin_nontemporal_store(v[k][e], out + xk + e);
+      }
+    }
+    if (!ballot(n > cb + 128)) break;
+  }
+}
+
 }  // namespace
 }  // namespace lddl
 
@@ -2176,12 +2338,12 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   LDDL_HIP(hipMemcpyAsync(&n_kept_tok, P->kscan + P->n_kept_sent, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipMemcpyAsync(&max_docs, d_max_docs, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
-  // 4 tokens of padding on both sides: the gather's 16-byte loads may overhang a window
+  // 8 tokens of padding on both sides: the gather's 4- and 8-token loads may overhang a window
   {
     const int32_t ib = c->id_bytes();
     uint8_t* raw;
-    TRY(P->alloc(&raw, (n_kept_tok + 8) * ib, st));
-    P->dense = IdPtr{raw + 4 * ib, ib};
+    TRY(P->alloc(&raw, (n_kept_tok + 16) * ib, st));
+    P->dense = IdPtr{raw + 8 * ib, ib};
   }
   // replay mode: the planner launch's tail workgroups pack `dense` (plan_replay_kernel)
   const bool dense_in_plan = prm->rng == LDDL_RNG_REPLAY && n_part > 0;
@@ -2511,7 +2673,7 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, void* d_tokens, int6
   G.out_lab = d_lab;
   G.out_tok_off = d_tok_off;
   G.out_pos_off = d_pos_off;
-  GatherLds Lg{(P->seq + 127) / 128 * 128};
+  GatherLds Lg{(P->seq + 127) / 128 * 128, P->dense.ib};
   auto launch = [&](auto kern, int K) {
     const int64_t per_wg = (int64_t)2 * K * kGWaves;
     const int64_t nwg = (P->n_pairs + per_wg - 1) / per_wg;
@@ -2522,7 +2684,7 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, void* d_tokens, int6
   };
   const bool i16 = P->dense.ib == 2;
   if (P->seq <= 600) {
-    if (i16) launch(gather_kernel<2, uint16_t>, 2);
+    if (i16) launch(gather16_kernel<16>, 2);  // (4 pairs per wave, like K = 2; LP = 8: 35.3 ms, r04ze)
     else launch(gather_kernel<2, int32_t>, 2);
   } else {  // (LDS: seq-entry decision tables)
     if (i16) launch(gather_kernel<1, uint16_t>, 1);
