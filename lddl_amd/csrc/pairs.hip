@@ -1705,7 +1705,7 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
 #pragma unroll
     for (int g = NG - 1; g >= 0; --g)
       if (g < nvec) vec(g, jv[g]);
-  } else {
+  } else if (nvec > 0) {  // (a pair without masks has no draws to read)
     uint4 nxt = jp[nvec - 1];
     x.iota(nc);
     for (int g = nvec - 1; g >= 0; --g) {
