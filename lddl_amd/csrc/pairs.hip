@@ -1604,31 +1604,31 @@ struct ResolveArgs {
   int2* cnt;
 };
 
-// A lane's column of LDS entries; 16-bit: x[k * 64 + lane]; 8-bit (seq <= 256): dword k/4 of
-// lane l at (k/4) * 64 + l, so every access of the wave hits 64 distinct banks either way.
-template <typename T>
+// A lane's column of LDS entries; 16-bit: x[k * LW + lane]; 8-bit (seq <= 256): dword k/4 of
+// lane l at (k/4) * LW + l, so every access of the wave hits distinct banks either way.
+template <typename T, int LW>
 struct LaneCol;
-template <>
-struct LaneCol<uint16_t> {
+template <int LW>
+struct LaneCol<uint16_t, LW> {
   uint16_t* base;
   int lane;
-  __device__ uint32_t get(int k) const { return base[k * 64 + lane]; }
-  __device__ void set(int k, uint32_t v) { base[k * 64 + lane] = (uint16_t)v; }
+  __device__ uint32_t get(int k) const { return base[k * LW + lane]; }
+  __device__ void set(int k, uint32_t v) { base[k * LW + lane] = (uint16_t)v; }
   __device__ void iota(int n) {
     for (int k = 0; k < n; ++k) set(k, (uint32_t)k);
   }
 };
-template <>
-struct LaneCol<uint8_t> {
+template <int LW>
+struct LaneCol<uint8_t, LW> {
   uint8_t* base;
   int lane;
-  __device__ int at(int k) const { return ((k >> 2) << 8) | (lane << 2) | (k & 3); }
+  __device__ int at(int k) const { return ((k >> 2) * (4 * LW)) | (lane << 2) | (k & 3); }
   __device__ uint32_t get(int k) const { return base[at(k)]; }
   __device__ void set(int k, uint32_t v) { base[at(k)] = (uint8_t)v; }
   __device__ void iota(int n) {
     uint32_t* w = reinterpret_cast<uint32_t*>(base);
     for (int k = 0; k < n; k += 4)
-      w[(k >> 2) * 64 + lane] = (uint32_t)k | (uint32_t)(k + 1) << 8 | (uint32_t)(k + 2) << 16 |
+      w[(k >> 2) * LW + lane] = (uint32_t)k | (uint32_t)(k + 1) << 8 | (uint32_t)(k + 2) << 16 |
                                 (uint32_t)(k + 3) << 24;
   }
 };
@@ -1636,15 +1636,18 @@ struct LaneCol<uint8_t> {
 // D: draw type (uint8_t for target_seq_length <= 256, else uint16_t); a uint4 holds 16 / sizeof(D)
 // draws. NG > 0: all of a pair's draws (nc <= NG * 16 / sizeof(D)) are loaded up front, NG uint4
 // in flight per lane.
-template <typename T, typename D, int NG>
+// LW: pairs (lanes) per workgroup of one wave. Long pairs run with LW < 64: a lane's column is
+// seq entries, so at seq 512 a full wave holds 64 KB of LDS and only two fit a CU; fewer lanes
+// per wave put more waves (more independent step chains) on each SIMD.
+template <typename T, typename D, int NG, int LW = 64>
 __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_xb[];
   constexpr int kPerVec = 16 / (int)sizeof(D);  // draws per uint4
   const int lane = threadIdx.x;
-  LaneCol<T> x{reinterpret_cast<T*>(s_xb), lane};
+  LaneCol<T, LW> x{reinterpret_cast<T*>(s_xb), lane};
   // (XCD-contiguous blocks: a partition's pairs, their kept-sentence offsets and records meet
   // in one L2)
-  const int64_t q = xcd_block(blockIdx.x, gridDim.x) * 64 + lane;
+  const int64_t q = xcd_block(blockIdx.x, gridDim.x) * LW + lane;
   if (q >= R.n_pairs) return;
   const int64_t slot = R.src[q];
   const int64_t oq = R.dstq ? R.dstq[q] : 0;
@@ -2619,12 +2622,16 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
       if (prm->seq <= 131)  // nc <= 128: all draws in registers (8 uint4 of 1-byte draws)
         hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 8>), grid, dim3(64),
                            (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
+      // long pairs: 16 lanes (pairs) per wave (C3, seq 512: 106 ms with 64, 109 with 32, 93 with
+      // 16; profiles/r04fy_*)
       else if (prm->seq <= 256)  // candidate indices, positions and draws fit a byte
-        hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 0>), grid, dim3(64),
-                           (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
+        hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 0, 16>),
+                           dim3((unsigned)((P->n_pairs + 15) / 16)), dim3(16),
+                           (size_t)16 * (size_t)((prm->seq + 3) & ~3), st, RA);
       else
-        hipLaunchKernelGGL((fy_resolve_kernel<uint16_t, uint16_t, 0>), grid, dim3(64),
-                           (size_t)2 * 64 * (size_t)prm->seq, st, RA);
+        hipLaunchKernelGGL((fy_resolve_kernel<uint16_t, uint16_t, 0, 16>),
+                           dim3((unsigned)((P->n_pairs + 15) / 16)), dim3(16),
+                           (size_t)2 * 16 * (size_t)prm->seq, st, RA);
     }
     LDDL_HIP(hipGetLastError());
     TRY(scan_only(st));

@@ -120,13 +120,14 @@ def test_pairs_large_partition_vs_oracle(ctx):
         assert np.array_equal(pb[k], np.concatenate(exp[k])), k
 
 
-@pytest.mark.parametrize('seq,extra', [(128, 40000), (512, 40000)])
+@pytest.mark.parametrize('seq,extra', [(128, 40000), (512, 40000), (256, 0), (200, 0)])
 def test_pairs_wide_vs_oracle(tmp_path, seq, extra):
-    """A vocab of more than 65,536 entries against the oracle: 4-byte token ids and labels in
-    the pair tables and the gather, random-token mask decisions above 65,535. The extra vocab
+    """Against the oracle: a vocab of more than 65,536 entries (4-byte token ids and labels in
+    the pair tables and the gather, random-token mask decisions above 65,535; the extra vocab
     lines are bracketed, so no word of the text can produce them and the tokenization is
-    unchanged. (The gather's seq > 600 instantiation runs in test_native_gpu.py: the replay
-    planner stops at seq 512.)"""
+    unchanged), and seq 200 / 256 with the BERT-sized vocab (the 1-byte-draw mask replay at 16
+    pairs per wave, which the reference goldens at 64 / 128 / 512 do not reach). (The gather's
+    seq > 600 instantiation runs in test_native_gpu.py: the replay planner stops at seq 512.)"""
     from lddl_amd import synth
     from lddl_amd.context import Context
     from lddl_amd.pairs import make_pairs
