@@ -1709,12 +1709,22 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
     for (int g = NG - 1; g >= 0; --g)
       if (g < nvec) vec(g, jv[g]);
   } else if (nvec > 0) {  // (a pair without masks has no draws to read)
-    uint4 nxt = jp[nvec - 1];
+    // four vectors of draws in flight: one vector ahead left each vector's global load latency
+    // exposed every 8 steps (C3, seq 512: 93 -> 77.7 ms; eight ahead 80.1 ms, profiles/r04zj_*,
+    // r04zk_*)
+    auto ld = [&](int g) { return jp[g < 0 ? 0 : g]; };
+    const int top = nvec - 1;
+    constexpr int kPf = 4;
+    uint4 rv[kPf];
+#pragma unroll
+    for (int u = 0; u < kPf; ++u) rv[u] = ld(top - u);
     x.iota(nc);
-    for (int g = nvec - 1; g >= 0; --g) {
-      const uint4 jv = nxt;
-      if (g > 0) nxt = jp[g - 1];  // next vector of draws in flight
-      vec(g, jv);
+    for (int g = top; g >= 0; g -= kPf) {
+#pragma unroll
+      for (int u = 0; u < kPf; ++u) {
+        if (g >= u) vec(g - u, rv[u]);
+        rv[u] = ld(g - u - kPf);
+      }
     }
   }
   if (R.rec) {

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out/r04zj
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_pairs_gpu.py > gpurun_out/r04zj/tests.log 2>&1 || exit 1
+echo tests ok
+bash tools/run_trace_copies.sh r04zj/trace --workload c3 || exit 1
