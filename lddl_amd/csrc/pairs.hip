@@ -2629,7 +2629,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
       ResolveArgs RA{M.slots, P->n_pairs, P->desc, spool, jpool, P->mpos, P->kscan, P->dense, cls,
                      sep, M.dstq, P->rec, pcnt};
       const dim3 grid((unsigned)((P->n_pairs + 63) / 64));
-      if (prm->seq <= 131)  // nc <= 128: all draws in registers (8 uint4 of 1-byte draws)
+      if (prm->seq <= 131)  // nc <= 128: all draws in registers (8 uint4 of 1-byte draws); 64
+        // pairs per wave (C2: 10.2 ms; 32 per wave 11.9, 16 per wave 20.1, profiles/r04slw_*)
         hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 8>), grid, dim3(64),
                            (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
       // long pairs: 16 lanes (pairs) per wave (C3, seq 512: 106 ms with 64, 109 with 32, 93 with
