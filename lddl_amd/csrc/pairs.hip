@@ -77,6 +77,15 @@ struct KeepSent {
   const int32_t* len;
   __device__ int64_t operator()(int64_t s) const { return (len[s] & kLenMask) > 0; }
 };
+// both sentence scans in one pass: kept-sentence index and token offset. A dropped sentence has
+// no tokens, so the token scan over all sentences, read at the kept ones, is the kept-token scan.
+struct SentCounts {
+  const int32_t* len;
+  __device__ Sum2 operator()(int64_t s) const {
+    const int32_t l = len[s] & kLenMask;
+    return Sum2{l > 0 ? 1 : 0, l};
+  }
+};
 struct KeepDoc {
   const int64_t* ks_pos;  // exclusive scan of KeepSent, n_sent+1
   const int64_t* doc_sent_off;
@@ -85,16 +94,23 @@ struct KeepDoc {
   }
 };
 
+// kept sentence k = ks_pos[s]: its text start, length and token offset kscan[k] = tok_pos[s]
+// (kscan[n_kept] = the total, from thread n_sent)
 __global__ void scatter_sentences_kernel(const int64_t* sent_off, const int32_t* sent_len,
-                                         int64_t n_sent, const int64_t* ks_pos, int64_t* ks_start,
-                                         int32_t* ks_len) {
+                                         int64_t n_sent, const int64_t* ks_pos, const int64_t* tok_pos,
+                                         int64_t* ks_start, int32_t* ks_len, int64_t* kscan) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n_sent) return;
+  if (s > n_sent) return;
+  if (s == n_sent) {
+    kscan[ks_pos[n_sent]] = tok_pos[n_sent];
+    return;
+  }
   const int32_t l = sent_len[s];
   if ((l & kLenMask) == 0) return;
   const int64_t k = ks_pos[s];
   ks_start[k] = sent_off[s];
   ks_len[k] = l;
+  kscan[k] = tok_pos[s];
 }
 
 __global__ void scatter_docs_kernel(const int64_t* doc_sent_off, int64_t n_doc, const int64_t* ks_pos,
@@ -1284,15 +1300,6 @@ __global__ void __launch_bounds__(256) order_native_kernel(NativeArgs A) {
   A.src[q] = pb + (int64_t)x;
 }
 
-// total kept tokens (sizing of the mask pool)
-__global__ void __launch_bounds__(256) sum_tokens_kernel(const int32_t* __restrict__ sent_len,
-                                                        int64_t n, unsigned long long* out) {
-  int64_t acc = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    acc += sent_len[i] & kLenMask;
-  acc = wave_sum(acc);
-  if (lane_id() == 0) atomicAdd(out, (unsigned long long)acc);
-}
 
 // The final per-partition Fisher-Yates swaps (draws from plan_replay_kernel) for partitions too
 // large for shuffle_sort_kernel's LDS tables (more than min_np pairs): one lane swaps in global
@@ -1539,10 +1546,6 @@ __global__ void __launch_bounds__(256) densify_kernel(const int64_t* __restrict_
   densify_group(k0, ks_start, ks_len, kscan, n, ids, dense);
 }
 
-struct KeptLen {
-  const int32_t* len;
-  __device__ int64_t operator()(int64_t k) const { return len[k] & kLenMask; }
-};
 
 struct GatherArgs {
   const void* dense;     // kept tokens, packed (IdT)
@@ -2311,29 +2314,33 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   P->sep_id = sep;
   TRY(hipEventCreate(&P->ev[0]) == hipSuccess && hipEventCreate(&P->ev[1]) == hipSuccess
           ? 0 : (set_error("hipEventCreate failed"), -100));
-  int64_t *ks_pos, *kd_pos, *scratch, *part_npairs, *part_base;
-  const int64_t nscr = scan_scratch_elems(std::max(n_sent, n_doc) + n_part + 1);
+  int64_t *ks_pos, *tok_pos, *kd_pos, *scratch, *part_npairs, *part_base;
+  const int64_t nscr = 2 * scan_scratch_elems(std::max(n_sent, n_doc) + n_part + 1);  // (dual scans)
   TRY(P->alloc(&scratch, nscr, st));
-  // compaction
+  // compaction: kept-sentence index and token offset of every sentence in one scan
   TRY(P->alloc(&ks_pos, n_sent + 1, st));
-  if (scan_exclusive(KeepSent{d_sent_len}, n_sent, ks_pos, scratch, st) != hipSuccess)
+  TRY(P->alloc(&tok_pos, n_sent + 1, st));
+  if (scan_exclusive2(SentCounts{d_sent_len}, n_sent, ks_pos, tok_pos, scratch, st) != hipSuccess)
     TRY(-100);
   TRY(P->alloc(&kd_pos, n_doc + 1, st));
   if (scan_exclusive(KeepDoc{ks_pos, d_doc_sent_off}, n_doc, kd_pos, scratch, st) != hipSuccess)
     TRY(-100);
-  int64_t h_counts[2];
+  int64_t h_counts[3];
   LDDL_HIP(hipMemcpyAsync(&h_counts[0], ks_pos + n_sent, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipMemcpyAsync(&h_counts[1], kd_pos + n_doc, 8, hipMemcpyDeviceToHost, st));
+  LDDL_HIP(hipMemcpyAsync(&h_counts[2], tok_pos + n_sent, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
   P->n_kept_sent = h_counts[0];
   P->n_kept_doc = h_counts[1];
+  const int64_t n_kept_tok = h_counts[2];  // (dropped sentences have no tokens)
   TRY(P->alloc(&P->ks_start, P->n_kept_sent, st));
   TRY(P->alloc(&P->ks_len, P->n_kept_sent, st));
+  TRY(P->alloc(&P->kscan, P->n_kept_sent + 1, st));
   TRY(P->alloc(&P->kd_off, P->n_kept_doc + 1, st));
   TRY(P->alloc(&P->kp_off, n_part + 1, st));
-  if (n_sent)
-    hipLaunchKernelGGL(scatter_sentences_kernel, dim3((unsigned)((n_sent + 255) / 256)), dim3(256), 0,
-                       st, d_sent_off, d_sent_len, n_sent, ks_pos, P->ks_start, P->ks_len);
+  hipLaunchKernelGGL(scatter_sentences_kernel, dim3((unsigned)((n_sent + 256) / 256)), dim3(256), 0,
+                     st, d_sent_off, d_sent_len, n_sent, ks_pos, tok_pos, P->ks_start, P->ks_len,
+                     P->kscan);
   hipLaunchKernelGGL(scatter_docs_kernel, dim3((unsigned)((n_doc + 256) / 256)), dim3(256), 0, st,
                      d_doc_sent_off, n_doc, ks_pos, kd_pos, P->kd_off);
   unsigned long long* d_max_docs;
@@ -2343,12 +2350,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
                      d_part_doc_off, n_part, kd_pos, P->kp_off, d_max_docs);
   LDDL_HIP(hipGetLastError());
   // dense kept tokens
-  TRY(P->alloc(&P->kscan, P->n_kept_sent + 1, st));
-  if (scan_exclusive(KeptLen{P->ks_len}, P->n_kept_sent, P->kscan, scratch, st) != hipSuccess)
-    TRY(-100);
-  int64_t n_kept_tok = 0;
   unsigned long long max_docs = 0;
-  LDDL_HIP(hipMemcpyAsync(&n_kept_tok, P->kscan + P->n_kept_sent, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipMemcpyAsync(&max_docs, d_max_docs, 8, hipMemcpyDeviceToHost, st));
   LDDL_HIP(hipStreamSynchronize(st));
   // 8 tokens of padding on both sides: the gather's 4- and 8-token loads may overhang a window
@@ -2464,12 +2466,7 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   void* jpool = nullptr;
   const int jbytes = prm->seq <= 256 ? 1 : 2;  // every draw j_i < nc <= seq - 3
   if (prm->masking && n_sent) {
-    LDDL_HIP(hipMemsetAsync(pool_ctl, 0, 24, st));
-    hipLaunchKernelGGL(sum_tokens_kernel, dim3(1024), dim3(256), 0, st, d_sent_len, n_sent,
-                       pool_ctl);
-    unsigned long long kept_tokens = 0;
-    LDDL_HIP(hipMemcpyAsync(&kept_tokens, pool_ctl, 8, hipMemcpyDeviceToHost, st));
-    LDDL_HIP(hipStreamSynchronize(st));
+    const int64_t kept_tokens = n_kept_tok;
     cap = (int64_t)(2.0 * prm->masked_lm_ratio * prm->dup * (double)kept_tokens) +
           (int64_t)prm->dup * P->n_kept_sent / 2 + kPoolChunk * (n_part + 16);
     jcap = (int64_t)(1.6 * prm->dup * (double)kept_tokens) + 8 * slots +
