@@ -101,7 +101,8 @@ int lddl_ctx_destroy(lddl_ctx* ctx);
 int lddl_ctx_info(const lddl_ctx* ctx, int32_t* vocab_size, int32_t* special_ids,
                   int32_t* max_piece_bytes);
 /* Bytes per token id in the pair tables (lddl_pairs_emit tokens and labels, the render inputs):
- * 2 (uint16) when vocab_size <= 65536, else 4 (int32). */
+ * 2 (uint16) when vocab_size <= 65534 (two 16-bit values stay free for the gather's decision
+ * table), else 4 (int32). */
 int lddl_ctx_id_bytes(const lddl_ctx* ctx);
 /* device pointers to the vocab strings (for rendering ' '.join(tokens)): token i is
  * bytes[off[i] .. off[i+1]) */

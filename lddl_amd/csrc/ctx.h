@@ -153,8 +153,9 @@ struct lddl_ctx {
   uint64_t* d_vlong = nullptr;
   int32_t vocab_size = 0;
   // bytes per token id in the pair tables (dense kept tokens, sample tokens, labels): 2 when every
-  // id fits uint16 (vocab_size <= 65536: BERT's uncased 30,522 and cased 28,996), else 4
-  int32_t id_bytes() const { return vocab_size <= 65536 ? 2 : 4; }
+  // id fits uint16 with two values to spare for the gather's decision table (vocab_size <=
+  // 65,534: BERT's uncased 30,522 and cased 28,996), else 4
+  int32_t id_bytes() const { return vocab_size <= 65534 ? 2 : 4; }
   size_t lds_per_block = 0;         // hipDeviceAttributeMaxSharedMemoryPerBlock of `device`
   std::vector<std::string> tokens;  // host copy of the vocab lines
   lddl::DevArena arena;             // per-call temporaries (pair plans)

@@ -1577,10 +1577,14 @@ constexpr int kStageRows = 128;  // + 32 trash entries, one per lane of the half
 struct GatherLds {
   int32_t seqp;
   int32_t ib;  // bytes per label id (the staging row's width)
+  int32_t db;  // bytes per decision-table entry: 4 (int32), 2 in gather16_kernel (16-bit ids)
   __host__ __device__ size_t per_pair() const {
-    return (size_t)4 * seqp + (size_t)(kStageRows + 32) * (size_t)(2 + ib);
+    return (size_t)db * seqp + (size_t)(kStageRows + 32) * (size_t)(2 + ib);
   }
 };
+// gather16_kernel's 16-bit decision table: a token id, or one of two values no id takes (the
+// context uses 2-byte ids only for vocabs of <= 65,534 entries)
+constexpr uint16_t kNoMask16 = 0xFFFFu, kKeep16 = 0xFFFEu;
 
 // Replay masks, off the planner's sequential chain: one LANE per pair replays the recorded swaps
 // of random.shuffle(cand_indexes) (draws j_i, i = nc-1 .. 1) on a lane-private LDS column and
@@ -2010,9 +2014,9 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather16_kernel(GatherArgs G,
   const int32_t nm = G.masking ? r.nm : 0;
   const int64_t mb = r.moff;
   uint8_t* pb = g_smem + ((size_t)w * PW + qw) * Lg.per_pair();
-  int32_t* dec = reinterpret_cast<int32_t*>(pb);
-  uint16_t* spos = reinterpret_cast<uint16_t*>(pb + 4 * (size_t)Lg.seqp);
-  uint16_t* slab = reinterpret_cast<uint16_t*>(pb + 4 * (size_t)Lg.seqp + 2 * (kStageRows + 32));
+  uint16_t* dec = reinterpret_cast<uint16_t*>(pb);
+  uint16_t* spos = reinterpret_cast<uint16_t*>(pb + 2 * (size_t)Lg.seqp);
+  uint16_t* slab = reinterpret_cast<uint16_t*>(pb + 2 * (size_t)Lg.seqp + 2 * (kStageRows + 32));
   if (ql == 0 && act) {
     G.len_a[q] = na;
     G.is_rn[q] = (uint8_t)((uint32_t)r.nb_rn >> 31);
@@ -2041,12 +2045,13 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather16_kernel(GatherArgs G,
   issue(NT * ql);
   int32_t rk = 0;
   if (G.masking) {
-    for (int i = 4 * ql; i < Lg.seqp; i += 4 * LP)
-      *reinterpret_cast<int4*>(dec + i) = make_int4(kNoMask, kNoMask, kNoMask, kNoMask);
+    for (int i = 8 * ql; i < Lg.seqp; i += 8 * LP)
+      *reinterpret_cast<uint4*>(dec + i) = make_uint4(~0u, ~0u, ~0u, ~0u);  // kNoMask16
     wave_sync();
     for (int j = ql; j < nm; j += LP) {
       const int p = G.mpos[mb + j];  // position in [CLS] A [SEP] B [SEP]: never a literal
-      dec[p <= na ? p - 1 : p - 2] = G.mtok[mb + j];
+      const int32_t t = G.mtok[mb + j];
+      dec[p <= na ? p - 1 : p - 2] = t == kKeep ? kKeep16 : (uint16_t)t;
     }
     wave_sync();
   }
@@ -2057,18 +2062,17 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather16_kernel(GatherArgs G,
 #pragma unroll
     for (int k = 0; k < NV; ++k) v[k] = __builtin_bit_cast(Tok8, blend8(ta[k], tb[k], na - x - 8 * k));
     if (G.masking) {
-      int32_t dd[NT];
+      uint32_t dd[NT];
 #pragma unroll
-      for (int k = 0; k < NT / 4; ++k) {  // (x < seqp, as in gather_kernel)
-        const int4 d = *reinterpret_cast<const int4*>(dec + x + 4 * k);
-        dd[4 * k] = d.x;
-        dd[4 * k + 1] = d.y;
-        dd[4 * k + 2] = d.z;
-        dd[4 * k + 3] = d.w;
+      for (int k = 0; k < NT / 8; ++k) {  // (x < seqp, as in gather_kernel)
+        const uint4 d = *reinterpret_cast<const uint4*>(dec + x + 8 * k);
+        const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dd[8 * k + e] = (dw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
       }
       uint32_t mk = 0;
 #pragma unroll
-      for (int e = 0; e < NT; ++e) mk |= dd[e] != kNoMask ? 1u << e : 0u;
+      for (int e = 0; e < NT; ++e) mk |= dd[e] != kNoMask16 ? 1u << e : 0u;
       const uint32_t c = (uint32_t)__popc(mk);
       uint32_t tot;
       const uint32_t inc = seg_scan<LP>(c, lane, &tot);
@@ -2079,7 +2083,7 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather16_kernel(GatherArgs G,
         const int32_t xe = x + e, at = m ? rr : kStageRows + ql;
         spos[at] = (uint16_t)(xe < na ? xe + 1 : xe + 2);
         slab[at] = v[e >> 3][e & 7];
-        v[e >> 3][e & 7] = m && dd[e] != kKeep ? (uint16_t)dd[e] : v[e >> 3][e & 7];
+        v[e >> 3][e & 7] = m && dd[e] != kKeep16 ? (uint16_t)dd[e] : v[e >> 3][e & 7];
         rr += m ? 1 : 0;
       }
       wave_sync();
@@ -2688,7 +2692,7 @@ extern "C" int lddl_pairs_emit(lddl_pairs* P, void* stream, void* d_tokens, int6
   G.out_lab = d_lab;
   G.out_tok_off = d_tok_off;
   G.out_pos_off = d_pos_off;
-  GatherLds Lg{(P->seq + 127) / 128 * 128, P->dense.ib};
+  GatherLds Lg{(P->seq + 127) / 128 * 128, P->dense.ib, P->dense.ib == 2 && P->seq <= 600 ? 2 : 4};
   auto launch = [&](auto kern, int K) {
     const int64_t per_wg = (int64_t)2 * K * kGWaves;
     const int64_t nwg = (P->n_pairs + per_wg - 1) / per_wg;
