@@ -165,3 +165,53 @@ def test_pairs_wide_vs_oracle(tmp_path, seq, extra):
                               np.concatenate(exp[k]).astype(np.int64)), k
     if extra:
         assert np.concatenate(exp['tokens']).max() > 65535  # random-token decisions reach them
+
+
+def test_pairs_empty_and_dropped_inputs(ctx):
+    """Edge inputs of the compaction and layout: no partitions; partitions whose documents hold
+    only sentences that tokenize to nothing (dropped, pretrain.py:89-97); and such documents
+    between real ones (kept-sentence and token offsets across the gaps), the last against the
+    oracle."""
+    from lddl_amd.pairs import make_pairs
+    from oracle import oracle as O
+    vocab = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         'lddl_amd', 'assets', 'vocab_synth_uncased_30522.txt')
+    real = ['the quick brown fox jumps over the lazy dog .', 'a second sentence of the document .',
+            'and one more line here .', 'short .', 'the end of the first real document .']
+    other = ['another document begins here with words .', 'it also has a second sentence .',
+             'and a third sentence to pair .', 'final words .']
+    docs = [['   ', ' '], real, ['  ', '   ', ''], other, ['  ']]
+    sents = [s for d in docs for s in d]
+    text = ''.join(sents).encode()
+    sent_off = np.concatenate([[0], np.cumsum([len(s.encode()) for s in sents])]).astype(np.int64)
+    doc_sent_off = np.concatenate([[0], np.cumsum([len(d) for d in docs])]).astype(np.int64)
+    so = torch.from_numpy(sent_off).cuda()
+    ids, sl = ctx.tokenize(torch.from_numpy(np.frombuffer(text, np.uint8).copy()).cuda(), so)
+    dso = torch.from_numpy(doc_sent_off).cuda()
+
+    def run(part, seeds):
+        return make_pairs(ctx, so, ids, sl, dso, torch.from_numpy(np.asarray(part, np.int64)).cuda(),
+                          torch.from_numpy(np.asarray(seeds, np.int64)).cuda(), seq=64, dup=3,
+                          masking=True).to_host()
+
+    out = run([0], [])  # no partitions
+    assert len(out['len_a']) == 0 and len(out['tokens']) == 0
+    out = run([0, 1], [7])  # one partition of dropped sentences only
+    assert len(out['len_a']) == 0 and len(out['tokens']) == 0
+    out = run([0, 5], [7])  # dropped documents around real ones
+    tok = O.Tokenizer(vocab)
+    e_ids, e_off = tok.tokenize(np.frombuffer(text, np.uint8), sent_off)
+    # the reference drops empty sentences and then empty documents before pairing
+    lens = np.diff(e_off)
+    kept_docs = [[s for s in range(doc_sent_off[d], doc_sent_off[d + 1]) if lens[s] > 0]
+                 for d in range(len(docs))]
+    kept_docs = [d for d in kept_docs if d]
+    ks = [s for d in kept_docs for s in d]
+    k_off = np.concatenate([[0], np.cumsum([lens[s] for s in ks])]).astype(np.int64)
+    k_ids = np.concatenate([e_ids[e_off[s]:e_off[s + 1]] for s in ks]).astype(np.int32)
+    k_doc = np.concatenate([[0], np.cumsum([len(d) for d in kept_docs])]).astype(np.int64)
+    exp = O.partition_pairs(k_doc, k_off, k_ids, 7, 3, 64, True, tok.vocab_size,
+                            *(tok.token_id(t) for t in ('[CLS]', '[SEP]', '[MASK]')))
+    assert len(exp['len_a']) > 0
+    for k in ('tokens', 'num_tokens', 'len_a', 'pos', 'labels'):
+        assert np.array_equal(np.asarray(out[k]).astype(np.int64), np.asarray(exp[k]).astype(np.int64)), k
