@@ -936,7 +936,14 @@ def main():
     plan_gbs = plan_bytes / (plan_ms * 1e-3) / 1e9 if plan_ms > 0 else 0.0
     tok_bytes = n_bytes + 8 * (n_sent + 1) + 4 * pieces + 4 * n_sent
     achieved = tok_bytes / (tok_ms * 1e-3) / 1e9
-    stage_bytes = 9 * st['tokens']
+    # pair stage, compulsory bytes at this build's id width: every A/B token's id read
+    # once and written once (id_bytes each), per masked token a uint16 position and an id_bytes
+    # label, per pair its tok_off (8) + pos_off (8) + len_a (4) + is_random_next (1). SURVEY
+    # 8d's 9 B per output token assumed 4-byte ids; it is kept as a labelled secondary figure.
+    idb = ctx.id_bytes
+    ab_tokens = st['tokens'] - 3 * n_pairs
+    stage_bytes = 2 * idb * ab_tokens + (2 + idb) * st['masked'] + 21 * n_pairs
+    stage_bytes_survey = 9 * st['tokens']
     stage_gbs = stage_bytes / (pair_ms * 1e-3) / 1e9
     # per-kernel counters per launch from the committed PMC passes (profiles/pmc_*.json, made by
     # tools/prof_counters.sh + tools/make_pmc_json.py) when taken on the same batch size
@@ -991,7 +998,23 @@ def main():
                             'gather)', 'bound': 'hbm', 'achieved': stage_gbs,
                   'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': stage_gbs / HBM_PEAK_GBS,
                   'algorithmic_bytes_per_step': stage_bytes, 'stage_ms': pair_ms,
-                  'note': 'SURVEY 8d: 9 B per output token'}
+                  'bytes_per_output_token': stage_bytes / max(1, st['tokens']),
+                  'id_bytes': idb,
+                  'survey_9b': {'algorithmic_bytes_per_step': stage_bytes_survey,
+                                'frac': stage_bytes_survey / (pair_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                'note': 'SURVEY 8d: 9 B per output token (4-byte ids)'},
+                  'note': 'compulsory bytes at this build\'s id width: 2 x id_bytes per A/B token '
+                          '(read + write), (2 + id_bytes) per mask, 21 B per pair of metadata'}
+    # the north star's path-level number ("% of HBM roofline on the 1-GPU WordPiece+masking
+    # path"): tokenizer + pair-stage compulsory bytes over the whole step's time
+    path_bytes = tok_bytes + stage_bytes
+
+    def path_roof(ms, rng):
+        gbs = path_bytes / (ms * 1e-3) / 1e9
+        return {'rng': rng, 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': gbs / HBM_PEAK_GBS, 'algorithmic_bytes_per_step': path_bytes,
+                'ms_per_step': ms,
+                'frac_survey_9b': (tok_bytes + stage_bytes_survey) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     res = {
         'metric': 'WordPiece+MLM tokens/sec (1/2/4/8 MI355X) and % of HBM roofline',
         'value': out_tokens / dt,
@@ -1003,7 +1026,7 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
-        'dtype': 'int32',
+        'dtype': 'uint16' if ctx.id_bytes == 2 else 'int32',
         'data': 'synthetic',
         'config': {
             'workload': ('C2: synthetic English-like corpus (SURVEY 8d generator, seed {}), '
@@ -1037,6 +1060,9 @@ def main():
                                        issue('plan_replay_kernel', plan_ms)) if x],
     }
     res['roofline'] = plan_roof if plan_ms >= tok_ms else tok_roof
+    res['roofline_path'] = [path_roof(dt * 1e3 / args.steps, args.rng)]
+    if alt is not None:
+        res['roofline_path'].append(path_roof(alt['ms_per_step'], alt['rng']))
     if bal_ms is not None:
         res['balance_phases_ms_untimed_step'] = bal_ms
         res['balance'] = {'num_shards': n_shards, 'moved_rows_per_step': moved_all,

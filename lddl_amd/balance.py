@@ -101,10 +101,11 @@ def _host_staged(group):
     return dist.get_backend(group) != 'nccl'
 
 
-def gather_counts(local_counts, group=None):
-    """all_gather of the per-bin counts (RCCL when the tensor is on the GPU)."""
+def gather_counts(local_counts, group=None, collective=None):
+    """all_gather of the per-bin counts (RCCL when the tensor is on the GPU). collective=True runs
+    the collective even at world size 1 (the GPU test of the RCCL branch on one device)."""
     W = dist.get_world_size(group) if dist.is_initialized() else 1
-    if W == 1:
+    if W == 1 and not collective:
         return local_counts.reshape(1, -1).cpu().numpy()
     flat = local_counts.contiguous().reshape(-1)
     if flat.is_cuda and _host_staged(group):
@@ -409,8 +410,11 @@ class StreamBalancer:
     (a rank without rows passes an empty PairBatch); `all_shard_counts` is the layout so far
     (every shard N or N+1 rows per bin after every step)."""
 
-    def __init__(self, ctx, bin_size, nbins, num_shards=None, group=None, ops=None):
-        self.multi = dist.is_initialized() and dist.get_world_size(group) > 1
+    def __init__(self, ctx, bin_size, nbins, num_shards=None, group=None, ops=None,
+                 collective=None):
+        # collective: None = the exchange runs when the group has more than one rank; True forces
+        # it at world size 1 too (tests/test_balance_rccl_gpu.py: the RCCL branch on one GPU)
+        self.multi = dist.is_initialized() and (dist.get_world_size(group) > 1 or bool(collective))
         self.W = dist.get_world_size(group) if self.multi else 1
         self.me = dist.get_rank(group) if self.multi else 0
         self.S = self.W if num_shards is None else int(num_shards)
@@ -428,7 +432,7 @@ class StreamBalancer:
         mark('start')
         rb = RankBalance(self.ops, pb, self.bin_size, self.nbins, self.me, self.W, self.S)
         mark('bin')
-        counts = gather_counts(rb.local_counts, self.group)
+        counts = gather_counts(rb.local_counts, self.group, collective=self.multi)
         rb.set_plan(counts, self.prior)
         mark('plan')
         if self.multi:

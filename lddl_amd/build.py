@@ -87,11 +87,22 @@ def build_product(verbose=False, jobs=8, diag=False, variant=None, defines=()):
     flags = ['-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function',
              '-I' + os.path.join(ROOT, 'include'), '-I' + CSRC] + (['-DLDDL_STAMPS'] if diag else []) + \
         ['-D' + d for d in defines] + os.environ.get('LDDL_EXTRA_FLAGS', '').split()
+    # a library built with anything but the product flags (diagnostic stamps, variant defines,
+    # LDDL_EXTRA_FLAGS) reports lddl_build_id() = source id + '-' + a hash of those flags, so a
+    # PMC pass of such a build never passes for the product's
+    import hashlib
+    extra = flags[flags.index('-I' + CSRC) + 1:]
+    if extra:
+        fid = hashlib.sha256(' '.join(extra).encode()).hexdigest()[:8]
+        flags = flags + ['-DLDDL_BUILD_VARIANT="-{}"'.format(fid)]
+    # the objects of a directory are rebuilt whenever its compile flags change
+    stamp = os.path.join(objdir, '.flags')
+    force = not os.path.exists(stamp) or open(stamp).read() != ' '.join(flags)
     objs, jobs_list = [], []
     for s in srcs:
         o = os.path.join(objdir, os.path.basename(s) + '.o')
         objs.append(o)
-        if _newer(o, [s] + headers):
+        if force or _newer(o, [s] + headers):
             if s.endswith('.hip'):
                 cmd = [HIPCC, '--offload-arch=' + ARCH, '-x', 'hip'] + flags + ['-c', s, '-o', o]
             else:
@@ -101,6 +112,8 @@ def build_product(verbose=False, jobs=8, diag=False, variant=None, defines=()):
         for out in ex.map(_run, jobs_list):
             if verbose and out:
                 print(out)
+    with open(stamp, 'w') as f:
+        f.write(' '.join(flags))
     if _newer(lib, objs):
         _run([HIPCC, '-shared', '-fPIC', '--offload-arch=' + ARCH, '-o', lib] + objs +
              ['-lpthread'])

@@ -31,8 +31,8 @@ files) writes the balancer's layout directly: `shard-<k>.parquet_<b>` (or `shard
 unbinned) with N or N+1 samples per bin, plus `.num_samples.json` (lddl/dask/load_balance.py:
 90-92, 372-378) — what get_bert_pretrain_data_loader consumes. `--balance-plan stream` (default)
 balances every GPU batch in HBM as it is produced (lddl_amd/balance.py: RCCL all-gather of the
-batch's per-bin counts, round-robin deal of each bin's rows over the shards, all-to-all-v of the
-rows owned by other ranks), so HBM holds one batch at any corpus size and each shard file grows
+batch's per-bin counts, per-rank shard quotas, all-to-all-v of only each bin's surplus rows over
+a rank's quota), so HBM holds one batch at any corpus size and each shard file grows
 by one row group per batch; `--balance-plan reference` writes the part files and runs the
 drop-in balance_dask_output over them (the reference's exact shard contents).
 """
@@ -480,27 +480,35 @@ class ShardWriters:
         ranges = [(s, b) + tuple(bb.shard_range(m, b)) for m, s in enumerate(bb.shards)
                   for b in range(self.nbins)]
 
+        writes = []  # this batch's write futures: its pinned copy lives until they finish
+
         def job(stream=None):
             rd = drd.to_host(stream)
             for f in self.pending:
                 f.result()
             self.pending = [self.pool.submit(self._append, (s, b), rd, r0, r1)
                             for s, b, r0, r1 in ranges if r1 > r0]
+            writes.extend(self.pending)
         if copier is None:
             job()
             return
         nb = drd.nbytes
+        # a batch's bytes count until its WRITES have finished (not only its copy job), so the
+        # pinned host copies held at once stay within max_inflight_bytes plus the newest batch
         while self.jobs and (len(self.jobs) >= 2 or
-                             sum(b for _, b in self.jobs) + nb > self.max_inflight_bytes):
-            self.jobs.pop(0)[0].result()
-        self.jobs.append((copier.submit(job, _copy_stream(ctx)), nb))
+                             sum(b for _, b, _ in self.jobs) + nb > self.max_inflight_bytes):
+            j, _, ws = self.jobs.pop(0)
+            j.result()
+            for f in ws:
+                f.result()
+        self.jobs.append((copier.submit(job, _copy_stream(ctx)), nb, writes))
 
     def close(self):
         """Finish the writes; shards of a bin that received no rows get an empty file (every bin
         has all shards, as the loader requires)."""
         import pyarrow.parquet as pq
         from ... import output
-        for j, _ in self.jobs:
+        for j, _, _ in self.jobs:
             j.result()
         self.jobs = []
         for f in self.pending:
@@ -864,14 +872,17 @@ def attach_args(parser=None):
                              'part.* files (see --balance-plan)')
     parser.add_argument('--balance-plan', choices=['stream', 'reference'], default='stream',
                         help="lddl_amd, with --num-shards: 'stream' balances each GPU batch in "
-                             "HBM as it is produced (round-robin deal of every bin's rows over "
-                             "the shards, RCCL exchange; one batch resident); 'reference' writes "
+                             "HBM as it is produced (per-rank shard quotas from the all-gathered "
+                             "bin counts: only each bin's surplus over a rank's quota crosses "
+                             "ranks, and every shard ends each batch with N or N+1 rows per bin; "
+                             "one batch resident); 'reference' writes "
                              "the part files and runs balance_dask_output over them, the "
                              "reference's exact shard layout")
     parser.add_argument('--max-inflight-render-bytes', type=int, default=_default_inflight_bytes(),
                         help='pinned host bytes of rendered batches waiting for their parquet '
                              'writes (default: 1/8 of host memory, 2-16 GiB); the GPU waits for '
-                             'the writes beyond it')
+                             'the writes beyond it; the newest batch always proceeds, so the peak is this '
+                             'bound plus one rendered batch')
     parser.add_argument('--max-open-files', type=int, default=None,
                         help='--num-shards: most shard files kept open at once (default: as many '
                              'as RLIMIT_NOFILE allows, raised to its hard limit); above it, each '

@@ -69,10 +69,13 @@ class HostStager:
         hv = buf.numpy()
         for a, o in zip(arrays, offs):
             hv[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
-        d = torch.empty(n, dtype=torch.uint8, device=device)
-        d.copy_(buf[:n], non_blocking=True)
-        ev = self._done[k] = torch.cuda.Event()
-        ev.record()
+        # the copy and its slot-reuse event on the DESTINATION device's current stream (the
+        # current device may be another one: an event recorded there would not cover the copy)
+        with torch.cuda.device(device):
+            d = torch.empty(n, dtype=torch.uint8, device=device)
+            d.copy_(buf[:n], non_blocking=True)
+            ev = self._done[k] = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(device))
         out = []
         for a, o in zip(arrays, offs):
             t = d[o:o + max(a.nbytes, 1)]

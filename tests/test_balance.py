@@ -223,3 +223,65 @@ def test_stream_virtual_gpu_balanced_moves_nothing(gpu_tables):
     # per bin, each rank holds floor or ceil of its share and so does its quota: at most W - 1
     # rows move per bin (the round-robin deal of round 3 moved (W - 1) / W of all rows)
     assert moved <= (W - 1) * nb and moved < 0.2 * pb.n_pairs
+
+
+@pytest.fixture
+def nccl_world1():
+    """A world-size-1 `nccl` (RCCL) process group on cuda:0, torn down after the test."""
+    import datetime
+    assert not dist.is_initialized()
+    dist.init_process_group('nccl', init_method='tcp://127.0.0.1:{}'.format(_free_port()),
+                            rank=0, world_size=1, timeout=datetime.timedelta(seconds=120),
+                            device_id=torch.device('cuda', 0))
+    try:
+        yield
+    finally:
+        dist.destroy_process_group()
+
+
+def _same_out(a, b):
+    ta, tb = a[0], b[0]
+    assert set(ta) == set(tb)
+    for k in ta:
+        np.testing.assert_array_equal(np.asarray(ta[k]), np.asarray(tb[k]), err_msg=k)
+    for x, y in zip(a[1:], b[1:]):
+        np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+
+
+@pytest.mark.gpu
+def test_rccl_branch_world1(gpu_tables, nccl_world1):
+    """The device-tensor (RCCL) branch of the balance's collectives, which multi-GPU runs take and
+    the gloo tests never do (lddl/dask/load_balance.py:210-223 replaced by all_gather /
+    all_to_all_single over RCCL): per-bin counts all-gathered from a device tensor; all-to-all-v
+    of a 16-bit id column moved as bytes, of int32 row metadata and of empty splits, all on the
+    device; then StreamBalancer's exchange path forced on at world size 1, equal to the in-process
+    driver (stream_virtual) batch by batch."""
+    from lddl_amd import balance as B
+    ctx, pb = gpu_tables
+    dev = pb.tok_off.device
+    assert dist.get_backend() == 'nccl' and not B._host_staged(None)
+    c = torch.arange(3, 67, dtype=torch.int64, device=dev)
+    np.testing.assert_array_equal(B.gather_counts(c, collective=True), c.cpu().numpy()[None])
+    ids = pb.tokens[:4099]
+    assert ids.element_size() == ctx.id_bytes
+    b8 = ids.view(torch.uint8)
+    r = B._a2a((b8, [b8.numel()], [b8.numel()]), None)
+    assert r.is_cuda and r.dtype == torch.uint8 and torch.equal(r.view(ids.dtype), ids)
+    meta = torch.arange(4 * 777, dtype=torch.int32, device=dev) * 7 - 5
+    r = B._a2a((meta, [meta.numel()], [meta.numel()]), None)
+    assert r.is_cuda and torch.equal(r, meta)
+    r = B._a2a((torch.zeros(0, dtype=torch.uint8, device=dev), [0], [0]), None)
+    assert r.is_cuda and r.numel() == 0
+    # StreamBalancer with the exchange forced on (nothing moves at W = 1, but every split is
+    # computed, packed, sent over RCCL and unpacked) against stream_virtual
+    n = pb.n_pairs
+    parts = _split_rows(pb, [0, n // 3, n // 3, n])  # the middle batch is empty
+    sb = StreamBalancer(ctx, 8, 64, num_shards=4, collective=True)
+    assert sb.multi
+    ops = B.HipOps(ctx)
+    ref = stream_virtual(ops, [[p] for p in parts], 8, 64, num_shards=4)
+    for p, rv in zip(parts, ref):
+        bb = sb.step(p)
+        assert bb.moved_rows == 0
+        _same_out(_to_host_out(bb, ops), _to_host_out(rv[0], ops))
+    np.testing.assert_array_equal(sb.all_shard_counts, sum(r[0].all_shard_counts for r in ref))
