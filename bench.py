@@ -449,10 +449,13 @@ def run_c5(args):
             t = time.perf_counter()
             tw = tn = 0.0
             gev = []
+            timed.kept = []
             for _ in range(k_steps):
                 n0 = time.perf_counter()
                 b = next(it)
                 tn += time.perf_counter() - n0
+                if with_train:  # the same batches are replayed by train_step_alone
+                    timed.kept.append(b)
                 real += b['attention_mask'].sum()
                 slots += b['input_ids'].numel()
                 if with_train:
@@ -503,9 +506,12 @@ def run_c5(args):
         cg = {k: c1[k] - c0.get(k, 0) for k in ('usage_usec', 'nr_periods', 'nr_throttled',
                                                   'throttled_usec') if k in c1}
         train_gpu_ms, train_gpu_pct = timed.gpu_ms, timed.gpu_ms_pct
-        # the same training step alone, on batches already resident in HBM (no loader in the
-        # loop): what the step costs when nothing else runs beside it
-        res_b = [next(it) for _ in range(8)]
+        # the same training step alone: the timed loop's own batches (same shapes, same order),
+        # already resident in HBM, no loader in the loop - what the step costs when nothing else
+        # runs beside it. (Round 4 replayed 8 other batches: their padded lengths, not the loader,
+        # made that figure differ from the in-loop step.)
+        res_b = timed.kept
+        timed.kept = []
         torch.cuda.synchronize()
         ra = []
         t_alone = time.perf_counter()
@@ -518,6 +524,8 @@ def run_c5(args):
         torch.cuda.synchronize()
         t_alone = time.perf_counter() - t_alone
         alone_gms = [a.elapsed_time(z) for a, z in ra]
+        padded_len_mean = float(np.mean([-(-x['input_ids'].size(1) // pad_mult) * pad_mult
+                                         for x in res_b]))
         del res_b
         host_phases = {k: round(v / args.steps * 1e3, 3) for k, v in
                        zip(('forward', 'backward', 'optimizer'), phase_s)}
@@ -559,8 +567,9 @@ def run_c5(args):
                     'gpu_ms': float(np.mean(alone_gms)),
                     'gpu_ms_p50_p90_max': [round(float(np.percentile(alone_gms, q)), 2)
                                            for q in (50, 90, 100)],
-                    'note': 'the same step on 8 HBM-resident batches in turn, no loader in the '
-                            'loop'},
+                    'padded_len_mean': padded_len_mean,
+                    'note': 'the same step replayed on the timed loop\'s own batches (same '
+                            'shapes and order), HBM-resident, no loader in the loop'},
                 'worker_start_method': args.c5_mp,
                 'pinned_stager_allocations': loaders[0]._stager.allocations,
                 'train_step_host_ms_by_phase': host_phases,

@@ -781,6 +781,19 @@ static_assert(kPcs * 64 * 4 >= 64 * kNorm, "normalised-word rows must fit the pi
 
 #ifdef LDDL_STAMPS
 __device__ unsigned long long* g_tok_tl;  // diagnostic build: [wave][2] s_memrealtime start / end
+// diagnostic build: shader cycles per region, summed over waves (kTokRegions entries)
+__device__ unsigned long long* g_tok_reg;
+constexpr int kTokRegions = 6;  // 0 banks, 1 phase A, 2 phase B, 3 place, 4 queue shift, 5 chunk
+#define TOK_STAMP(r)                                                     \
+  do {                                                                   \
+    const unsigned long long _now = __builtin_amdgcn_s_memtime();       \
+    reg_acc[r] += _now - reg_last;                                       \
+    reg_last = _now;                                                     \
+  } while (0)
+#else
+#define TOK_STAMP(r) \
+  do {               \
+  } while (0)
 #endif
 __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
     Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
@@ -792,6 +805,8 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
   __shared__ StreamLds s_w[kBW];
 #ifdef LDDL_STAMPS
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long reg_acc[kTokRegions] = {0, 0, 0, 0, 0, 0};
+  unsigned long long reg_last = __builtin_amdgcn_s_memtime();
 #endif
   for (int c = threadIdx.x; c < 128; c += blockDim.x) s_ascii[c] = tab_entry(T, (uint32_t)c);
   for (int c = threadIdx.x; c < 256; c += blockDim.x) {
@@ -884,6 +899,7 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
 
       // resolve and place the complete units [0, m), then drop them from the queue
       auto flush = [&](int m) {
+        TOK_STAMP(0);
         // phase A: specials and single-piece words
         int nh = 0;
         {  // all rounds' text loads, then all first table loads, then the checks: one latency each
@@ -939,6 +955,7 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
           }
         }
         wave_sync();
+        TOK_STAMP(1);
         // phase B in chunks of 64 hard units, each chunk placed with the units before the next one
         int placed = 0;
         for (int h0 = 0; h0 < nh; h0 += 64) {
@@ -972,10 +989,13 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
           }
           wave_sync();
           const int lim = h0 + 64 < nh ? (int)W.h_idx[h0 + 64] : m;
+          TOK_STAMP(2);
           place(placed, lim);
           placed = lim;
+          TOK_STAMP(3);
         }
         place(placed, m);
+        TOK_STAMP(3);
         // drop the processed units: < 128 starts and < 128 ends remain (read all, then write)
         const int rs = ns - m, re = ne - m;
         int32_t a0 = 0, a1 = 0, e0 = 0, e1 = 0;
@@ -991,6 +1011,7 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
         wave_sync();
         ns = rs;
         ne = re;
+        TOK_STAMP(4);
       };
 
       // ---- the chunk's banks ----
@@ -1128,6 +1149,7 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
         ne += (int)__popcll(UEp);
       }
       wave_sync();
+      TOK_STAMP(0);
       while (ne > 0) flush(ne < kSF ? ne : kSF);
       // the chunk's sentences
       for (int j = lane; j < n; j += 64) {
@@ -1141,6 +1163,7 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
       }
       wave_sync();  // before the next chunk reuses s_off / r_cnt
     }
+    TOK_STAMP(5);
     int32_t nc = 0;
     if (lane == 0) nc = atomicAdd(chunk_ctr, kChunk);
     nc = __builtin_amdgcn_readfirstlane(nc);
@@ -1152,6 +1175,8 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
     g_tok_tl[2 * wv] = rt0;
     g_tok_tl[2 * wv + 1] = __builtin_amdgcn_s_memrealtime();
   }
+  if (lane == 0 && g_tok_reg)
+    for (int r = 0; r < kTokRegions; ++r) atomicAdd(g_tok_reg + r, reg_acc[r]);
 #endif
 }
 
@@ -1206,9 +1231,13 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     if (const char* g = getenv("LDDL_TOKENIZE_GRID")) grid = std::max<int64_t>(1, std::min<int64_t>(grid, atoll(g)));
 #ifdef LDDL_STAMPS
     unsigned long long* tl = nullptr;
+    unsigned long long* rg = nullptr;
     LDDL_HIP(hipMalloc(&tl, 16 * grid * kBW));
     LDDL_HIP(hipMemsetAsync(tl, 0, 16 * grid * kBW, st));
     LDDL_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tok_tl), &tl, sizeof(tl), 0, hipMemcpyHostToDevice, st));
+    LDDL_HIP(hipMalloc(&rg, 8 * kTokRegions));
+    LDDL_HIP(hipMemsetAsync(rg, 0, 8 * kTokRegions, st));
+    LDDL_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tok_reg), &rg, sizeof(rg), 0, hipMemcpyHostToDevice, st));
 #endif
     // the first grid x kBW chunks are taken statically (chunk w by wave w)
     const int64_t first = std::min<int64_t>(grid * kBW * kChunk, (int64_t)INT32_MAX);
@@ -1243,6 +1272,15 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
       }
       fprintf(stderr, "\n");
       LDDL_HIP(hipFree(tl));
+      unsigned long long r[kTokRegions];
+      LDDL_HIP(hipMemcpy(r, rg, sizeof r, hipMemcpyDeviceToHost));
+      unsigned long long tot = 0;
+      for (int q = 0; q < kTokRegions; ++q) tot += r[q];
+      static const char* names[kTokRegions] = {"banks", "phaseA", "phaseB", "place", "qshift", "chunk"};
+      fprintf(stderr, "[tok regions] wave-cycle shares:");
+      for (int q = 0; q < kTokRegions; ++q) fprintf(stderr, " %s %.1f%%", names[q], 100.0 * r[q] / (tot ? tot : 1));
+      fprintf(stderr, "\n");
+      LDDL_HIP(hipFree(rg));
     }
 #endif
   }

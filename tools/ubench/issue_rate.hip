@@ -3,6 +3,7 @@
 // adds (8 registers round robin); cycles from s_memtime (shader clock) per wave.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <string>
 #include <vector>
 
 constexpr int ITER = 4096;
@@ -83,13 +84,64 @@ __global__ void probe(unsigned long long* cyc, int* sink) {
   if (r == 0x7fffffff) sink[0] = r;
 }
 
-int main() {
+// Co-residency: a SALU-only kernel and a VALU-only kernel on two streams at
+// the same time, each with `wps` waves per SIMD, against each alone. If the CU's scalar unit and
+// the SIMDs' vector pipes serve different waves in the same cycles, the pair takes ~max of the
+// two alone; if issue is shared, ~their sum.
+static void corun(int ncu, unsigned long long* cyc, unsigned long long* cyc2, int* sink) {
+  hipStream_t s1, s2;
+  hipStreamCreateWithFlags(&s1, hipStreamNonBlocking);
+  hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+  const int reps = 20;
+  for (int wps : {1, 2, 4}) {
+    const int threads = 256 * wps, blocks = ncu;
+    auto run = [&](bool sa, bool va, float* t_s, float* t_v, float* t_all) {
+      hipEvent_t a, b1, b2;
+      hipEventCreate(&a);
+      hipEventCreate(&b1);
+      hipEventCreate(&b2);
+      hipDeviceSynchronize();
+      hipEventRecord(a, 0);
+      hipDeviceSynchronize();
+      for (int r = 0; r < reps; ++r) {
+        if (sa) hipLaunchKernelGGL(probe<0>, dim3(blocks), dim3(threads), 0, s1, cyc, sink);
+        if (va) hipLaunchKernelGGL(probe<1>, dim3(blocks), dim3(threads), 0, s2, cyc2, sink);
+      }
+      hipEventRecord(b1, s1);
+      hipEventRecord(b2, s2);
+      hipEventSynchronize(b1);
+      hipEventSynchronize(b2);
+      float x = 0, y = 0;
+      hipEventElapsedTime(&x, a, b1);
+      hipEventElapsedTime(&y, a, b2);
+      if (t_s) *t_s = x;
+      if (t_v) *t_v = y;
+      if (t_all) *t_all = x > y ? x : y;
+    };
+    float ts = 0, tv = 0, cs = 0, cv = 0, call = 0;
+    run(true, false, &ts, nullptr, nullptr);
+    run(false, true, nullptr, &tv, nullptr);
+    run(true, true, &cs, &cv, &call);
+    printf("corun waves/SIMD %d+%d: SALU alone %.3f ms, VALU alone %.3f ms (sum %.3f, max %.3f); "
+           "together: SALU stream %.3f ms, VALU stream %.3f ms, both done %.3f ms -> overlap %.0f%%\n",
+           wps, wps, ts, tv, ts + tv, ts > tv ? ts : tv, cs, cv, call,
+           100.0 * (ts + tv - call) / (ts < tv ? ts : tv));
+  }
+}
+
+int main(int argc, char** argv) {
   int ncu = 0;
   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
   unsigned long long* cyc;
   int* sink;
   hipMalloc(&cyc, sizeof(unsigned long long) * ncu * 32);
   hipMalloc(&sink, 4);
+  if (argc > 1 && std::string(argv[1]) == "corun") {
+    unsigned long long* cyc2;
+    hipMalloc(&cyc2, sizeof(unsigned long long) * ncu * 32);
+    corun(ncu, cyc, cyc2, sink);
+    return 0;
+  }
   const char* names[5] = {"salu32", "valu32", "mix16+16", "mul_lo32", "mad_u24"};
   for (int mode = 0; mode < 5; ++mode) {
     for (int wps : {1, 2, 4, 8}) {  // waves per SIMD: workgroups of 4 * wps waves, one per CU
