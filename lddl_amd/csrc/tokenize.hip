@@ -262,6 +262,22 @@ struct Pcs {
   __device__ int32_t get(int q) const { return b[64 * q]; }
 };
 
+// Diagnostic build: work counters of phase B (per lane; summed at the kernel's end).
+struct TokStats {
+#ifdef LDDL_STAMPS
+  uint64_t c[10];
+  __device__ void add(int i, uint64_t v) { c[i] += v; }
+  // once per wave-level iteration: only the first active lane counts
+  __device__ void wave(int i) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(true);
+    if ((uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(m)) c[i] += 1;
+  }
+#else
+  __device__ void add(int, uint64_t) {}
+  __device__ void wave(int) {}
+#endif
+};
+
 // Bytes 8 .. len-1 (len 13..32) of a against piece id's zero-padded 32-byte copy (the hash key
 // already matched bytes 0..11).
 __device__ inline bool tail_match(const Tables& T, int32_t id, const B32& a, int len) {
@@ -306,13 +322,17 @@ __device__ inline int32_t probe_finish(const Tables& T, const B32& a, int len, P
 // Bloom candidates for the pieces starting at a's first byte: bit L-1 set iff the filter may
 // contain (cont, bytes[0, L)), L = 1 .. maxl (<= 32).
 __device__ inline uint32_t bloom_candidates32(const uint32_t* bloom, const B32& a, int maxl,
-                                              uint32_t cont) {
+                                              uint32_t cont, TokStats* ts = nullptr) {
   uint32_t h = 0, cand = 0;
 #pragma unroll
   for (int L = 1; L <= 32; ++L) {
     // wave-uniform exit (lanes past their own maxl compute don't-care bits, masked below): no
     // exec-mask bookkeeping per length
     if (!ballot(L <= maxl)) break;
+    if (ts) {
+      ts->wave(4);
+      ts->add(5, L <= maxl);
+    }
     const uint64_t wv = L <= 8 ? a.w0 : L <= 16 ? a.w1 : L <= 24 ? a.w2 : a.w3;
     const uint32_t byte = (uint32_t)(wv >> (8 * ((L - 1) & 7))) & 0xFFu;
     h = h * kBloomP + byte + 1u;
@@ -331,42 +351,71 @@ __device__ inline uint32_t bloom_candidates32(const uint32_t* bloom, const B32& 
 // slots are loaded together: a lane waits on ONE table round trip per piece in the common case.
 // (Round 3 probed the full length alone first, then two candidates per round trip: 21.9 ms per
 // 2 GiB against 20.7 now; three candidates per trip spilled VGPRs and took 22.1 ms, r04o.)
-__device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v, int nb,
-                           uint64_t ends, Pcs& pc, bool first_probe_missed = false) {
-  int n = 0, start = 0;
-  while (start < nb) {
-    const B32 a = shr_bytes(v, start);
-    const uint32_t cont = start > 0;
-    const uint64_t e = ends >> start;  // bit L: a piece of length L may end here
-    int len = nb - start < T.max_piece_bytes ? nb - start : T.max_piece_bytes;
-    {  // the longest length <= len that ends on a character boundary (bit L-1 of okl: length L)
-      const uint64_t okl = (e >> 1) & ((1ull << len) - 1ull);
-      len = okl ? 64 - __clzll(okl) : 0;
+// One greedy longest-match step of a word held in registers: the longest vocab piece (continuation
+// iff start > 0) starting at byte `start`; returns its id and length, or -1 (no piece matches:
+// the word is [UNK]). Per step, the Bloom filter (LDS) gives the lengths that may be pieces (every
+// vocab piece is in it: the longest candidate that hits is the greedy match), and the two longest
+// candidates' home slots are loaded together, so a lane waits on ONE table round trip per piece
+// in the common case. first_probe_missed: phase A already probed the whole word (start 0).
+__device__ inline int32_t piece_step(const Tables& T, const uint32_t* bloom, const B32& v, int nb,
+                                     uint64_t ends, int start, bool first_probe_missed, int& out_len,
+                                     TokStats* ts = nullptr) {
+  const B32 a = shr_bytes(v, start);
+  const uint32_t cont = start > 0;
+  const uint64_t e = ends >> start;  // bit L: a piece of length L may end here
+  int len = nb - start < T.max_piece_bytes ? nb - start : T.max_piece_bytes;
+  {  // the longest length <= len that ends on a character boundary (bit L-1 of okl: length L)
+    const uint64_t okl = (e >> 1) & ((1ull << len) - 1ull);
+    len = okl ? 64 - __clzll(okl) : 0;
+  }
+  uint32_t cand = len > 0 ? bloom_candidates32(bloom, a, len, cont, ts) & (uint32_t)(e >> 1) : 0u;
+  // (the caller may already know that the whole word is not one piece)
+  if (first_probe_missed && start == 0 && len == nb) cand &= ~(1u << (len - 1));
+  int32_t id = -1;
+  while (cand) {
+    if (ts) {
+      ts->wave(6);
+      ts->add(7, 1);
     }
-    uint32_t cand = len > 0 ? bloom_candidates32(bloom, a, len, cont) & (uint32_t)(e >> 1) : 0u;
-    // (the caller may already know that the whole word is not one piece)
-    if (first_probe_missed && start == 0 && len == nb) cand &= ~(1u << (len - 1));
-    int32_t id = -1;
-    while (cand) {
-      const int l1 = 32 - __clz(cand);
-      const uint32_t r1 = cand & ~(1u << (l1 - 1));
-      const int l2 = r1 ? 32 - __clz(r1) : 0;
-      const Probe q1 = probe_first(T, a, l1, cont);
-      const Probe q2 = probe_first(T, a, l2 ? l2 : l1, cont);
-      id = probe_finish(T, a, l1, q1);
+    const int l1 = 32 - __clz(cand);
+    const uint32_t r1 = cand & ~(1u << (l1 - 1));
+    const int l2 = r1 ? 32 - __clz(r1) : 0;
+    const Probe q1 = probe_first(T, a, l1, cont);
+    const Probe q2 = probe_first(T, a, l2 ? l2 : l1, cont);
+    id = probe_finish(T, a, l1, q1);
+    if (id >= 0) {
+      len = l1;
+      break;
+    }
+    if (l2) {
+      id = probe_finish(T, a, l2, q2);
       if (id >= 0) {
-        len = l1;
+        len = l2;
         break;
       }
-      if (l2) {
-        id = probe_finish(T, a, l2, q2);
-        if (id >= 0) {
-          len = l2;
-          break;
-        }
-      }
-      cand = l2 ? r1 & ~(1u << (l2 - 1)) : 0u;
     }
+    cand = l2 ? r1 & ~(1u << (l2 - 1)) : 0u;
+  }
+  out_len = len;
+  return id;
+}
+
+// Greedy longest-match WordPiece (HF WordPiece::tokenize) of a normalised word of nb <= 32 bytes
+// held in registers. ends: bit e set iff a piece may end at byte e (a UTF-8 character boundary;
+// all bits for ASCII). Returns the piece count written to pc, or -1 if more than kPcs pieces.
+// (Round 3 probed the full length alone first, then two candidates per round trip: 21.9 ms per
+// 2 GiB against 20.7 now; three candidates per trip spilled VGPRs and took 22.1 ms, r04o.)
+__device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v, int nb,
+                           uint64_t ends, Pcs& pc, bool first_probe_missed = false,
+                           TokStats* ts = nullptr) {
+  int n = 0, start = 0;
+  while (start < nb) {
+    if (ts) {
+      ts->wave(2);
+      ts->add(3, 1);
+    }
+    int len;
+    const int32_t id = piece_step(T, bloom, v, nb, ends, start, first_probe_missed, len, ts);
     if (id < 0) {  // no piece: the whole word is [UNK]
       pc.put(0, T.special_id[kUnk]);
       return 1;
@@ -608,6 +657,70 @@ struct UnitWord {
   int status;
 };
 
+// unit_word's generic (non-ASCII) normalisation without an LDS row: the normalised bytes are
+// appended straight into the four registers of the word (rare path; kCP's phase B, whose lanes
+// normalise at different times and so cannot share the piece columns as row space).
+__device__ inline void put_byte32(B32& v, int pos, uint32_t b) {
+  const uint64_t x = (uint64_t)(b & 0xFFu) << (8 * (pos & 7));
+  const int q = pos >> 3;
+  v.w0 |= q == 0 ? x : 0ull;
+  v.w1 |= q == 1 ? x : 0ull;
+  v.w2 |= q == 2 ? x : 0ull;
+  v.w3 |= q == 3 ? x : 0ull;
+}
+__device__ inline uint32_t get_byte32(const B32& v, int pos) {
+  const int q = pos >> 3;
+  const uint64_t w = q == 0 ? v.w0 : q == 1 ? v.w1 : q == 2 ? v.w2 : v.w3;
+  return (uint32_t)(w >> (8 * (pos & 7))) & 0xFFu;
+}
+__device__ UnitWord unit_word_reg(const Tables& T, const uint32_t* s_ascii,
+                                  const uint8_t* __restrict__ text, int64_t start, int len) {
+  UnitWord u;
+  u.status = 0;
+  B32 v{0, 0, 0, 0};
+  int nb = 0;
+  int64_t j = start;
+  const int64_t je = start + len;
+  while (j < je) {
+    const uint32_t b0 = text[j];
+    uint32_t cp, e;
+    if (b0 < 0x80) {
+      cp = b0;
+      e = s_ascii[b0];
+      ++j;
+    } else {
+      cp = utf8_next(text, je, j);
+      e = tab_entry(T, cp);
+    }
+    if ((e >> 30) == kDrop) continue;
+    uint8_t ob[12];
+    int olen;
+    if (e & kIdent) olen = put_utf8(ob, cp);
+    else if (e & kMulti) {
+      const uint8_t* p = T.pool + (e & 0xFFFFFFu);
+      olen = p[0];
+      for (int q = 0; q < olen; ++q) ob[q] = p[2 + q];
+    } else olen = put_utf8(ob, e & 0x1FFFFFu);
+    if (nb + olen > kNorm) {
+      u.status = -1;
+      return u;
+    }
+    for (int q = 0; q < olen; ++q) put_byte32(v, nb + q, ob[q]);
+    nb += olen;
+  }
+  u.nb = nb;
+  u.v = v;
+  if (nb == 0) {
+    u.status = 1;
+    return u;
+  }
+  uint64_t ends = 1ull << nb;
+  for (int e = 1; e < nb; ++e)
+    if ((get_byte32(v, e) & 0xC0) != 0x80) ends |= 1ull << e;
+  u.ends = ends;
+  return u;
+}
+
 __device__ UnitWord unit_word(const Tables& T, const uint32_t* s_ascii, const uint8_t* __restrict__ text,
                               int64_t n_bytes, int64_t start, int len, bool unit_slow, uint8_t* w) {
   UnitWord u;
@@ -778,6 +891,15 @@ struct alignas(16) StreamLds {
   alignas(16) int32_t pcs[kPcs * 64];
 };
 static_assert(kPcs * 64 * 4 >= 64 * kNorm, "normalised-word rows must fit the piece columns");
+// kCP: phase A's results go to the wave's global scratch, so only the unit queue and the chunk's
+// sentence tables stay in LDS (3.8 KB per wave instead of 7.0: two workgroups fit a CU)
+struct alignas(16) StreamLdsCP {
+  int32_t q_s[kQ];
+  int32_t q_e[kQ];
+  int32_t trash[64];
+  int32_t s_off[kChunk + 1];
+  int32_t r_cnt[kChunk];
+};
 
 #ifdef LDDL_STAMPS
 __device__ unsigned long long* g_tok_tl;  // diagnostic build: [wave][2] s_memrealtime start / end
@@ -795,18 +917,48 @@ constexpr int kTokRegions = 6;  // 0 banks, 1 phase A, 2 phase B, 3 place, 4 que
   do {               \
   } while (0)
 #endif
-__global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
+// Chunk-phased resolution (kCP): phase A still runs every kSF queued units, but its results go to
+// a per-wave global scratch (L2-resident) as one 32-bit record per unit, and the hard units to a
+// list there; phase B and placement run once per chunk (or when the scratch fills), phase B over
+// the whole chunk's hard units with lane refill: a lane that finishes its word takes the next one,
+// so the wave's piece-steps are not bounded by the longest word of each 64 (round 4: 43 % of the
+// lanes busy per piece-step, 1 phase-B pass per flush with ~48 hard units).
+// record: bits 0..20 piece id (easy; bit 21 literal [CLS]/[SEP]) or, with kRecHard, the hard-list
+// index (bits 0..12) and, once phase B is done, the piece count + 1 (bits 13..20; 0: the lane
+// kernel); bits 22..28 the unit's sentence slot in the chunk
+constexpr int kSpanCap = 8192;     // text bytes per (sub-)chunk in kCP mode (13-bit indices)
+constexpr int kRecCap = kSpanCap;  // unit records per sub-chunk (a unit has >= 1 byte)
+constexpr int kHardCap = kSpanCap;
+constexpr uint32_t kRecHard = 1u << 29, kRecCS = 1u << 21, kRecVal = (1u << 21) - 1;
+constexpr int kRecSlotShift = 22;
+static_assert(kChunk <= 128, "sentence slot: 7 bits of the record");
+// per-wave scratch (32-bit words): records, hard list (start, len | slow << 16 | known-miss << 17 |
+// record index << 18),
+// hard pieces [h * kPcs + q], hard piece counts (-1: the sentence goes to the lane kernel)
+constexpr int kScrRec = 0, kScrHl = kRecCap, kScrHp = kScrHl + 2 * kHardCap,
+              kScrHn = kScrHp + kPcs * kHardCap, kScrWords = kScrHn + kHardCap;
+
+template <bool kCP, int kW, int kWPE, int kCPRoundsInFlight = 3>  // kW waves per workgroup,
+// >= kWPE waves per SIMD; kCP: phase-A rounds of 64 units in flight together
+__global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
     Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
     int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
-    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr) {
+    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr,
+    uint32_t* __restrict__ scratch) {
   __shared__ uint32_t s_ascii[128];
   __shared__ uint8_t s_cls[256];
   __shared__ uint32_t s_bloom[kBloomWords];
-  __shared__ StreamLds s_w[kBW];
+  using WL = std::conditional_t<kCP, StreamLdsCP, StreamLds>;
+  __shared__ WL s_w[kW];
 #ifdef LDDL_STAMPS
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long reg_acc[kTokRegions] = {0, 0, 0, 0, 0, 0};
   unsigned long long reg_last = __builtin_amdgcn_s_memtime();
+  TokStats tstat;
+  for (int q = 0; q < 10; ++q) tstat.c[q] = 0;
+  TokStats* tsp = &tstat;
+#else
+  TokStats* tsp = nullptr;
 #endif
   for (int c = threadIdx.x; c < 128; c += blockDim.x) s_ascii[c] = tab_entry(T, (uint32_t)c);
   for (int c = threadIdx.x; c < 256; c += blockDim.x) {
@@ -820,7 +972,13 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
   for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
   __syncthreads();
   const int lane = lane_id();
-  StreamLds& W = s_w[threadIdx.x >> 6];
+  WL& W = s_w[threadIdx.x >> 6];
+  uint32_t* __restrict__ wscr =
+      kCP ? scratch + ((int64_t)blockIdx.x * kW + (threadIdx.x >> 6)) * kScrWords : nullptr;
+  uint32_t* __restrict__ s_rec = wscr + kScrRec;
+  int2* __restrict__ s_hl = reinterpret_cast<int2*>(wscr + kScrHl);
+  int32_t* __restrict__ s_hp = reinterpret_cast<int32_t*>(wscr + kScrHp);
+  int32_t* __restrict__ s_hn = reinterpret_cast<int32_t*>(wscr + kScrHn);
   // sentence indices fit int32 (lddl_tokenize: n_sent < INT32_MAX - 2^22)
   const int32_t n_sent32 = (int32_t)n_sent;
   // Chunks: wave w starts with chunk w, then takes the next unclaimed chunk from chunk_ctr
@@ -828,13 +986,34 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
   // tail: waves of one SIMD are issued oldest first, so the first finishes ~25 % before the last.
   int32_t c0;
   {
-    const int64_t w = (int64_t)blockIdx.x * kBW + (threadIdx.x >> 6);
+    const int64_t w = (int64_t)blockIdx.x * kW + (threadIdx.x >> 6);
     c0 = w * kChunk < n_sent32 ? (int32_t)(w * kChunk) : n_sent32;
   }
   const uint64_t upto = (2ull << lane) - 1;  // lanes <= this one (lane 63: all)
 
   while (c0 < n_sent32) {
-    const int32_t n = n_sent32 - c0 < kChunk ? n_sent32 - c0 : kChunk;
+   const int32_t cend = n_sent32 - c0 < kChunk ? n_sent32 : c0 + kChunk;
+   // kCP: the claimed chunk is processed in sub-chunks of at most kSpanCap bytes (so that its units,
+   // hence its records and hard units, fit the wave's scratch: a unit has >= 1 byte); a sentence
+   // longer than that alone goes to the lane kernel
+   for (int32_t cb = c0; cb < cend;) {
+    int32_t n = cend - cb;
+    if constexpr (kCP) {
+      const int64_t a0 = sent_off[cb];
+      int32_t fit = 0;
+      for (int j0 = 0; j0 < n; j0 += 64) {
+        const int j = j0 + lane;
+        fit += __popcll(ballot(j < n && sent_off[cb + j + 1] - a0 <= (int64_t)kSpanCap));
+      }
+      if (fit == 0) {  // one sentence of more than kSpanCap bytes
+        if (lane == 0) fb_list[atomicAdd(fb_n, 1u)] = cb;
+        cb += 1;
+        continue;
+      }
+      n = fit;
+    }
+    const int32_t c0 = cb;  // (this sub-chunk's first sentence)
+    cb += n;
     const int64_t A = sent_off[c0];
     const int64_t span64 = sent_off[c0 + n] - A;
     if (span64 >= kMaxSpan) {  // pathological chunk (>= 256 MiB of text): the lane kernel
@@ -860,6 +1039,7 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
 
       // place queue units [u0, u1) (all resolved) in order: segmented scan per sentence
       auto place = [&](int u0, int u1) {
+        if constexpr (!kCP) {
         for (int r0 = u0; r0 < u1; r0 += 64) {
           const int u = r0 + lane;
           const bool act = u < u1;
@@ -893,12 +1073,14 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
           if (seg_last) W.r_cnt[slot] += seg_excl + npc;  // (count bits only: < 2^28 pieces)
           wave_sync();
         }
+        }
       };
 
       int ns = 0, ne = 0;  // queued unit starts / ends
 
       // resolve and place the complete units [0, m), then drop them from the queue
       auto flush = [&](int m) {
+        if constexpr (!kCP) {
         TOK_STAMP(0);
         // phase A: specials and single-piece words
         int nh = 0;
@@ -958,8 +1140,16 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
         TOK_STAMP(1);
         // phase B in chunks of 64 hard units, each chunk placed with the units before the next one
         int placed = 0;
+        if (tsp) {
+          tsp->wave(8);
+          tsp->add(9, lane == 0 ? m : 0);
+        }
         for (int h0 = 0; h0 < nh; h0 += 64) {
           const int hn = nh - h0 < 64 ? nh - h0 : 64;
+          if (tsp) {
+            tsp->wave(0);
+            tsp->add(1, lane < hn);
+          }
           int u = -1, st = 0;
           UnitWord uw;
           uw.status = 1;
@@ -978,7 +1168,7 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
           int npc = 0;
           if (lane < hn) {
             Pcs pc{W.pcs + lane};
-            if (uw.status == 0) npc = wordpiece32(T, s_bloom, uw.v, uw.nb, uw.ends, pc, known_miss);
+            if (uw.status == 0) npc = wordpiece32(T, s_bloom, uw.v, uw.nb, uw.ends, pc, known_miss, tsp);
             else if (uw.status < 0) npc = -1;
             if (npc < 0) {  // the sentence goes to the lane kernel
               atomicOr(&W.r_cnt[sent_of(st)], kRFb);
@@ -996,6 +1186,241 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
         }
         place(placed, m);
         TOK_STAMP(3);
+        // drop the processed units: < 128 starts and < 128 ends remain (read all, then write)
+        const int rs = ns - m, re = ne - m;
+        int32_t a0 = 0, a1 = 0, e0 = 0, e1 = 0;
+        if (lane < rs) a0 = W.q_s[m + lane];
+        if (lane + 64 < rs) a1 = W.q_s[m + 64 + lane];
+        if (lane < re) e0 = W.q_e[m + lane];
+        if (lane + 64 < re) e1 = W.q_e[m + 64 + lane];
+        wave_sync();
+        if (lane < rs) W.q_s[lane] = a0;
+        if (lane + 64 < rs) W.q_s[64 + lane] = a1;
+        if (lane < re) W.q_e[lane] = e0;
+        if (lane + 64 < re) W.q_e[64 + lane] = e1;
+        wave_sync();
+        ns = rs;
+        ne = re;
+        TOK_STAMP(4);
+        }
+      };
+
+      // ---- chunk-phased resolution (kCP) ----
+      int nrec = 0, nhard = 0;  // records / hard units of this sub-chunk in the scratch
+
+      // phase B over the scratch's hard units [0, nhard), lanes refilled from the list. Latency
+      // hiding: the list is read 64 entries at a time into a register window (a refilled lane
+      // takes its entry from the window by a lane shuffle), and a refilled lane's text load is
+      // issued at the end of one iteration and consumed at the end of the next, so it overlaps
+      // the busy lanes' probes instead of adding a round trip to each iteration. Finished units
+      // write their piece count into their record (placement then reads records only).
+      auto phase_b_cp = [&]() {
+        enum { kIdle = 0, kLoading = 1, kBusy = 2 };
+        int state = kIdle, h = -1, nb = 0, start = 0, np = 0, hlen = 0;
+        uint32_t hflags = 0;
+        B32 v{0, 0, 0, 0};
+        uint64_t ends = 0;
+        int nextu = 0;  // wave-uniform: the next unassigned hard unit
+        int wbase = 0;  // wave-uniform: the window holds entries [wbase, wbase + 64)
+        int2 win = lane < nhard ? s_hl[lane] : make_int2(0, 0);
+        auto finish = [&](int npc) {
+          const int ri = (int)(hflags >> 18);  // the unit's record index
+          s_rec[ri] = (s_rec[ri] & ~kRecVal) | (uint32_t)h | ((uint32_t)(npc + 1) << 13);
+          state = kIdle;
+          h = -1;
+        };
+        auto refill = [&]() {
+          const bool want = state == kIdle;
+          const uint64_t Wm = ballot(want);
+          const int room = wbase + 64 - nextu;  // window entries not yet taken
+          const int take = __popcll(Wm) < room ? __popcll(Wm) : room;
+          const int k = (int)popc_below(Wm);
+          const int cand = nextu + k;
+          const int src = (nextu - wbase + k) & 63;
+          const int2 he = make_int2(__shfl(win.x, src, 64), __shfl(win.y, src, 64));
+          if (want && k < take && cand < nhard) {
+            h = cand;
+            hlen = he.y & 0xFFFF;
+            hflags = (uint32_t)he.y & 0xFFFF0000u;
+            const int st = he.x;
+            const bool slow = (he.y >> 16) & 1;
+            if (!slow && hlen <= 32 && T.ascii_mode != 0) {
+              v = load32(text, n_bytes, A + st);  // consumed at the end of the next iteration
+              state = kLoading;
+            } else {  // normalised now, into registers (rare)
+              const UnitWord uw = unit_word_reg(T, s_ascii, text, A + st, hlen);
+              if (uw.status != 0) {  // empty (every char dropped) or too long
+                finish(uw.status > 0 ? 0 : -1);
+              } else {
+                v = uw.v;
+                nb = uw.nb;
+                ends = uw.ends;
+                start = 0;
+                np = 0;
+                state = kBusy;
+              }
+            }
+          }
+          nextu = nextu + take < nhard ? nextu + take : nhard;
+          if (nextu == wbase + 64 && nextu < nhard) {  // the next window
+            wbase = nextu;
+            win = wbase + lane < nhard ? s_hl[wbase + lane] : make_int2(0, 0);
+          }
+        };
+        refill();
+        while (ballot(state != kIdle) || nextu < nhard) {
+          if (state == kBusy) {
+            if (tsp) {
+              tsp->wave(2);
+              tsp->add(3, 1);
+            }
+            int len;
+            const int32_t id = piece_step(T, s_bloom, v, nb, ends, start, ((hflags >> 17) & 1) != 0, len, tsp);
+            if (id < 0) {  // no piece: the whole word is [UNK]
+              s_hp[h * kPcs] = T.special_id[kUnk];
+              finish(1);
+            } else if (np == kPcs) {  // too many pieces: the sentence goes to the lane kernel
+              finish(-1);
+            } else {
+              s_hp[h * kPcs + np] = id;
+              ++np;
+              start += len;
+              if (start >= nb) finish(np);
+            }
+          } else if (state == kLoading) {  // its text (loaded last iteration) is in v
+            if (T.ascii_mode == 1) v = B32{swar_lower(v.w0), swar_lower(v.w1), swar_lower(v.w2), swar_lower(v.w3)};
+            nb = hlen;
+            ends = ~0ull;
+            start = 0;
+            np = 0;
+            state = kBusy;
+          }
+          refill();
+        }
+      };
+
+      // place the scratch's records [0, nrec) in order (segmented scan per sentence slot); a hard
+      // unit's record holds its hard index and (piece count + 1) << 13 (0: the lane kernel)
+      auto place_cp = [&]() {
+        uint32_t nxt = lane < nrec ? s_rec[lane] : 0u;
+        for (int r0 = 0; r0 < nrec; r0 += 64) {
+          const int u = r0 + lane;
+          const bool act = u < nrec;
+          const uint32_t rec = nxt;
+          nxt = u + 64 < nrec ? s_rec[u + 64] : 0u;  // next group's records in flight
+          const bool hard = (rec & kRecHard) != 0;
+          const int hv = hard ? (int)(rec & 0x1FFF) : (int)(rec & kRecVal);
+          int npc = act ? (hard ? (int)((rec >> 13) & 0xFF) - 1 : 1) : 0;
+          const int slot = act ? (int)((rec >> kRecSlotShift) & 127u) : -1;
+          if (npc < 0) {  // the sentence goes to the lane kernel
+            atomicOr(&W.r_cnt[slot], kRFb);
+            npc = 0;
+          }
+          const int incl = wave_incl_scan(npc);
+          const int excl = incl - npc;
+          const int prev_slot = wave_prev(slot);
+          const uint64_t F = ballot(act && (lane == 0 || slot != prev_slot));
+          const int s0 = 63 - __clzll(F & upto);
+          const int seg_excl = excl - __shfl(excl, s0, 64);
+          const int next_slot = wave_next(slot);
+          const bool seg_last = act && (lane == 63 || u + 1 >= nrec || next_slot != slot);
+          if (act) {
+            const int o = (W.r_cnt[slot] & kRCnt) + seg_excl;
+            const int64_t bb = A + W.s_off[slot];
+            if (hard) {
+              for (int q = 0; q < npc; ++q)
+                if (o + q < max_pieces) ids[bb + o + q] = s_hp[hv * kPcs + q];
+            } else if (o < max_pieces) {
+              ids[bb + o] = hv;
+              if (rec & kRecCS) atomicOr(&W.r_cnt[slot], kLenHasClsSep);
+            }
+          }
+          wave_sync();
+          if (seg_last) W.r_cnt[slot] += seg_excl + npc;  // (count bits only: < 2^28 pieces)
+          wave_sync();
+        }
+      };
+
+      auto chunk_flush_cp = [&]() {
+        TOK_STAMP(0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        phase_b_cp();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        TOK_STAMP(2);
+        place_cp();
+        TOK_STAMP(3);
+        nrec = nhard = 0;
+      };
+
+      // phase A of the queued units [0, m): a record per unit, hard units to the list; then drop
+      // them from the queue
+      auto flush_cp = [&](int m) {
+        TOK_STAMP(0);
+        // kRF rounds of 64 units in flight at a time (all their text loads, then all their first
+        // table loads, then the checks); fewer rounds in flight hold fewer registers
+        constexpr int kR = kSF / 64;
+        constexpr int kRF = kCPRoundsInFlight;
+        static_assert(kR % kRF == 0, "phase A rounds");
+#pragma unroll 1
+        for (int r0 = 0; r0 < kR; r0 += kRF) {
+          bool elig[kRF], hardr[kRF];
+          int lenr[kRF], str[kRF];  // lenr: length | sentence slot << 16 | slow << 23
+          int32_t resr[kRF];        // id | kRecCS
+          B32 vv[kRF];
+          Probe pr[kRF];
+#pragma unroll
+          for (int r = 0; r < kRF; ++r) {
+            const int u = 64 * (r0 + r) + lane;
+            elig[r] = hardr[r] = false;
+            lenr[r] = str[r] = 0;
+            resr[r] = 0;
+            if (u < m) {
+              const int32_t qs = W.q_s[u];
+              const int st = qs & 0xFFFF, kind = (qs >> 28) & 7;
+              const int len = W.q_e[u] - st + 1;
+              lenr[r] = len | (qs & 0x7F0000) | (qs < 0 ? 1 << 23 : 0);  // slot from the bank loop
+              str[r] = st;
+              if (kind >= 2) {
+                resr[r] = T.special_id[kind - 2] | ((kind - 2 == kCls || kind - 2 == kSep) ? (int32_t)kRecCS : 0);
+              } else if (qs >= 0 && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32) {
+                elig[r] = true;
+                vv[r] = load32(text, n_bytes, A + st);
+              } else {
+                hardr[r] = true;
+              }
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < kRF; ++r)
+            if (elig[r]) {
+              if (T.ascii_mode == 1)
+                vv[r] = B32{swar_lower(vv[r].w0), swar_lower(vv[r].w1), swar_lower(vv[r].w2), swar_lower(vv[r].w3)};
+              pr[r] = probe_first(T, vv[r], lenr[r] & 0xFFFF, 0);
+            }
+#pragma unroll
+          for (int r = 0; r < kRF; ++r) {
+            bool km = false;
+            if (elig[r]) {
+              resr[r] = probe_finish(T, vv[r], lenr[r] & 0xFFFF, pr[r]);
+              hardr[r] = km = resr[r] < 0;
+            }
+            const int u = 64 * (r0 + r) + lane;
+            const uint64_t H = ballot(hardr[r]);
+            const int hidx = nhard + (int)popc_below(H);
+            if (u < m) {
+              const uint32_t slotb = (uint32_t)((lenr[r] >> 16) & 127) << kRecSlotShift;
+              s_rec[nrec + u] = hardr[r] ? (kRecHard | (uint32_t)hidx | slotb) : ((uint32_t)resr[r] | slotb);
+            }
+            if (hardr[r])  // start, len | slow << 16 | known miss << 17 | record index << 18
+              s_hl[hidx] = make_int2(str[r], (lenr[r] & 0xFFFF) | ((lenr[r] >> 23) & 1) << 16 |
+                                                 (km ? 1 << 17 : 0) | (nrec + u) << 18);
+            nhard += __popcll(H);
+          }
+        }
+        nrec += m;
+        TOK_STAMP(1);
         // drop the processed units: < 128 starts and < 128 ends remain (read all, then write)
         const int rs = ns - m, re = ne - m;
         int32_t a0 = 0, a1 = 0, e0 = 0, e1 = 0;
@@ -1042,15 +1467,20 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
         const uint32_t x = x0 + lane;
         const bool in = x < span;
         uint64_t BRK = 0;
+        // kCP: this lane's sentence slot (the last sentence starting at or before byte x, as
+        // sent_of), carried in its unit start so that phase A needs no search
+        int32_t lslot = jn - 1;
         while (nextS < x0 + 64) {
           BRK |= 1ull << (nextS - x0);
+          if constexpr (kCP) lslot += (x0 + lane >= nextS) ? 1 : 0;
           ++jn;
           nextS = jn <= n ? (uint32_t)__builtin_amdgcn_readfirstlane(W.s_off[jn]) : 0xFFFFFFFFu;
         }
         const uint32_t v = s_cls[byte];
         const uint64_t VALID = ballot(in);
         uint64_t RUN, UNIT, CONT, SL = 0;
-        int32_t sval = (int32_t)x;
+        // unit start: chunk-relative byte | kind << 28 (| slot << 16 in kCP: x < kSpanCap)
+        int32_t sval = kCP ? (int32_t)(x | (uint32_t)lslot << 16) : (int32_t)x;
         if (!(ballot(v >= kFSlow) | insc | k1 | k2 | k3)) {  // plain ASCII bank
           RUN = ballot(v == kFRun) & VALID;
           UNIT = VALID & ~ballot(v == kFSep);
@@ -1104,7 +1534,8 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
           const uint64_t ISO = ballot(cat == kCatIso), LEAD = ballot(cplen > 0);
           UNIT = ballot(cat != kCatSep);
           CONT = (RUN & ((RUN << 1) | cin) & ~BRK) | (ISO & ~LEAD) | inside;
-          sval = (int32_t)(x | ((uint32_t)(spk >= 0 ? 2 + spk : 0) << 28));
+          sval = (int32_t)(x | ((uint32_t)(spk >= 0 ? 2 + spk : 0) << 28) |
+                           (kCP ? (uint32_t)lslot << 16 : 0u));
           SL = ballot(slow && cat != kCatSep);
           k1 = (V2 | V3 | V4) >> 63;
           k2 = (V3 | V4) >> 62;
@@ -1138,7 +1569,8 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
         CONTp = CONT;
         if (ne >= kSF) {
           wave_sync();
-          flush(kSF);
+          if constexpr (kCP) flush_cp(kSF);
+          else flush(kSF);
         }
       }
       {  // the last bank's ends (nothing continues past the chunk)
@@ -1150,7 +1582,12 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
       }
       wave_sync();
       TOK_STAMP(0);
-      while (ne > 0) flush(ne < kSF ? ne : kSF);
+      if constexpr (kCP) {
+        while (ne > 0) flush_cp(ne < kSF ? ne : kSF);
+        chunk_flush_cp();
+      } else {
+        while (ne > 0) flush(ne < kSF ? ne : kSF);
+      }
       // the chunk's sentences
       for (int j = lane; j < n; j += 64) {
         const int32_t rc = W.r_cnt[j];
@@ -1163,6 +1600,7 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
       }
       wave_sync();  // before the next chunk reuses s_off / r_cnt
     }
+   }
     TOK_STAMP(5);
     int32_t nc = 0;
     if (lane == 0) nc = atomicAdd(chunk_ctr, kChunk);
@@ -1171,12 +1609,17 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
   }
 #ifdef LDDL_STAMPS
   if (lane == 0 && g_tok_tl) {
-    const int64_t wv = (int64_t)blockIdx.x * kBW + (threadIdx.x >> 6);
+    const int64_t wv = (int64_t)blockIdx.x * kW + (threadIdx.x >> 6);
     g_tok_tl[2 * wv] = rt0;
     g_tok_tl[2 * wv + 1] = __builtin_amdgcn_s_memrealtime();
   }
   if (lane == 0 && g_tok_reg)
     for (int r = 0; r < kTokRegions; ++r) atomicAdd(g_tok_reg + r, reg_acc[r]);
+  if (g_tok_reg)
+    for (int q = 0; q < 10; ++q) {
+      const uint64_t v = wave_sum(tstat.c[q]);
+      if (lane == 0) atomicAdd(g_tok_reg + kTokRegions + q, (unsigned long long)v);
+    }
 #endif
 }
 
@@ -1223,31 +1666,51 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
                        d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + kFbHead,
                        reinterpret_cast<uint32_t*>(fb));
   } else {
-    LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_batch_kernel, 64 * kBW, 0));
+    // A/B: chunk-phased phase B + placement, with 16 / 12 / 10 / 8 waves per workgroup
+    const int cpw = !path ? 0 : !strcmp(path, "cp") ? 16 : !strcmp(path, "cp12") ? 12
+                  : !strcmp(path, "cp10") ? 10 : !strcmp(path, "cp8") ? 8 : 0;
+    const bool cp = cpw > 0;
+    const void* kfn = cpw == 16 ? (const void*)tokenize_batch_kernel<true, 16, 1, 3>
+                    : cpw == 12 ? (const void*)tokenize_batch_kernel<true, 12, 6, 1>
+                    : cpw == 10 ? (const void*)tokenize_batch_kernel<true, 10, 5, 1>
+                    : cpw == 8 ? (const void*)tokenize_batch_kernel<true, 8, 4, 3>
+                               : (const void*)tokenize_batch_kernel<false, kBW, 1, 3>;
+    const int wpb = cp ? cpw : kBW;  // waves per workgroup
+    LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 64 * wpb, 0));
     // each wave streams >= ~16 sentences so its unit queue stays full across sentences
-    const int64_t want = (n_sent + 16 * kBW - 1) / (16 * kBW);
+    const int64_t want = (n_sent + 16 * wpb - 1) / (16 * wpb);
     int64_t grid = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1)));
     // tests: a smaller grid makes small inputs take the dynamic chunk claims
     if (const char* g = getenv("LDDL_TOKENIZE_GRID")) grid = std::max<int64_t>(1, std::min<int64_t>(grid, atoll(g)));
 #ifdef LDDL_STAMPS
     unsigned long long* tl = nullptr;
     unsigned long long* rg = nullptr;
-    LDDL_HIP(hipMalloc(&tl, 16 * grid * kBW));
-    LDDL_HIP(hipMemsetAsync(tl, 0, 16 * grid * kBW, st));
+    LDDL_HIP(hipMalloc(&tl, 16 * grid * wpb));
+    LDDL_HIP(hipMemsetAsync(tl, 0, 16 * grid * wpb, st));
     LDDL_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tok_tl), &tl, sizeof(tl), 0, hipMemcpyHostToDevice, st));
-    LDDL_HIP(hipMalloc(&rg, 8 * kTokRegions));
-    LDDL_HIP(hipMemsetAsync(rg, 0, 8 * kTokRegions, st));
+    LDDL_HIP(hipMalloc(&rg, 8 * (kTokRegions + 10)));
+    LDDL_HIP(hipMemsetAsync(rg, 0, 8 * (kTokRegions + 10), st));
     LDDL_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tok_reg), &rg, sizeof(rg), 0, hipMemcpyHostToDevice, st));
 #endif
-    // the first grid x kBW chunks are taken statically (chunk w by wave w)
-    const int64_t first = std::min<int64_t>(grid * kBW * kChunk, (int64_t)INT32_MAX);
+    // the first grid x wpb chunks are taken statically (chunk w by wave w)
+    const int64_t first = std::min<int64_t>(grid * wpb * kChunk, (int64_t)INT32_MAX);
     LDDL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(chunk_ctr), (int)first, 1, st));
-    hipLaunchKernelGGL(tokenize_batch_kernel, dim3((unsigned)grid), dim3(64 * kBW), 0, st, c->tab,
-                       d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + kFbHead,
-                       reinterpret_cast<uint32_t*>(fb), chunk_ctr);
+    DevArena::Block scr;
+    if (cp) LDDL_HIP(c->arena.take(sizeof(uint32_t) * (size_t)kScrWords * (size_t)(grid * wpb), st, scr));
+    uint32_t* scrp = cp ? static_cast<uint32_t*>(scr.p) : nullptr;
+#define LDDL_TOK_LAUNCH(KCP, KW, KWPE, KRF)                                                       \
+  hipLaunchKernelGGL((tokenize_batch_kernel<KCP, KW, KWPE, KRF>), dim3((unsigned)grid), dim3(64 * KW), 0, \
+                     st, c->tab, d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len,  \
+                     fb + kFbHead, reinterpret_cast<uint32_t*>(fb), chunk_ctr, scrp)
+    if (cpw == 16) LDDL_TOK_LAUNCH(true, 16, 1, 3);
+    else if (cpw == 12) LDDL_TOK_LAUNCH(true, 12, 6, 1);
+    else if (cpw == 10) LDDL_TOK_LAUNCH(true, 10, 5, 1);
+    else if (cpw == 8) LDDL_TOK_LAUNCH(true, 8, 4, 3);
+    else LDDL_TOK_LAUNCH(false, kBW, 1, 3);
+#undef LDDL_TOK_LAUNCH
 #ifdef LDDL_STAMPS
     {  // wave timeline (100 MHz real-time clock)
-      const int64_t nw = grid * kBW;
+      const int64_t nw = grid * wpb;
       std::vector<unsigned long long> t(2 * nw);
       LDDL_HIP(hipMemcpyAsync(t.data(), tl, 16 * nw, hipMemcpyDeviceToHost, st));
       LDDL_HIP(hipStreamSynchronize(st));
@@ -1272,8 +1735,16 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
       }
       fprintf(stderr, "\n");
       LDDL_HIP(hipFree(tl));
-      unsigned long long r[kTokRegions];
+      unsigned long long r[kTokRegions + 10];
       LDDL_HIP(hipMemcpy(r, rg, sizeof r, hipMemcpyDeviceToHost));
+      const unsigned long long* k = r + kTokRegions;
+      fprintf(stderr,
+              "[tok phaseB] flushes %llu units %llu | passes %llu lanes/pass %.1f | piece-steps: wave %llu "
+              "lane %llu (lane util %.2f) | bloom iters: wave %llu lane-useful %llu (util %.2f, per wave "
+              "step %.1f) | probe trips: wave %llu lane %llu (util %.2f)\n",
+              k[8], k[9], k[0], (double)k[1] / (k[0] ? k[0] : 1), k[2], k[3],
+              (double)k[3] / (64.0 * (k[2] ? k[2] : 1)), k[4], k[5], (double)k[5] / (64.0 * (k[4] ? k[4] : 1)),
+              (double)k[4] / (k[2] ? k[2] : 1), k[6], k[7], (double)k[7] / (64.0 * (k[6] ? k[6] : 1)));
       unsigned long long tot = 0;
       for (int q = 0; q < kTokRegions; ++q) tot += r[q];
       static const char* names[kTokRegions] = {"banks", "phaseA", "phaseB", "place", "qshift", "chunk"};
@@ -1283,6 +1754,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
       LDDL_HIP(hipFree(rg));
     }
 #endif
+    if (cp) c->arena.give(scr, st);
   }
   const int64_t fgrid = std::min<int64_t>((n_sent + kBlock - 1) / kBlock, (int64_t)n_cu * 2);
   hipLaunchKernelGGL(tokenize_lane_kernel, dim3((unsigned)fgrid), dim3(kBlock), 0, st, c->tab,

@@ -630,6 +630,74 @@ class _StageTimer:
             self.t = time.perf_counter()
 
 
+def _run_gpu_workers(args, n_workers, vocab, ctx0, batch_it, outdir, pool, copier, inflight):
+    """The non-balanced batch loop over `n_workers` GPU worker threads (main's --gpu-workers).
+    Worker 0 uses the main Context; the others create their own (a Context holds per-call state:
+    the segmenter's count / fill pair). Returns the number of files written; `inflight` is left
+    empty."""
+    import threading
+    import torch
+    from ...context import Context
+    lock = threading.Lock()
+    errors = []
+    n_files = [0]
+
+    def drain(limit_batches, limit_bytes):
+        # wait for the oldest batches' writes while more than `limit_batches` are in flight or
+        # their pinned bytes exceed `limit_bytes` (the newest batch always proceeds)
+        while True:
+            with lock:
+                if not (len(inflight) > limit_batches or (len(inflight) > 1 and sum(
+                        getattr(j, 'render_bytes', 0) for j, _ in inflight) > limit_bytes)):
+                    return
+                j, fs = inflight.pop(0)
+            if not isinstance(j, list):
+                n = len(j.result())
+                with lock:
+                    n_files[0] += n
+            for f in fs:
+                f.result()
+
+    def worker(k):
+        try:
+            wctx = ctx0
+            if k > 0:
+                wctx = Context(vocab, do_lower_case=True, device=ctx0.device.index)
+                if args.sentence_splitter == 'gpu':
+                    from ... import punkt
+                    punkt.set_params(wctx, getattr(ctx0, '_punkt_params', None))
+            st = torch.cuda.Stream(device=wctx.device)
+            with torch.cuda.device(wctx.device), torch.cuda.stream(st):
+                while not errors:
+                    with lock:
+                        item = next(batch_it, None)
+                    if item is None:
+                        return
+                    batch, corpus = item
+                    _trace('batch_ready', batch[0][0] if batch else -1)
+                    futs = []
+                    job = process_batch(wctx, args, batch, corpus, outdir, None, pool, futs, copier)
+                    with lock:
+                        if isinstance(job, list):
+                            n_files[0] += len(job)
+                        inflight.append((job, futs))
+                    drain(n_workers + 1, args.max_inflight_render_bytes)
+                st.synchronize()
+        except BaseException as e:  # noqa: B902 - re-raised by the caller
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(k,), name='gpu-worker-{}'.format(k))
+               for k in range(n_workers)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    drain(0, 0)
+    return n_files[0]
+
+
 def _warm_parquet_writer(outdir):
     import pyarrow as pa
     import pyarrow.parquet as pq
@@ -715,6 +783,17 @@ def main(args):
     copier = ThreadPoolExecutor(max_workers=1)  # device -> host copies of rendered batches
     inflight = []  # (copy future, write futures) of the batches not yet written
     batch_it = iter(batches)
+    gpu_workers = max(1, int(getattr(args, 'gpu_workers', 1) or 1))
+    if stream is None and gpu_workers > 1:
+        # Several GPU batches in flight: a batch's replay planner is one sequential chain per
+        # partition (~0.1 s for a 1 MiB partition whatever the batch size), so one batch of a few
+        # hundred partitions leaves the GPU mostly idle while it runs. Each worker thread owns a
+        # Context and a stream, takes the next batch from the reader and runs it through the
+        # whole GPU path; batches are independent (files are named by partition), so they may
+        # finish in any order.
+        n_files += _run_gpu_workers(args, gpu_workers, vocab, ctx, batch_it, outdir, pool, copier,
+                                    inflight)
+        batch_it = iter(())
     while True:
         item = next(batch_it, None)
         if stream is not None and world > 1:
@@ -887,6 +966,10 @@ def attach_args(parser=None):
                         help='--num-shards: most shard files kept open at once (default: as many '
                              'as RLIMIT_NOFILE allows, raised to its hard limit); above it, each '
                              'batch is written as a piece and the pieces are merged at the end')
+    parser.add_argument('--gpu-workers', type=int, default=2,
+                        help='lddl_amd: GPU batches processed concurrently, each by a host thread '
+                             'with its own stream (without --num-shards; the balanced path keeps '
+                             'batch order). Default: 2')
     parser.add_argument('--write-threads', type=int, default=min(os.cpu_count() or 1, 16),
                         help='lddl_amd: parquet files written concurrently (threads). Default: '
                              'min(cpus, 16)')

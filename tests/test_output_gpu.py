@@ -119,8 +119,11 @@ def _write_source(root, n_docs=300, seed=11):
             f.write('\n'.join(chunk) + '\n\n')
 
 
-@pytest.mark.parametrize('binned,params', [(False, False), (True, False), (False, True)])
-def test_pretrain_cli_vs_oracle(tmp_path, binned, params):
+@pytest.mark.parametrize('binned,params,workers', [(False, False, 1), (True, False, 2),
+                                                    (False, True, 2), (True, False, 3)])
+def test_pretrain_cli_vs_oracle(tmp_path, binned, params, workers):
+    """CLI output == the oracle's rows per partition. workers = 3: one partition per GPU batch
+    (--gpu-batch-bytes 1) over three concurrent GPU worker threads (--gpu-workers)."""
     from lddl_amd import synth
     from lddl_amd.dask.bert import pretrain as P
     from oracle import oracle as O
@@ -129,7 +132,10 @@ def test_pretrain_cli_vs_oracle(tmp_path, binned, params):
     sink = tmp_path / 'out'
     argv = ['--schedule', 'local', '--wikipedia', str(src), '--sink', str(sink), '--masking',
             '--target-seq-length', '128', '--num-blocks', '4', '--seed', '7',
-            '--vocab-file', VOCAB_UNCASED, '--local-n-workers', '1', '--duplicate-factor', '2']
+            '--vocab-file', VOCAB_UNCASED, '--local-n-workers', '1', '--duplicate-factor', '2',
+            '--gpu-workers', str(workers)]
+    if workers > 2:
+        argv += ['--gpu-batch-bytes', '1', '--shuffle-group-bytes', '1']
     if binned:
         argv += ['--bin-size', '32']
     prm = None
