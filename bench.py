@@ -982,9 +982,14 @@ def main():
                 'unit': 'wave64 VALU instr/s', 'frac': a / valu_peak,
                 'salu_instructions_per_launch': sc, 'salu_achieved': sa, 'salu_peak': salu_peak,
                 'salu_frac': sa / salu_peak,
-                # the model both hot kernels fit: scalar and vector issue barely
-                # overlap, a SALU instruction costs a SIMD 4 cycles and a VALU one 2
-                'issue_model_frac': (4.0 * (sc or 0) + 2.0 * v) / (256 * 4 * 2.4e9 * ms * 1e-3),
+                # additive model (4 cycles per SALU + 2 per VALU instruction): it fits both hot
+                # kernels' times, but it describes their dependency chains, not a pipe bound -
+                # the scalar and vector pipes serve different waves in the same cycles
+                # (profiles/r05a_corun_salu_valu.txt: 86-97 % overlap; the planner keeps its time
+                # beside a VALU filler, profiles/r05b_corun_planner_valu_filler.log). The pipe
+                # bound is max(salu_frac, frac).
+                'additive_chain_model_frac': (4.0 * (sc or 0) + 2.0 * v) / (256 * 4 * 2.4e9 * ms * 1e-3),
+                'pipe_bound_frac': max(a / valu_peak, sa / salu_peak),
                 'source': pmc_src, 'pmc_build_id': pmc_meta.get('build_id'),
                 'pmc_git_head': pmc_meta.get('git_head'), 'same_build': same_build,
                 'note': ('PMC pass of this build (lddl_build_id {})'.format(build_id) if same_build
@@ -997,12 +1002,14 @@ def main():
                  'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': plan_gbs / HBM_PEAK_GBS,
                  'traffic': traffic('plan_replay_kernel') if args.rng == 'replay' else None,
                  'algorithmic_bytes_per_launch': plan_bytes, 'launch_ms': plan_ms,
-                 'note': 'instruction-issue-bound (issue_roofline), not HBM-bound (DESIGN.md 4)'}
+                 'note': 'latency-bound (dependent scalar chains; issue_roofline pipe fractions '
+                         '< 0.6), not HBM-bound (DESIGN.md 4)'}
     tok_roof = {'kernel': 'tokenize_batch_kernel', 'bound': 'hbm', 'achieved': achieved,
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                 'traffic': traffic('tokenize_batch_kernel'), 'algorithmic_bytes_per_launch': tok_bytes,
                 'launch_ms': tok_ms,
-                'note': 'instruction-issue-bound (issue_roofline), not HBM-bound (DESIGN.md 4)'}
+                'note': 'latency-bound at 4 waves/SIMD (~50 % of wave cycles waiting; '
+                        'issue_roofline pipe fractions < 0.6), not HBM-bound (DESIGN.md 4)'}
     stage_roof = {'kernel': 'pair stage (compaction, densify, plan, shuffle, resolve, layout, '
                             'gather)', 'bound': 'hbm', 'achieved': stage_gbs,
                   'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': stage_gbs / HBM_PEAK_GBS,

@@ -880,7 +880,7 @@ enum : uint32_t { kFRun = 0, kFSep = 1, kFIso = 2, kFSlow = 4 };
 struct alignas(16) StreamLds {
   int32_t q_s[kQ];          // unit starts (see kQPos)
   int32_t q_e[kQ];          // unit ends (inclusive, chunk-relative)
-  int32_t trash[64];        // target of the lanes that store nothing (no exec-mask branch)
+  uint8_t q_slot[kQ];       // unit start's sentence slot in the chunk (from the bank loop)
   int32_t q_res[kSF];       // phase A/B result: the single piece id, or kHardBit | column
   uint8_t q_npc[kSF];       // pieces of the unit
   HIdx h_idx[kSF];          // queue positions of the hard units, in order
@@ -973,6 +973,12 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
   __syncthreads();
   const int lane = lane_id();
   WL& W = s_w[threadIdx.x >> 6];
+  // target of the bank loop's lanes that store nothing (no exec-mask branch): the piece columns,
+  // unused outside a flush (kCP: a trash row of its own)
+  int32_t* const trashp = [&]() -> int32_t* {
+    if constexpr (kCP) return &W.trash[lane_id()];
+    else return &W.pcs[lane_id()];
+  }();
   uint32_t* __restrict__ wscr =
       kCP ? scratch + ((int64_t)blockIdx.x * kW + (threadIdx.x >> 6)) * kScrWords : nullptr;
   uint32_t* __restrict__ s_rec = wscr + kScrRec;
@@ -1046,7 +1052,7 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
           const int uc = act ? u : u0;
           const int32_t qs = W.q_s[uc];
           const int npc = act ? W.q_npc[uc] : 0;
-          const int slot = act ? sent_of(qs & kQPos) : -1;
+          const int slot = act ? (int)W.q_slot[uc] : -1;
           const int incl = wave_incl_scan(npc);
           const int excl = incl - npc;
           const int prev_slot = wave_prev(slot);
@@ -1189,13 +1195,14 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         // drop the processed units: < 128 starts and < 128 ends remain (read all, then write)
         const int rs = ns - m, re = ne - m;
         int32_t a0 = 0, a1 = 0, e0 = 0, e1 = 0;
-        if (lane < rs) a0 = W.q_s[m + lane];
-        if (lane + 64 < rs) a1 = W.q_s[m + 64 + lane];
+        uint8_t l0 = 0, l1 = 0;
+        if (lane < rs) a0 = W.q_s[m + lane], l0 = W.q_slot[m + lane];
+        if (lane + 64 < rs) a1 = W.q_s[m + 64 + lane], l1 = W.q_slot[m + 64 + lane];
         if (lane < re) e0 = W.q_e[m + lane];
         if (lane + 64 < re) e1 = W.q_e[m + 64 + lane];
         wave_sync();
-        if (lane < rs) W.q_s[lane] = a0;
-        if (lane + 64 < rs) W.q_s[64 + lane] = a1;
+        if (lane < rs) W.q_s[lane] = a0, W.q_slot[lane] = l0;
+        if (lane + 64 < rs) W.q_s[64 + lane] = a1, W.q_slot[64 + lane] = l1;
         if (lane < re) W.q_e[lane] = e0;
         if (lane + 64 < re) W.q_e[64 + lane] = e1;
         wave_sync();
@@ -1467,12 +1474,12 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         const uint32_t x = x0 + lane;
         const bool in = x < span;
         uint64_t BRK = 0;
-        // kCP: this lane's sentence slot (the last sentence starting at or before byte x, as
-        // sent_of), carried in its unit start so that phase A needs no search
+        // this lane's sentence slot (the last sentence starting at or before byte x, as sent_of),
+        // stored with its unit start so that placement (kCP: phase A) needs no search
         int32_t lslot = jn - 1;
         while (nextS < x0 + 64) {
           BRK |= 1ull << (nextS - x0);
-          if constexpr (kCP) lslot += (x0 + lane >= nextS) ? 1 : 0;
+          lslot += (x0 + lane >= nextS) ? 1 : 0;
           ++jn;
           nextS = jn <= n ? (uint32_t)__builtin_amdgcn_readfirstlane(W.s_off[jn]) : 0xFFFFFFFFu;
         }
@@ -1549,8 +1556,13 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         const uint64_t US = UNIT & ~CONT;
         {
           const uint32_t r = popc_below(US) + (uint32_t)ns;
-          int32_t* dst = ((US >> lane) & 1ull) ? &W.q_s[r] : &W.trash[lane];
+          const bool st_here = (US >> lane) & 1ull;
+          int32_t* dst = st_here ? &W.q_s[r] : trashp;
           *dst = sval;
+          if constexpr (!kCP) {  // the unit's sentence slot (placement needs no search)
+            uint8_t* sd = st_here ? &W.q_slot[r] : reinterpret_cast<uint8_t*>(trashp);
+            *sd = (uint8_t)lslot;
+          }
         }
         if (SL) {  // slow bytes flag their unit (started in this bank or before)
           if ((SL >> lane) & 1ull) atomicOr(&W.q_s[ns + (int)__popcll(US & upto) - 1], kQSlow);
@@ -1560,7 +1572,7 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         const uint64_t UEp = UNITp & ~((CONTp >> 1) | (CONT << 63));
         {
           const uint32_t r = popc_below(UEp) + (uint32_t)ne;
-          int32_t* dst = ((UEp >> lane) & 1ull) ? &W.q_e[r] : &W.trash[lane];
+          int32_t* dst = ((UEp >> lane) & 1ull) ? &W.q_e[r] : trashp;
           *dst = (int32_t)(x - 64u);
         }
         ne += (int)__popcll(UEp);
@@ -1576,7 +1588,7 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
       {  // the last bank's ends (nothing continues past the chunk)
         const uint64_t UEp = UNITp & ~(CONTp >> 1);
         const uint32_t r = popc_below(UEp) + (uint32_t)ne;
-        int32_t* dst = ((UEp >> lane) & 1ull) ? &W.q_e[r] : &W.trash[lane];
+        int32_t* dst = ((UEp >> lane) & 1ull) ? &W.q_e[r] : trashp;
         *dst = (int32_t)(x0 - 64u + lane);
         ne += (int)__popcll(UEp);
       }
@@ -1670,12 +1682,16 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     const int cpw = !path ? 0 : !strcmp(path, "cp") ? 16 : !strcmp(path, "cp12") ? 12
                   : !strcmp(path, "cp10") ? 10 : !strcmp(path, "cp8") ? 8 : 0;
     const bool cp = cpw > 0;
+    // A/B: the round-4 kernel with 8-wave workgroups (88 KB of LDS: room beside it on a CU for
+    // other kernels' workgroups, e.g. the pair planner of the previous chunk)
+    const bool b8 = path && !strcmp(path, "batch8");
     const void* kfn = cpw == 16 ? (const void*)tokenize_batch_kernel<true, 16, 1, 3>
                     : cpw == 12 ? (const void*)tokenize_batch_kernel<true, 12, 6, 1>
                     : cpw == 10 ? (const void*)tokenize_batch_kernel<true, 10, 5, 1>
                     : cpw == 8 ? (const void*)tokenize_batch_kernel<true, 8, 4, 3>
+                    : b8 ? (const void*)tokenize_batch_kernel<false, 8, 1, 3>
                                : (const void*)tokenize_batch_kernel<false, kBW, 1, 3>;
-    const int wpb = cp ? cpw : kBW;  // waves per workgroup
+    const int wpb = cp ? cpw : b8 ? 8 : kBW;  // waves per workgroup
     LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 64 * wpb, 0));
     // each wave streams >= ~16 sentences so its unit queue stays full across sentences
     const int64_t want = (n_sent + 16 * wpb - 1) / (16 * wpb);
@@ -1706,6 +1722,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     else if (cpw == 12) LDDL_TOK_LAUNCH(true, 12, 6, 1);
     else if (cpw == 10) LDDL_TOK_LAUNCH(true, 10, 5, 1);
     else if (cpw == 8) LDDL_TOK_LAUNCH(true, 8, 4, 3);
+    else if (b8) LDDL_TOK_LAUNCH(false, 8, 1, 3);
     else LDDL_TOK_LAUNCH(false, kBW, 1, 3);
 #undef LDDL_TOK_LAUNCH
 #ifdef LDDL_STAMPS
