@@ -630,7 +630,8 @@ class _StageTimer:
             self.t = time.perf_counter()
 
 
-def _run_gpu_workers(args, n_workers, vocab, ctx0, batch_it, outdir, pool, copier, inflight):
+def _run_gpu_workers(args, n_workers, vocab, ctx0, batch_it, outdir, pool, copier, inflight,
+                     timer=None):
     """The non-balanced batch loop over `n_workers` GPU worker threads (main's --gpu-workers).
     Worker 0 uses the main Context; the others create their own (a Context holds per-call state:
     the segmenter's count / fill pair). Returns the number of files written; `inflight` is left
@@ -667,6 +668,8 @@ def _run_gpu_workers(args, n_workers, vocab, ctx0, batch_it, outdir, pool, copie
                     from ... import punkt
                     punkt.set_params(wctx, getattr(ctx0, '_punkt_params', None))
             st = torch.cuda.Stream(device=wctx.device)
+            wt = _StageTimer(args.profile_stages)  # this worker's stages (its own stream)
+            timers.append(wt)
             with torch.cuda.device(wctx.device), torch.cuda.stream(st):
                 while not errors:
                     with lock:
@@ -676,7 +679,8 @@ def _run_gpu_workers(args, n_workers, vocab, ctx0, batch_it, outdir, pool, copie
                     batch, corpus = item
                     _trace('batch_ready', batch[0][0] if batch else -1)
                     futs = []
-                    job = process_batch(wctx, args, batch, corpus, outdir, None, pool, futs, copier)
+                    wt.mark()
+                    job = process_batch(wctx, args, batch, corpus, outdir, wt, pool, futs, copier)
                     with lock:
                         if isinstance(job, list):
                             n_files[0] += len(job)
@@ -686,6 +690,7 @@ def _run_gpu_workers(args, n_workers, vocab, ctx0, batch_it, outdir, pool, copie
         except BaseException as e:  # noqa: B902 - re-raised by the caller
             errors.append(e)
 
+    timers = []
     threads = [threading.Thread(target=worker, args=(k,), name='gpu-worker-{}'.format(k))
                for k in range(n_workers)]
     for t in threads:
@@ -695,7 +700,35 @@ def _run_gpu_workers(args, n_workers, vocab, ctx0, batch_it, outdir, pool, copie
     if errors:
         raise errors[0]
     drain(0, 0)
+    if timer is not None and timer.enabled:  # per-stage seconds summed over the workers
+        for wt in timers:
+            for k, v in wt.acc.items():
+                timer.acc[k] = timer.acc.get(k, 0.0) + v
+        timer.acc['gpu_workers'] = n_workers
     return n_files[0]
+
+
+# rendered parquet bytes per input text byte (seq 128, static masking, duplicate factor 5: 10.5 GB
+# of output per GB of input, profiles/r04e2e_*); the pinned pool is pre-sized from it
+_RENDER_PER_INPUT_BYTE = 11
+
+
+def _prewarm_pinned(args, blocks, rank, world):
+    """Allocate the pinned blocks the first batches' device-to-host copies will take, on a
+    background thread, while the input is read and the first batches run on the GPU (a pinned
+    allocation runs at ~24.5 GB/s; output.PinnedPool)."""
+    if args.output_format != 'parquet':
+        return
+    import threading
+    from ... import output
+    mine = sum(b.nbytes for p, b in enumerate(blocks) if p % world == rank)
+    per = min(args.gpu_batch_bytes, mine) * _RENDER_PER_INPUT_BYTE * args.duplicate_factor // 5
+    n = min(-(-mine // max(1, args.gpu_batch_bytes)), max(1, getattr(args, 'gpu_workers', 1)) + 1)
+    n = min(n, max(1, args.max_inflight_render_bytes // max(1, per)))
+    if per < (64 << 20) or n < 1:
+        return  # small inputs: allocate on demand
+    threading.Thread(target=output.PINNED.prewarm, args=([per] * n,), daemon=True,
+                     name='pinned-prewarm').start()
 
 
 def _warm_parquet_writer(outdir):
@@ -760,6 +793,7 @@ def main(args):
                 dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     from ...context import Context
     ctx = Context(vocab, do_lower_case=True)  # BertTokenizerFast default, SURVEY H5
+    _prewarm_pinned(args, blocks, rank, world)
     if args.sentence_splitter == 'gpu':
         from ... import punkt
         punkt.set_params(ctx, punkt_params(args))
@@ -792,7 +826,8 @@ def main(args):
         # whole GPU path; batches are independent (files are named by partition), so they may
         # finish in any order.
         n_files += _run_gpu_workers(args, gpu_workers, vocab, ctx, batch_it, outdir, pool, copier,
-                                    inflight)
+                                    inflight, timer)
+        timer.mark()
         batch_it = iter(())
     while True:
         item = next(batch_it, None)
@@ -866,8 +901,10 @@ def main(args):
     if rank == 0:
         print('Running the dask pipeline took {} s'.format(time.perf_counter() - tic))
         if args.profile_stages:
-            print('stage seconds (rank 0): ' + json.dumps(
-                {k: round(v, 3) for k, v in timer.acc.items()}))
+            print('stage seconds (rank 0{}): '.format(
+                ', summed over {} GPU workers'.format(timer.acc['gpu_workers'])
+                if 'gpu_workers' in timer.acc else '') + json.dumps(
+                {k: round(v, 3) for k, v in timer.acc.items() if k != 'gpu_workers'}))
             hs = torch.cuda.host_memory_stats()  # torch's pinned host allocator
             print('pinned host memory peak (rank 0): {:.2f} GB'.format(max(
                 [v for k, v in hs.items() if 'bytes' in k and k.endswith('peak')] or [0]) / 1e9))

@@ -10,6 +10,9 @@ work at its own rate, the additive model describes the planner's dependency chai
 bound, and a VALU-heavy stage (the tokenizer) could run beside it.
 
     python tools/corun_planner.py [batch_bytes=2e9]
+
+A SALU-only filler is run the same way: if the planner slowed beside it, the CU's scalar unit
+(shared by the waves of its four SIMDs) would be what the planner waits on.
 """
 import ctypes
 import json
@@ -51,12 +54,12 @@ def main():
                         short_seq_prob=0.1, masked_lm_ratio=0.15)
         return pb.plan_ms
 
-    def filler(iters):
+    def filler(iters, kind):
+        fn = lib.ubench_valu_filler if kind == 'valu' else lib.ubench_salu_filler
         with torch.cuda.stream(fs):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(fs)
-            assert lib.ubench_valu_filler(ctypes.c_void_p(fs.cuda_stream), n_cu, iters,
-                                          ctypes.c_void_p(sink.data_ptr())) == 0
+            assert fn(ctypes.c_void_p(fs.cuda_stream), n_cu, iters, ctypes.c_void_p(sink.data_ptr())) == 0
             e1.record(fs)
         return e0, e1
 
@@ -64,28 +67,31 @@ def main():
         pairs()
     torch.cuda.synchronize()
     plan_alone = float(np.mean([pairs() for _ in range(3)]))
-    # calibrate the filler to about the planner's time alone
-    e0, e1 = filler(2000)
-    torch.cuda.synchronize()
-    per_iter = e0.elapsed_time(e1) / 2000
-    iters = max(1, int(plan_alone / per_iter))
-    e0, e1 = filler(iters)
-    torch.cuda.synchronize()
-    fill_alone = e0.elapsed_time(e1)
-    # together: the filler first (one wave per SIMD on every CU), then the pair stage
-    res = []
-    for _ in range(3):
+    out = {'batch_bytes': nbytes, 'planner_ms_alone': plan_alone}
+    for kind in ('valu', 'salu'):
+        # calibrate the filler to about the planner's time alone
+        e0, e1 = filler(2000, kind)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        e0, e1 = filler(iters)
-        p = pairs()
+        per_iter = e0.elapsed_time(e1) / 2000
+        iters = max(1, int(plan_alone / per_iter))
+        e0, e1 = filler(iters, kind)
         torch.cuda.synchronize()
-        res.append((p, e0.elapsed_time(e1), (time.perf_counter() - t0) * 1e3))
-    p_t, f_t, wall = (float(np.mean(x)) for x in zip(*res))
-    out = {'batch_bytes': nbytes, 'planner_ms_alone': plan_alone, 'filler_ms_alone': fill_alone,
-           'filler_iters': iters, 'filler_waves_per_simd': 1,
-           'together': {'planner_ms': p_t, 'filler_ms': f_t, 'wall_ms_incl_pair_stage': wall},
-           'planner_slowdown': p_t / plan_alone, 'filler_slowdown': f_t / fill_alone}
+        fill_alone = e0.elapsed_time(e1)
+        # together: the filler first (one wave per SIMD on every CU), then the pair stage
+        res = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            e0, e1 = filler(iters, kind)
+            p = pairs()
+            torch.cuda.synchronize()
+            res.append((p, e0.elapsed_time(e1), (time.perf_counter() - t0) * 1e3))
+        p_t, f_t, wall = (float(np.mean(x)) for x in zip(*res))
+        out[kind] = {'filler_ms_alone': fill_alone, 'filler_iters': iters,
+                     'filler_waves_per_simd': 1,
+                     'together': {'planner_ms': p_t, 'filler_ms': f_t,
+                                  'wall_ms_incl_pair_stage': wall},
+                     'planner_slowdown': p_t / plan_alone, 'filler_slowdown': f_t / fill_alone}
     print(json.dumps(out), flush=True)
 
 
