@@ -321,36 +321,43 @@ __device__ inline int32_t probe_finish(const Tables& T, const B32& a, int len, P
 
 // Bloom candidates for the pieces starting at a's first byte: bit L-1 set iff the filter may
 // contain (cont, bytes[0, L)), L = 1 .. maxl (<= 32).
+#ifndef LDDL_BLOOM_GROUP
+#define LDDL_BLOOM_GROUP 4
+#endif
+constexpr int kBloomGroup = LDDL_BLOOM_GROUP;
 __device__ inline uint32_t bloom_candidates32(const uint32_t* bloom, const B32& a, int maxl,
                                               uint32_t cont, TokStats* ts = nullptr) {
   uint32_t h = 0, cand = 0;
+  // lengths in groups of kBloomGroup: a group's filter words are all read before any is used,
+  // so the wave waits on one LDS round trip per group, not per length (round 4 waited on each
+  // length's read before computing the next: a dependent LDS latency per length)
 #pragma unroll
-  for (int L = 1; L <= 32; ++L) {
+  for (int L0 = 1; L0 <= 32; L0 += kBloomGroup) {
     // wave-uniform exit (lanes past their own maxl compute don't-care bits, masked below): no
     // exec-mask bookkeeping per length
-    if (!ballot(L <= maxl)) break;
-    if (ts) {
-      ts->wave(4);
-      ts->add(5, L <= maxl);
+    if (!ballot(L0 <= maxl)) break;
+    uint32_t wrd[kBloomGroup], msk[kBloomGroup];
+#pragma unroll
+    for (int q = 0; q < kBloomGroup; ++q) {
+      const int L = L0 + q;
+      if (ts) {
+        ts->wave(4);
+        ts->add(5, L <= maxl);
+      }
+      const uint64_t wv = L <= 8 ? a.w0 : L <= 16 ? a.w1 : L <= 24 ? a.w2 : a.w3;
+      const uint32_t byte = (uint32_t)(wv >> (8 * ((L - 1) & 7))) & 0xFFu;
+      h = h * kBloomP + byte + 1u;
+      const uint32_t x = bloom_mix(h, (uint32_t)L, cont);
+      msk[q] = bloom_bits(x);
+      wrd[q] = bloom[bloom_word(x)];
     }
-    const uint64_t wv = L <= 8 ? a.w0 : L <= 16 ? a.w1 : L <= 24 ? a.w2 : a.w3;
-    const uint32_t byte = (uint32_t)(wv >> (8 * ((L - 1) & 7))) & 0xFFu;
-    h = h * kBloomP + byte + 1u;
-    const uint32_t x = bloom_mix(h, (uint32_t)L, cont);
-    const uint32_t m = bloom_bits(x);
-    cand |= (bloom[bloom_word(x)] & m) == m ? 1u << (L - 1) : 0u;
+#pragma unroll
+    for (int q = 0; q < kBloomGroup; ++q)
+      cand |= (wrd[q] & msk[q]) == msk[q] ? 1u << (L0 + q - 1) : 0u;
   }
   return maxl >= 32 ? cand : cand & ((1u << maxl) - 1u);
 }
 
-// Greedy longest-match WordPiece (HF WordPiece::tokenize) of a normalised word of nb <= 32 bytes
-// held in registers. ends: bit e set iff a piece may end at byte e (a UTF-8 character boundary;
-// all bits for ASCII). Returns the piece count written to pc, or -1 if more than kPcs pieces.
-// Per piece, the Bloom filter (LDS) gives the lengths that may be pieces (every vocab piece is in
-// it: the longest candidate that hits is the greedy match), and the two longest candidates' home
-// slots are loaded together: a lane waits on ONE table round trip per piece in the common case.
-// (Round 3 probed the full length alone first, then two candidates per round trip: 21.9 ms per
-// 2 GiB against 20.7 now; three candidates per trip spilled VGPRs and took 22.1 ms, r04o.)
 // One greedy longest-match step of a word held in registers: the longest vocab piece (continuation
 // iff start > 0) starting at byte `start`; returns its id and length, or -1 (no piece matches:
 // the word is [UNK]). Per step, the Bloom filter (LDS) gives the lengths that may be pieces (every
@@ -1457,18 +1464,33 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
       int32_t jn = 1;  // the next sentence start to mark
       uint32_t nextS = (uint32_t)__builtin_amdgcn_readfirstlane(W.s_off[1]);
       const uint32_t last = span ? span - 1 : 0;
-      // software prefetch two banks ahead (clamped into the chunk; bytes past it are unused)
-      uint32_t pf1 = 0x20u, pf2 = 0x20u;
+      // software prefetch three banks ahead (clamped into the chunk; bytes past it are unused),
+      // and the fast-path class of the next bank's byte looked up one bank ahead, so neither the
+      // text load nor the LDS class read is waited for in the bank that uses it (round 4 waited
+      // for the class read right after issuing it, every bank)
+      uint32_t cur = 0x20u, pf1 = 0x20u, pf2 = 0x20u;
       if (span) {
-        pf1 = ctext[(uint32_t)lane < last ? (uint32_t)lane : last];
-        pf2 = ctext[64u + lane < last ? 64u + lane : last];
+        cur = ctext[(uint32_t)lane < last ? (uint32_t)lane : last];
+        pf1 = ctext[64u + lane < last ? 64u + lane : last];
+        pf2 = ctext[128u + lane < last ? 128u + lane : last];
       }
+#ifndef LDDL_TOK_CLS_AHEAD
+#define LDDL_TOK_CLS_AHEAD 1
+#endif
+      uint32_t vcur = s_cls[cur];
       uint32_t x0 = 0;
       for (; x0 < span; x0 += 64) {
-        const uint32_t byte = pf1;
+        const uint32_t byte = cur;
+#if LDDL_TOK_CLS_AHEAD
+        const uint32_t v = vcur;
+        vcur = s_cls[pf1];  // the next bank's (its byte was loaded two banks ago)
+#else
+        const uint32_t v = s_cls[byte];
+#endif
+        cur = pf1;
         pf1 = pf2;
         {
-          const uint32_t xq = x0 + 128u + lane;
+          const uint32_t xq = x0 + 192u + lane;
           pf2 = ctext[xq < last ? xq : last];
         }
         const uint32_t x = x0 + lane;
@@ -1483,7 +1505,6 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
           ++jn;
           nextS = jn <= n ? (uint32_t)__builtin_amdgcn_readfirstlane(W.s_off[jn]) : 0xFFFFFFFFu;
         }
-        const uint32_t v = s_cls[byte];
         const uint64_t VALID = ballot(in);
         uint64_t RUN, UNIT, CONT, SL = 0;
         // unit start: chunk-relative byte | kind << 28 (| slot << 16 in kCP: x < kSpanCap)
