@@ -1675,38 +1675,18 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   // steps [8h, 8h+8): swap, or (i < num) finalise slot i; w = the two (1-byte draws) or four
   // (2-byte draws) dwords holding their draws
   auto group = [&](int h, const uint32_t* w) {
-    // All 8 steps' reads are issued first - x[i] of each step and, for the steps that finalise a
-    // slot (i < num), x[j] - and the group's own writes are forwarded into them in registers, so
-    // the lane waits on one LDS round trip per group instead of one or two per step (round 4:
-    // a dependent read -> write per step). The writes still go to LDS in step order for the
-    // groups below. (j <= i, so a step's x[j] read can only be changed by a write of this group
-    // at the same j, and its x[i] read by a write at j == i.)
-    int jj[8];
-    uint32_t xs[8], ys[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = 8 * h + u;
-      jj[u] = sizeof(D) == 1 ? (int)((w[u >> 2] >> (8 * (u & 3))) & 0xFFu)
-                             : (int)((w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
-      xs[u] = i < nc ? x.get(i) : 0u;
-      ys[u] = (i < nc && i < num && i >= 1) ? x.get(jj[u]) : 0u;
-    }
 #pragma unroll
     for (int u = 7; u >= 0; --u) {
       const int i = 8 * h + u;
       if (i >= nc) continue;
-      const int j = jj[u];
-      const uint32_t xi = xs[u];
-      if (i >= 1) {
-        x.set(j, xi);
-#pragma unroll
-        for (int v = 0; v < u; ++v) {  // forward the write to the group's pending reads
-          if (8 * h + v == j) xs[v] = xi;
-          if (jj[v] == j) ys[v] = xi;
-        }
-      }
-      if (i < num) {
-        const int y = i >= 1 ? (int)ys[u] : (int)xi;  // slot 0 keeps x[0]
+      const int j = sizeof(D) == 1 ? (int)((w[u >> 2] >> (8 * (u & 3))) & 0xFFu)
+                                   : (int)((w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
+      const uint32_t xi = x.get(i);
+      if (i >= num) {
+        if (i >= 1) x.set(j, xi);
+      } else {
+        const int y = i >= 1 ? (int)x.get(j) : (int)xi;  // slot 0 keeps x[0]
+        if (i >= 1) x.set(j, xi);
         const uint32_t pos = (uint32_t)(fast ? (y < na ? y + 1 : y + 2) : y);
         // 128-bit shift register, newest at slot offset 0 (slots arrive in descending order)
         acc = make_uint4((acc.x << 16) | pos, (acc.y << 16) | (acc.x >> 16),

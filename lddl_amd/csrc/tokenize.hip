@@ -320,9 +320,12 @@ __device__ inline int32_t probe_finish(const Tables& T, const B32& a, int len, P
 }
 
 // Bloom candidates for the pieces starting at a's first byte: bit L-1 set iff the filter may
-// contain (cont, bytes[0, L)), L = 1 .. maxl (<= 32).
+// contain (cont, bytes[0, L)), L = 1 .. maxl (<= 32). LDDL_BLOOM_GROUP > 1 reads the filter words
+// of that many lengths before testing any (A/B: 2 -> 19.31 ms per 2 GB, 4 -> 21.1 and 8 -> 22.9
+// against 19.32 with 1; profiles/r05i_tok_variants.txt): the grouped reads cost registers and
+// the kernel spills, and the round trip they hide is not what it waits on.
 #ifndef LDDL_BLOOM_GROUP
-#define LDDL_BLOOM_GROUP 4
+#define LDDL_BLOOM_GROUP 1
 #endif
 constexpr int kBloomGroup = LDDL_BLOOM_GROUP;
 __device__ inline uint32_t bloom_candidates32(const uint32_t* bloom, const B32& a, int maxl,
@@ -1464,18 +1467,17 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
       int32_t jn = 1;  // the next sentence start to mark
       uint32_t nextS = (uint32_t)__builtin_amdgcn_readfirstlane(W.s_off[1]);
       const uint32_t last = span ? span - 1 : 0;
-      // software prefetch three banks ahead (clamped into the chunk; bytes past it are unused),
-      // and the fast-path class of the next bank's byte looked up one bank ahead, so neither the
-      // text load nor the LDS class read is waited for in the bank that uses it (round 4 waited
-      // for the class read right after issuing it, every bank)
+      // software prefetch three banks ahead (clamped into the chunk; bytes past it are unused);
+      // with LDDL_TOK_CLS_AHEAD the fast-path class of the next bank's byte is also looked up one
+      // bank ahead (measured neutral: the class read's wait is not on the critical path)
       uint32_t cur = 0x20u, pf1 = 0x20u, pf2 = 0x20u;
       if (span) {
         cur = ctext[(uint32_t)lane < last ? (uint32_t)lane : last];
         pf1 = ctext[64u + lane < last ? 64u + lane : last];
         pf2 = ctext[128u + lane < last ? 128u + lane : last];
       }
-#ifndef LDDL_TOK_CLS_AHEAD
-#define LDDL_TOK_CLS_AHEAD 1
+#ifndef LDDL_TOK_CLS_AHEAD  // 1: the class read a bank ahead (A/B: 19.31 vs 19.32 ms, r05i)
+#define LDDL_TOK_CLS_AHEAD 0
 #endif
       uint32_t vcur = s_cls[cur];
       uint32_t x0 = 0;

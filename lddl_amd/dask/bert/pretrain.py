@@ -716,8 +716,11 @@ _RENDER_PER_INPUT_BYTE = 11
 def _prewarm_pinned(args, blocks, rank, world):
     """Allocate the pinned blocks the first batches' device-to-host copies will take, on a
     background thread, while the input is read and the first batches run on the GPU (a pinned
-    allocation runs at ~24.5 GB/s; output.PinnedPool)."""
-    if args.output_format != 'parquet':
+    allocation runs at ~24.5 GB/s; output.PinnedPool). Opt-in (LDDL_PINNED_PREWARM=1): beside
+    the native reader it slowed the 1 GB read from 0.10 to 1.15 s (page pinning and the reader's
+    page faults contend), profiles/r05h_e2e_w1.log; by default blocks are pinned on demand and
+    reused."""
+    if args.output_format != 'parquet' or os.environ.get('LDDL_PINNED_PREWARM') != '1':
         return
     import threading
     from ... import output
