@@ -803,16 +803,27 @@ __global__ void __launch_bounds__(64, 6) plan_replay_kernel(PlanArgs A) {
           const bool fits = pool_fits && jpool_fits;
           if (!fits) *A.overflow = 1;  // (uniform; every lane stores the same flag)
           // random.shuffle(cand_indexes): draws j_i (i = nc-1 .. 1) to the pool
+          // The region's other entries, 0 and [nc, nc rounded up to 16), get j_i = i: fy_resolve's
+          // steps there move an entry onto itself, so its step loop needs no per-step guard.
+          const int32_t ip = nc + lane;
           if constexpr (kJB == 1) {
             uint8_t* jd = static_cast<uint8_t*>(A.jpool) + jb;
             rng.fy_draws(nc, [&](int32_t i, uint32_t j) {
               if (fits) jd[i] = (uint8_t)j;  // (fits is uniform: a scalar branch)
             });
+            if (fits && nc > 0) {
+              if (ip < ((nc + 15) & ~15)) jd[ip] = (uint8_t)ip;
+              if (lane == 63) jd[0] = 0;
+            }
           } else {
             uint16_t* jd = static_cast<uint16_t*>(A.jpool) + jb;
             rng.fy_draws(nc, [&](int32_t i, uint32_t j) {
               if (fits) jd[i] = (uint16_t)j;
             });
+            if (fits && nc > 0) {
+              if (ip < ((nc + 15) & ~15)) jd[ip] = (uint16_t)ip;
+              if (lane == 63) jd[0] = 0;
+            }
           }
           STAMP_ADD(2, st_t);
           // decisions of the masked candidates in shuffled order (pretrain.py:208-221)
@@ -1646,7 +1657,7 @@ struct LaneCol<uint8_t, LW> {
 // LW: pairs (lanes) per workgroup of one wave. Long pairs run with LW < 64: a lane's column is
 // seq entries, so at seq 512 a full wave holds 64 KB of LDS and only two fit a CU; fewer lanes
 // per wave put more waves (more independent step chains) on each SIMD.
-template <typename T, typename D, int NG, int LW = 64>
+template <typename T, typename D, int NG, int LW = 64, bool kBF = false, int kRA = 0>
 __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_xb[];
   constexpr int kPerVec = 16 / (int)sizeof(D);  // draws per uint4
@@ -1695,10 +1706,68 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
     }
     if (8 * h < num) mp[h] = acc;  // slots [8h, 8h+8) complete (the top group zero-padded)
   };
+  // kBF: the same steps without exec-mask branches. The planner pads a pair's draw region
+  // (entry 0 and [nc, nc rounded up to 16) hold j_i = i), so every step of a loaded vector
+  // is x[j] = x[i] unguarded (a padding step rewrites x[i] onto itself); a group in which no
+  // lane of the wave finalises a slot is that move alone (read, wait, write: ~2 VALU per
+  // step); otherwise each step also reads y = x[j] before the write (i = 0: j = 0, y = x[0])
+  // and keeps its position by select. Round 4's guarded steps spent ~10 scalar exec-mask
+  // instructions and three branches per step.
+  const int32_t padd = fast ? 1 : 0, thr = fast ? na : INT32_MAX;  // pos = y + padd + (y >= thr)
+  auto group_bf = [&](int h, const uint32_t* w) {
+    if (__any(8 * h < num)) {
+      uint32_t pos[8];
+#pragma unroll
+      for (int u = 7; u >= 0; --u) {
+        const int i = 8 * h + u;
+        const int j = sizeof(D) == 1 ? (int)((w[u >> 2] >> (8 * (u & 3))) & 0xFFu)
+                                     : (int)((w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
+        const uint32_t xi = x.get(i);
+        const int y = (int)x.get(j);
+        x.set(j, xi);
+        pos[u] = i < num ? (uint32_t)(y + padd + (y >= thr ? 1 : 0)) : 0u;
+      }
+      if (8 * h < num)
+        mp[h] = make_uint4(pos[0] | pos[1] << 16, pos[2] | pos[3] << 16, pos[4] | pos[5] << 16,
+                           pos[6] | pos[7] << 16);
+    } else if (kRA == 0) {
+#pragma unroll
+      for (int u = 7; u >= 0; --u) {
+        const int j = sizeof(D) == 1 ? (int)((w[u >> 2] >> (8 * (u & 3))) & 0xFFu)
+                                     : (int)((w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
+        x.set(j, x.get(8 * h + u));
+      }
+    } else {
+      // kRA reads ahead: x[i - kRA] is read before step i's write (the group's top kRA entries
+      // at its start), so step u's read misses the writes of steps u + 1 .. min(u + kRA, 7),
+      // which are forwarded from registers (the most recent wins)
+      int jr[8];  // j - 8h: compared with the step offset u
+      uint32_t r[8], v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        jr[u] = (sizeof(D) == 1 ? (int)((w[u >> 2] >> (8 * (u & 3))) & 0xFFu)
+                                : (int)((w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu)) - 8 * h;
+#pragma unroll
+      for (int u = 7; u >= 8 - kRA; --u) r[u] = x.get(8 * h + u);
+#pragma unroll
+      for (int u = 7; u >= 0; --u) {
+        if (u - kRA >= 0) r[u - kRA] = x.get(8 * h + u - kRA);
+        uint32_t val = r[u];
+#pragma unroll
+        for (int t = kRA; t >= 1; --t)  // oldest first
+          if (u + t <= 7) val = jr[u + t] == u ? v[u + t] : val;
+        v[u] = val;
+        x.set(jr[u] + 8 * h, val);
+      }
+    }
+  };
   // one uint4 of draws = kPerVec / 8 groups of 8 steps, processed top down
   auto vec = [&](int g, const uint4& v) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    if (sizeof(D) == 1) {
+    if (kBF) {
+      if (sizeof(D) == 1) group_bf(2 * g + 1, w + 2);
+      group_bf(sizeof(D) == 1 ? 2 * g : g, w);
+    } else if (sizeof(D) == 1) {
       if (16 * g + 8 < nc) group(2 * g + 1, w + 2);
       group(2 * g, w);
     } else {
@@ -2630,20 +2699,39 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
       ResolveArgs RA{M.slots, P->n_pairs, P->desc, spool, jpool, P->mpos, P->kscan, P->dense, cls,
                      sep, M.dstq, P->rec, pcnt};
       const dim3 grid((unsigned)((P->n_pairs + 63) / 64));
-      if (prm->seq <= 131)  // nc <= 128: all draws in registers (8 uint4 of 1-byte draws); 64
+      // a lane's column covers the padded draw region (steps up to nc rounded up to 16)
+      const size_t col = (size_t)((prm->seq + 15) & ~15);
+      // Branch-free steps for long pairs (C3, seq 512: 77.6 -> 46.8 ms), the guarded ones at
+      // seq <= 131 (64 pairs per wave: 10.1 ms against 11.5 branch-free; profiles/r05k_*).
+      // A/B: LDDL_FY_MODE=0 / 1 forces one kind everywhere; LDDL_FY_LW=32: 32 pairs per wave at
+      // seq > 256 (50.7 ms)
+      const int fy_mode = getenv("LDDL_FY_MODE") ? atoi(getenv("LDDL_FY_MODE")) : -1;
+      const int fy_lw = getenv("LDDL_FY_LW") ? atoi(getenv("LDDL_FY_LW")) : 16;
+      const int fy_ra = getenv("LDDL_FY_RA") ? atoi(getenv("LDDL_FY_RA")) : 0;
+#define LDDL_FY_LAUNCH(T, NG, LW, BF, ...)                                                     \
+  hipLaunchKernelGGL((fy_resolve_kernel<T, T, NG, LW, BF, ##__VA_ARGS__>),                     \
+                     dim3((unsigned)((P->n_pairs + LW - 1) / LW)), dim3(LW),                   \
+                     (size_t)LW * sizeof(T) * col, st, RA)
+      if (prm->seq <= 131) {  // nc <= 128: all draws in registers (8 uint4 of 1-byte draws); 64
         // pairs per wave (C2: 10.2 ms; 32 per wave 11.9, 16 per wave 20.1, profiles/r04slw_*)
-        hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 8>), grid, dim3(64),
-                           (size_t)64 * (size_t)((prm->seq + 3) & ~3), st, RA);
+        if (fy_mode == 1) LDDL_FY_LAUNCH(uint8_t, 8, 64, true);
+        else LDDL_FY_LAUNCH(uint8_t, 8, 64, false);
       // long pairs: 16 lanes (pairs) per wave (C3, seq 512: 106 ms with 64, 109 with 32, 93 with
       // 16; profiles/r04fy_*)
-      else if (prm->seq <= 256)  // candidate indices, positions and draws fit a byte
-        hipLaunchKernelGGL((fy_resolve_kernel<uint8_t, uint8_t, 0, 16>),
-                           dim3((unsigned)((P->n_pairs + 15) / 16)), dim3(16),
-                           (size_t)16 * (size_t)((prm->seq + 3) & ~3), st, RA);
-      else
-        hipLaunchKernelGGL((fy_resolve_kernel<uint16_t, uint16_t, 0, 16>),
-                           dim3((unsigned)((P->n_pairs + 15) / 16)), dim3(16),
-                           (size_t)2 * 16 * (size_t)prm->seq, st, RA);
+      } else if (prm->seq <= 256) {  // candidate indices, positions and draws fit a byte
+        if (fy_mode) LDDL_FY_LAUNCH(uint8_t, 0, 16, true);
+        else LDDL_FY_LAUNCH(uint8_t, 0, 16, false);
+      } else if (fy_lw == 32) {
+        if (fy_mode) LDDL_FY_LAUNCH(uint16_t, 0, 32, true);
+        else LDDL_FY_LAUNCH(uint16_t, 0, 32, false);
+      } else {
+        if (!fy_mode) LDDL_FY_LAUNCH(uint16_t, 0, 16, false);
+        else if (fy_ra == 1) LDDL_FY_LAUNCH(uint16_t, 0, 16, true, 1);
+        else if (fy_ra == 2) LDDL_FY_LAUNCH(uint16_t, 0, 16, true, 2);
+        else if (fy_ra == 3) LDDL_FY_LAUNCH(uint16_t, 0, 16, true, 3);
+        else LDDL_FY_LAUNCH(uint16_t, 0, 16, true);
+      }
+#undef LDDL_FY_LAUNCH
     }
     LDDL_HIP(hipGetLastError());
     TRY(scan_only(st));

@@ -708,32 +708,6 @@ def _run_gpu_workers(args, n_workers, vocab, ctx0, batch_it, outdir, pool, copie
     return n_files[0]
 
 
-# rendered parquet bytes per input text byte (seq 128, static masking, duplicate factor 5: 10.5 GB
-# of output per GB of input, profiles/r04e2e_*); the pinned pool is pre-sized from it
-_RENDER_PER_INPUT_BYTE = 11
-
-
-def _prewarm_pinned(args, blocks, rank, world):
-    """Allocate the pinned blocks the first batches' device-to-host copies will take, on a
-    background thread, while the input is read and the first batches run on the GPU (a pinned
-    allocation runs at ~24.5 GB/s; output.PinnedPool). Opt-in (LDDL_PINNED_PREWARM=1): beside
-    the native reader it slowed the 1 GB read from 0.10 to 1.15 s (page pinning and the reader's
-    page faults contend), profiles/r05h_e2e_w1.log; by default blocks are pinned on demand and
-    reused."""
-    if args.output_format != 'parquet' or os.environ.get('LDDL_PINNED_PREWARM') != '1':
-        return
-    import threading
-    from ... import output
-    mine = sum(b.nbytes for p, b in enumerate(blocks) if p % world == rank)
-    per = min(args.gpu_batch_bytes, mine) * _RENDER_PER_INPUT_BYTE * args.duplicate_factor // 5
-    n = min(-(-mine // max(1, args.gpu_batch_bytes)), max(1, getattr(args, 'gpu_workers', 1)) + 1)
-    n = min(n, max(1, args.max_inflight_render_bytes // max(1, per)))
-    if per < (64 << 20) or n < 1:
-        return  # small inputs: allocate on demand
-    threading.Thread(target=output.PINNED.prewarm, args=([per] * n,), daemon=True,
-                     name='pinned-prewarm').start()
-
-
 def _warm_parquet_writer(outdir):
     import pyarrow as pa
     import pyarrow.parquet as pq
@@ -796,7 +770,6 @@ def main(args):
                 dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     from ...context import Context
     ctx = Context(vocab, do_lower_case=True)  # BertTokenizerFast default, SURVEY H5
-    _prewarm_pinned(args, blocks, rank, world)
     if args.sentence_splitter == 'gpu':
         from ... import punkt
         punkt.set_params(ctx, punkt_params(args))
@@ -1006,10 +979,10 @@ def attach_args(parser=None):
                         help='--num-shards: most shard files kept open at once (default: as many '
                              'as RLIMIT_NOFILE allows, raised to its hard limit); above it, each '
                              'batch is written as a piece and the pieces are merged at the end')
-    parser.add_argument('--gpu-workers', type=int, default=2,
+    parser.add_argument('--gpu-workers', type=int, default=1,
                         help='lddl_amd: GPU batches processed concurrently, each by a host thread '
                              'with its own stream (without --num-shards; the balanced path keeps '
-                             'batch order). Default: 2')
+                             'batch order). Default: 1')
     parser.add_argument('--write-threads', type=int, default=min(os.cpu_count() or 1, 16),
                         help='lddl_amd: parquet files written concurrently (threads). Default: '
                              'min(cpus, 16)')

@@ -109,57 +109,6 @@ def render(ctx, pb, rows=None, bin_id=None):
     return render_device(ctx, pb, rows, bin_id).to_host()
 
 
-class PinnedPool:
-    """Reusable pinned host blocks for the rendered batches' device-to-host copies.
-
-    Measured on the box (tools/d2h_probe.py, profiles/r05g_d2h.log): a fresh pinned allocation
-    runs at ~24.5 GB/s and torch's host allocator handed back no cached block for a same-size
-    request, while the copy into pinned memory runs at ~57 GB/s; a 512 MiB input batch renders
-    ~5.5 GB, so allocating per batch cost the CLI ~0.2 s per batch. A block taken here returns to
-    the pool when the last numpy view of it is gone (the rendered batch is written and dropped),
-    so no view can outlive its block's reuse. `prewarm` allocates blocks ahead (the CLI does it
-    on a background thread while the input is read and the first batch runs)."""
-
-    GRANULE = 64 << 20
-
-    def __init__(self):
-        import threading
-        self._free = []
-        self._lock = threading.Lock()
-        self.allocations = 0
-
-    def _alloc(self, n):
-        self.allocations += 1
-        return torch.empty(-(-n // self.GRANULE) * self.GRANULE, dtype=torch.uint8, pin_memory=True)
-
-    def _give(self, t):
-        with self._lock:
-            self._free.append(t)
-
-    def prewarm(self, sizes):
-        for n in sizes:
-            self._give(self._alloc(int(n)))
-
-    def take(self, n):
-        """(pinned uint8 tensor of >= n bytes, ctypes buffer over it): numpy views are made from
-        the buffer; the tensor goes back to the pool when the buffer and every view are gone."""
-        import weakref
-        n = max(int(n), 1)
-        with self._lock:
-            fit = [t for t in self._free if n <= t.numel() <= 4 * n + self.GRANULE]
-            t = min(fit, key=lambda x: x.numel()) if fit else None
-            if t is not None:
-                self._free.remove(t)
-        if t is None:
-            t = self._alloc(n)
-        buf = (ctypes.c_uint8 * t.numel()).from_address(t.data_ptr())
-        weakref.finalize(buf, self._give, t)
-        return t, buf
-
-
-PINNED = PinnedPool()
-
-
 @dataclass
 class DeviceRendered:
     """render()'s columns still in HBM (device tensors), with the stream event after which they
@@ -179,36 +128,22 @@ class DeviceRendered:
         st = stream if stream is not None else torch.cuda.current_stream()
         if self.event is not None:
             st.wait_event(self.event)
-        n = {}
-        cols = [(k, t) for k, t in self.cols.items() if t is not None]
-        if _PAGEABLE:  # (A/B diagnostics) pageable host buffers, one per column
-            with torch.cuda.stream(st):
-                for k, t in cols:
+        out = {}
+        with torch.cuda.stream(st):
+            for k, t in self.cols.items():
+                if t is None:
+                    out[k] = None
+                    continue
+                if _PAGEABLE:  # (A/B diagnostics) pageable host buffers
                     h = torch.empty(max(t.numel(), 1), dtype=t.dtype)[:t.numel()]
                     h.copy_(t)
-                    t.record_stream(st)
-                    n[k] = h.numpy()
-            st.synchronize()
-        else:  # all columns into one pooled pinned block, 256-byte aligned
-            offs, tot = [], 0
-            for _, t in cols:
-                offs.append(tot)
-                tot += -(-max(t.numel() * t.element_size(), 1) // 256) * 256
-            blk, buf = PINNED.take(tot)
-            with torch.cuda.stream(st):
-                for (k, t), o in zip(cols, offs):
-                    nb = t.numel() * t.element_size()
-                    if nb:
-                        blk[o:o + nb].copy_(t.reshape(-1).view(torch.uint8), non_blocking=True)
-                    t.record_stream(st)
-            st.synchronize()
-            for (k, t), o in zip(cols, offs):
-                dt = np.dtype(str(t.dtype).replace('torch.', ''))
-                n[k] = np.frombuffer(buf, dtype=dt, count=t.numel(), offset=o)
-            del blk, buf  # (the views keep the block leased)
-        for k, t in self.cols.items():
-            if t is None:
-                n[k] = None
+                else:
+                    h = torch.empty(max(t.numel(), 1), dtype=t.dtype, pin_memory=True)[:t.numel()]
+                    h.copy_(t, non_blocking=True)
+                t.record_stream(st)
+                out[k] = h
+        st.synchronize()
+        n = {k: (v.numpy() if v is not None else None) for k, v in out.items()}
         rd = Rendered(n['a_off'], n['a_bytes'], n['b_off'], n['b_bytes'],
                       n['is_rn'].astype(bool), n['num_tokens'].view(np.uint16))
         if self.masking:

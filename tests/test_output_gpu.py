@@ -439,27 +439,3 @@ def test_pretrain_cli_num_shards_world2_unequal_batches(tmp_path):
             counts.append(t.num_rows)
         assert sorted(shards) == parts
         assert max(counts) - min(counts) <= 1
-
-
-def test_pinned_pool_reuse_and_lease():
-    """output.PinnedPool: a block returns to the pool only when the last numpy view made from its
-    buffer is gone, and a later request of a fitting size gets the same block back."""
-    import gc
-    from lddl_amd.output import PinnedPool
-    pool = PinnedPool()
-    t, buf = pool.take(100 << 20)
-    v = np.frombuffer(buf, dtype=np.uint8, count=10, offset=5)
-    v[:] = 7
-    del buf, t
-    gc.collect()
-    assert pool.allocations == 1 and not pool._free  # the view still leases the block
-    del v
-    gc.collect()
-    assert len(pool._free) == 1
-    t2, buf2 = pool.take(90 << 20)
-    assert pool.allocations == 1 and not pool._free and t2.is_pinned()
-    assert np.frombuffer(buf2, dtype=np.uint8, count=10, offset=5).tolist() == [7] * 10
-    del t2, buf2
-    gc.collect()
-    t3, _ = pool.take(1 << 30)  # too large for the pooled block: a new allocation
-    assert pool.allocations == 2 and t3.numel() >= 1 << 30

@@ -80,6 +80,18 @@ def test_mask_pool_overflow_replans(ctx, docs_dev, monkeypatch):
     test_pairs_golden_gpu(name, ctx, docs_dev)
 
 
+@pytest.mark.parametrize('env', [{'LDDL_FY_MODE': '0'}, {'LDDL_FY_MODE': '1'},
+                                 {'LDDL_FY_LW': '32'}])
+def test_fy_resolve_variants_golden(ctx, docs_dev, monkeypatch, env):
+    """Every mask-replay variant against the reference goldens: the guarded and the branch-free
+    steps at every sequence length (the defaults use one kind per length), and 32 pairs per wave
+    at seq 512 (the branch-free steps rely on the planner's padded draw regions)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for name in ('s128_mask', 's512_mask', 's64_mask_ratio'):
+        test_pairs_golden_gpu(name, ctx, docs_dev)
+
+
 def test_partition_shuffle_global_path(ctx, docs_dev, monkeypatch):
     """The partition shuffle's path for partitions beyond the LDS budget (swaps in global
     memory, inverse permutation by cycles) gives the reference's pair order."""
