@@ -2707,7 +2707,9 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
       // seq > 256 (50.7 ms)
       const int fy_mode = getenv("LDDL_FY_MODE") ? atoi(getenv("LDDL_FY_MODE")) : -1;
       const int fy_lw = getenv("LDDL_FY_LW") ? atoi(getenv("LDDL_FY_LW")) : 16;
-      const int fy_ra = getenv("LDDL_FY_RA") ? atoi(getenv("LDDL_FY_RA")) : 0;
+      // move-only groups at seq > 256 read one entry ahead (46.8 -> 44.4 ms; 2 ahead 45.9, 3 ahead
+      // 46.7: the forwarding selects grow; profiles/r05m_*). LDDL_FY_RA=0..3 (A/B)
+      const int fy_ra = getenv("LDDL_FY_RA") ? atoi(getenv("LDDL_FY_RA")) : 1;
 #define LDDL_FY_LAUNCH(T, NG, LW, BF, ...)                                                     \
   hipLaunchKernelGGL((fy_resolve_kernel<T, T, NG, LW, BF, ##__VA_ARGS__>),                     \
                      dim3((unsigned)((P->n_pairs + LW - 1) / LW)), dim3(LW),                   \

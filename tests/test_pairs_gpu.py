@@ -81,11 +81,13 @@ def test_mask_pool_overflow_replans(ctx, docs_dev, monkeypatch):
 
 
 @pytest.mark.parametrize('env', [{'LDDL_FY_MODE': '0'}, {'LDDL_FY_MODE': '1'},
-                                 {'LDDL_FY_LW': '32'}])
+                                 {'LDDL_FY_LW': '32'}, {'LDDL_FY_RA': '0'}, {'LDDL_FY_RA': '2'},
+                                 {'LDDL_FY_RA': '3'}])
 def test_fy_resolve_variants_golden(ctx, docs_dev, monkeypatch, env):
     """Every mask-replay variant against the reference goldens: the guarded and the branch-free
     steps at every sequence length (the defaults use one kind per length), and 32 pairs per wave
-    at seq 512 (the branch-free steps rely on the planner's padded draw regions)."""
+    at seq 512, and 0 / 2 / 3 entries read ahead in its move-only groups (default 1; the
+    branch-free steps rely on the planner's padded draw regions)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     for name in ('s128_mask', 's512_mask', 's64_mask_ratio'):
