@@ -1620,6 +1620,7 @@ struct ResolveArgs {
   const int64_t* dstq;
   GatherRec* rec;
   int2* cnt;
+  int32_t col_rows;  // entries per lane column in LDS (seq rounded up to 16)
 };
 
 // A lane's column of LDS entries; 16-bit: x[k * LW + lane]; 8-bit (seq <= 256): dword k/4 of
@@ -1657,7 +1658,7 @@ struct LaneCol<uint8_t, LW> {
 // LW: pairs (lanes) per workgroup of one wave. Long pairs run with LW < 64: a lane's column is
 // seq entries, so at seq 512 a full wave holds 64 KB of LDS and only two fit a CU; fewer lanes
 // per wave put more waves (more independent step chains) on each SIMD.
-template <typename T, typename D, int NG, int LW = 64, bool kBF = false, int kRA = 0>
+template <typename T, typename D, int NG, int LW = 64, bool kBF = false, int kRA = 0, int kPf = 4>
 __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_xb[];
   constexpr int kPerVec = 16 / (int)sizeof(D);  // draws per uint4
@@ -1666,6 +1667,19 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
   // (XCD-contiguous blocks: a partition's pairs, their kept-sentence offsets and records meet
   // in one L2)
   const int64_t q = xcd_block(blockIdx.x, gridDim.x) * LW + lane;
+  // 16-bit columns, branch-free steps: the workgroup writes the identity into every column at
+  // once, 8 rows (one entry per lane and row) per 16-byte store per lane, before any lane leaves
+  // (a lane's own per-entry iota was ~20 % of the kernel's LDS instructions and half its scalar
+  // ones; C3 profiles/r05n_*). Rows past a lane's nc are only touched by its padding steps.
+  constexpr bool kCoopIota = kBF && sizeof(T) == 2 && LW == 16;
+  if constexpr (kCoopIota) {
+    const int rows = (int)(R.col_rows);
+    uint4* base = reinterpret_cast<uint4*>(s_xb);
+    for (int k0 = 0; k0 < rows; k0 += 8) {
+      const uint32_t k = (uint32_t)(k0 + (lane >> 1)), kk = k | k << 16;
+      base[2 * k + (lane & 1)] = make_uint4(kk, kk, kk, kk);  // row k = 32 bytes = 2 uint4
+    }
+  }
   if (q >= R.n_pairs) return;
   const int64_t slot = R.src[q];
   const int64_t oq = R.dstq ? R.dstq[q] : 0;
@@ -1780,7 +1794,7 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
 #pragma unroll
     for (int g = 0; g < NG; ++g)
       if (g < nvec) jv[g] = jp[g];
-    x.iota(nc);  // (after the draws' loads are issued)
+    if (!kCoopIota) x.iota(nc);  // (after the draws' loads are issued)
 #pragma unroll
     for (int g = NG - 1; g >= 0; --g)
       if (g < nvec) vec(g, jv[g]);
@@ -1790,11 +1804,10 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
     // r04zk_*)
     auto ld = [&](int g) { return jp[g < 0 ? 0 : g]; };
     const int top = nvec - 1;
-    constexpr int kPf = 4;
     uint4 rv[kPf];
 #pragma unroll
     for (int u = 0; u < kPf; ++u) rv[u] = ld(top - u);
-    x.iota(nc);
+    if (!kCoopIota) x.iota(nc);
     for (int g = top; g >= 0; g -= kPf) {
 #pragma unroll
       for (int u = 0; u < kPf; ++u) {
@@ -2697,10 +2710,11 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
   if (prm->masking) {
     if (P->n_pairs) {
       ResolveArgs RA{M.slots, P->n_pairs, P->desc, spool, jpool, P->mpos, P->kscan, P->dense, cls,
-                     sep, M.dstq, P->rec, pcnt};
+                     sep, M.dstq, P->rec, pcnt, 0};
       const dim3 grid((unsigned)((P->n_pairs + 63) / 64));
       // a lane's column covers the padded draw region (steps up to nc rounded up to 16)
       const size_t col = (size_t)((prm->seq + 15) & ~15);
+      RA.col_rows = (int32_t)col;
       // Branch-free steps for long pairs (C3, seq 512: 77.6 -> 46.8 ms), the guarded ones at
       // seq <= 131 (64 pairs per wave: 10.1 ms against 11.5 branch-free; profiles/r05k_*).
       // A/B: LDDL_FY_MODE=0 / 1 forces one kind everywhere; LDDL_FY_LW=32: 32 pairs per wave at
@@ -2710,6 +2724,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
       // move-only groups at seq > 256 read one entry ahead (46.8 -> 44.4 ms; 2 ahead 45.9, 3 ahead
       // 46.7: the forwarding selects grow; profiles/r05m_*). LDDL_FY_RA=0..3 (A/B)
       const int fy_ra = getenv("LDDL_FY_RA") ? atoi(getenv("LDDL_FY_RA")) : 1;
+      // draw vectors (8 steps each) in flight per lane at seq > 256 (A/B: LDDL_FY_PF=2 / 8)
+      const int fy_pf = getenv("LDDL_FY_PF") ? atoi(getenv("LDDL_FY_PF")) : 4;
 #define LDDL_FY_LAUNCH(T, NG, LW, BF, ...)                                                     \
   hipLaunchKernelGGL((fy_resolve_kernel<T, T, NG, LW, BF, ##__VA_ARGS__>),                     \
                      dim3((unsigned)((P->n_pairs + LW - 1) / LW)), dim3(LW),                   \
@@ -2728,6 +2744,8 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
         else LDDL_FY_LAUNCH(uint16_t, 0, 32, false);
       } else {
         if (!fy_mode) LDDL_FY_LAUNCH(uint16_t, 0, 16, false);
+        else if (fy_ra == 1 && fy_pf == 8) LDDL_FY_LAUNCH(uint16_t, 0, 16, true, 1, 8);
+        else if (fy_ra == 1 && fy_pf == 2) LDDL_FY_LAUNCH(uint16_t, 0, 16, true, 1, 2);
         else if (fy_ra == 1) LDDL_FY_LAUNCH(uint16_t, 0, 16, true, 1);
         else if (fy_ra == 2) LDDL_FY_LAUNCH(uint16_t, 0, 16, true, 2);
         else if (fy_ra == 3) LDDL_FY_LAUNCH(uint16_t, 0, 16, true, 3);
