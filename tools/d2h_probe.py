@@ -109,3 +109,28 @@ for name, fn, fr in (('torch', alloc_torch, lambda r: None), ('hipHostMalloc', a
     del box
     print('512 MiB pageable H2D: alone {:.3f} s, beside a 4 GiB {} allocation {:.3f} s'.format(
         t_alone, name, tb), flush=True)
+
+# ... and other HIP work beside such an allocation: 100 small kernel launches + sync, and a
+# 512 MiB H2D copy from pinned memory
+dev = torch.ones(1 << 20, device='cuda')
+pin_src = torch.empty(512 << 20, dtype=torch.uint8, pin_memory=True)
+t(lambda: pin_src.to('cuda', non_blocking=True))
+
+
+def launches():
+    for _ in range(100):
+        dev.add_(1.0)
+
+
+tl_alone, _ = t(launches)
+tp_alone, _ = t(lambda: pin_src.to('cuda', non_blocking=True))
+for name, fn in (('100 launches', launches), ('512 MiB pinned H2D', lambda: pin_src.to('cuda', non_blocking=True))):
+    box = []
+    th = threading.Thread(target=lambda: box.append(alloc_hip(n)))
+    th.start()
+    time.sleep(0.005)
+    tb, _ = t(fn)
+    th.join()
+    free_hip(box[0])
+    print('{}: alone {:.4f} s, beside a 4 GiB hipHostMalloc {:.4f} s'.format(
+        name, tl_alone if name.startswith('100') else tp_alone, tb), flush=True)
