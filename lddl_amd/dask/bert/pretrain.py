@@ -302,6 +302,18 @@ def process_batch(ctx, args, partitions, corpus, outdir, timer=None, executor=No
 
     def finish(stream=None):
         _trace('d2h_start', index[0])
+        chunk = _D2H_CHUNK_BYTES
+        if args.output_format == 'parquet' and chunk > 0:
+            # string columns in partition groups of ~chunk bytes, each handed to the writers as
+            # it lands (output.DeviceRendered.to_host_chunks)
+            paths = []
+            for p0, p1, rd in drd.to_host_chunks(part_rows, chunk, stream):
+                paths += output.write_parquet(outdir, rd, part_rows[p0:p1 + 1], index[p0:p1],
+                                              args.masking, nbins,
+                                              None if counts is None else counts[p0:p1],
+                                              executor=executor, futures=futures)
+            _trace('d2h_end', index[0])
+            return paths
         rd = drd.to_host(stream)
         _trace('d2h_end', index[0])
         if args.output_format == 'parquet':
@@ -320,6 +332,9 @@ def process_batch(ctx, args, partitions, corpus, outdir, timer=None, executor=No
 
 _T0 = time.perf_counter()
 _TRACE = os.environ.get('LDDL_TRACE_PIPELINE')
+# rendered batches leave the GPU in partition groups of about this many MiB of strings (0: the
+# whole batch in one pinned allocation per column, the round-4 behaviour)
+_D2H_CHUNK_BYTES = int(os.environ.get('LDDL_D2H_CHUNK_MB', '128')) << 20
 
 
 def _trace(what, batch):

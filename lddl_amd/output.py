@@ -154,6 +154,82 @@ class DeviceRendered:
         self.cols = None
         return rd
 
+    _ROW_COLS = ('a_off', 'b_off', 'l_off', 'npy_off', 'is_rn', 'num_tokens', 'bin_id')
+    _BYTE_COLS = (('a_off', 'a_bytes'), ('b_off', 'b_bytes'), ('l_off', 'l_bytes'),
+                  ('npy_off', 'npy_bytes'))
+
+    def to_host_chunks(self, part_rows, chunk_bytes, stream=None):
+        """to_host() in pieces: the per-row columns once, then the string columns of consecutive
+        partition groups of about `chunk_bytes` each, yielded as (p0, p1, Rendered) with the
+        batch's global row numbers and offsets (the byte columns are addressed through
+        `_Shifted`). A pinned allocation holds up every concurrent pageable host copy of the
+        process for its whole duration (tools/d2h_probe.py: a 512 MiB H2D 0.010 s alone, 0.18-0.29
+        s beside a 4 GiB allocation), so one allocation per batch stalled the next batch's
+        pageable copies for ~0.2-0.3 s; chunks bound each stall to a few ms, and the blocks that
+        their writes release come back from torch's host cache for the later chunks."""
+        st = stream if stream is not None else torch.cuda.current_stream()
+        if self.event is not None:
+            st.wait_event(self.event)
+        cols = self.cols
+        host = {}
+        with torch.cuda.stream(st):
+            for k in self._ROW_COLS:
+                t = cols.get(k)
+                if t is None:
+                    continue
+                h = torch.empty(max(t.numel(), 1), dtype=t.dtype, pin_memory=True)[:t.numel()]
+                h.copy_(t, non_blocking=True)
+                t.record_stream(st)
+                host[k] = h
+        st.synchronize()
+        n = {k: v.numpy() for k, v in host.items()}
+        bin_id = n['bin_id'].astype(np.int64) if 'bin_id' in n else None
+        byte_cols = [(ok, bk) for ok, bk in self._BYTE_COLS if cols.get(bk) is not None]
+        n_part = len(part_rows) - 1
+        p0 = 0
+        while p0 < n_part:
+            def span(p, q):
+                r0, r1 = int(part_rows[p]), int(part_rows[q])
+                return sum(int(n[ok][r1]) - int(n[ok][r0]) for ok, _ in byte_cols)
+            p1 = p0 + 1
+            while p1 < n_part and span(p0, p1 + 1) <= chunk_bytes:
+                p1 += 1
+            r0, r1 = int(part_rows[p0]), int(part_rows[p1])
+            chunk = {}
+            with torch.cuda.stream(st):
+                for ok, bk in byte_cols:
+                    b0, b1 = int(n[ok][r0]), int(n[ok][r1])
+                    t = cols[bk]
+                    h = torch.empty(max(b1 - b0, 1), dtype=t.dtype, pin_memory=True)[:b1 - b0]
+                    if b1 > b0:
+                        h.copy_(t[b0:b1], non_blocking=True)
+                    chunk[bk] = _Shifted(h.numpy(), b0)
+            st.synchronize()
+            rd = Rendered(n['a_off'], chunk['a_bytes'], n['b_off'], chunk['b_bytes'],
+                          n['is_rn'].view(bool), n['num_tokens'].view(np.uint16))
+            if self.masking:
+                rd.l_off, rd.l_bytes = n['l_off'], chunk['l_bytes']
+                rd.npy_off, rd.npy_bytes = n['npy_off'], chunk['npy_bytes']
+            if bin_id is not None:
+                rd.bin_id = bin_id
+            yield p0, p1, rd
+            p0 = p1
+        for _, bk in byte_cols:
+            cols[bk].record_stream(st)
+        self.cols = None
+
+
+class _Shifted:
+    """A string column's host bytes [base, base + len) addressed with the batch's global byte
+    offsets (what `_var` and `Rendered.row` slice)."""
+    __slots__ = ('a', 'base')
+
+    def __init__(self, a, base):
+        self.a, self.base = a, base
+
+    def __getitem__(self, s):
+        return self.a[s.start - self.base:s.stop - self.base]
+
 
 def render_device(ctx, pb, rows=None, bin_id=None):
     """The GPU half of render(): kernels only (one host sync for the byte totals)."""

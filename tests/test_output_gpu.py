@@ -119,13 +119,20 @@ def _write_source(root, n_docs=300, seed=11):
             f.write('\n'.join(chunk) + '\n\n')
 
 
-@pytest.mark.parametrize('binned,params,workers', [(False, False, 1), (True, False, 2),
-                                                    (False, True, 2), (True, False, 3)])
-def test_pretrain_cli_vs_oracle(tmp_path, binned, params, workers):
+@pytest.mark.parametrize('binned,params,workers,chunk', [(False, False, 1, None),
+                                                          (True, False, 2, 1),
+                                                          (False, True, 2, 0),
+                                                          (True, False, 3, None),
+                                                          (False, False, 1, 1)])
+def test_pretrain_cli_vs_oracle(tmp_path, monkeypatch, binned, params, workers, chunk):
     """CLI output == the oracle's rows per partition. workers = 3: one partition per GPU batch
-    (--gpu-batch-bytes 1) over three concurrent GPU worker threads (--gpu-workers)."""
+    (--gpu-batch-bytes 1) over three concurrent GPU worker threads (--gpu-workers). chunk: the
+    rendered batch's device-to-host copy in partition groups of that many bytes (1: one
+    partition per group; 0: the whole batch at once; None: the default 128 MiB)."""
     from lddl_amd import synth
     from lddl_amd.dask.bert import pretrain as P
+    if chunk is not None:
+        monkeypatch.setattr(P, '_D2H_CHUNK_BYTES', chunk)
     from oracle import oracle as O
     src = tmp_path / 'source'
     _write_source(str(src))
