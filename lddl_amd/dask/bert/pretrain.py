@@ -496,8 +496,25 @@ class ShardWriters:
                   for b in range(self.nbins)]
 
         writes = []  # this batch's write futures: its pinned copy lives until they finish
+        # the (shard, bin) row ranges in row order (bin-major): contiguous, so the copy can leave
+        # the GPU in groups of them (output.DeviceRendered.to_host_chunks, as process_batch)
+        srt = sorted(ranges, key=lambda x: x[2])
+        bounds = [srt[0][2]] + [x[3] for x in srt] if srt else [0]
+        chunked = _D2H_CHUNK_BYTES > 0 and all(srt[i][2] == bounds[i] for i in range(len(srt)))
 
         def job(stream=None):
+            if chunked:
+                first = True
+                for p0, p1, rd in drd.to_host_chunks(bounds, _D2H_CHUNK_BYTES, stream):
+                    if first:  # appends stay in batch order per (shard, bin) writer
+                        for f in self.pending:
+                            f.result()
+                        self.pending, first = [], False
+                    new = [self.pool.submit(self._append, (s, b), rd, r0, r1)
+                           for s, b, r0, r1 in srt[p0:p1] if r1 > r0]
+                    self.pending += new
+                    writes.extend(new)
+                return
             rd = drd.to_host(stream)
             for f in self.pending:
                 f.result()
@@ -580,6 +597,27 @@ def _any_rank(flag, device):
     t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return bool(t.item())
+
+
+def _warm_gpu_path(ctx, args):
+    """One tiny batch of made-up documents through segment -> tokenize -> pairs -> render, output
+    discarded: the first launch of each kernel (code object loading) and the first allocations
+    happen here, while the host reader is still reading, instead of in the first real batch."""
+    import torch
+    from ... import output
+    doc = ('The first sentence is here. A second one follows it! Then a third, with more words '
+           'in it? The fourth ends the document.')
+    lines = [('{} {}'.format(k, doc)).encode('utf-8') for k in range(8)]
+    corpus = build_doc_corpus([(0, lines[:4]), (1, lines[4:])])
+    pb = make_batch_pairs(ctx, args, [(0, None), (1, None)], corpus)
+    if args.bin_size is not None:
+        nbins = args.target_seq_length // args.bin_size
+        perm, bin_id, _ = output.bin_partitions(ctx, None, pb.part_off, args.bin_size, nbins,
+                                                tok_off=pb.tok_off)
+        output.render_device(ctx, pb, perm, bin_id)
+    else:
+        output.render_device(ctx, pb)
+    torch.cuda.synchronize(ctx.device)
 
 
 def _empty_pairs(ctx, masking):
@@ -788,6 +826,13 @@ def main(args):
     if args.sentence_splitter == 'gpu':
         from ... import punkt
         punkt.set_params(ctx, punkt_params(args))
+    # (only when the read outlasts the setup: with less than one GPU batch of input per rank the
+    # warm-up would sit on the critical path; 1 GB seq 128: segment 0.06-0.09 -> 0.035 s, the run
+    # 1.36-1.47 -> 1.26-1.39 s on one box, profiles/r05s_*)
+    warm = os.environ.get('LDDL_CLI_WARMUP', '1') != '0' and \
+        sum(b.nbytes for b in blocks) >= world * args.gpu_batch_bytes
+    if args.sentence_splitter == 'gpu' and warm:
+        _warm_gpu_path(ctx, args)
     timer = _StageTimer(args.profile_stages)
     _trace('setup_end', -1)
     timer.mark()

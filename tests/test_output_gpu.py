@@ -298,14 +298,19 @@ def test_pretrain_cli_txt_output(tmp_path, binned):
                                                          r['num_tokens']) in got
 
 
-@pytest.mark.parametrize('binned,masking', [(True, True), (False, False)])
-def test_pretrain_cli_num_shards_balanced(tmp_path, binned, masking):
+@pytest.mark.parametrize('binned,masking,chunk', [(True, True, None), (False, False, None),
+                                                   (True, True, 1)])
+def test_pretrain_cli_num_shards_balanced(tmp_path, monkeypatch, binned, masking, chunk):
     """--num-shards (stream plan, world size 1): per GPU batch, bin b's rows (the part.* rows of
     the batch's partitions, in order) are cut into consecutive runs, shard s taking
     batch_shard_counts' share (N or N+1 per shard after every batch), with .num_samples.json;
     checked for one batch and for one batch per partition (`--gpu-batch-bytes 1`); then
-    get_bert_pretrain_data_loader consumes them."""
+    get_bert_pretrain_data_loader consumes them. chunk = 1: the rendered rows leave the GPU one
+    (shard, bin) range at a time."""
     from lddl_amd.balance import batch_shard_counts
+    if chunk is not None:
+        from lddl_amd.dask.bert import pretrain as P0
+        monkeypatch.setattr(P0, '_D2H_CHUNK_BYTES', chunk)
 
     def dealt(batches, S):  # batches: bin b's rows per GPU batch -> rows per shard
         out, prior = [[] for _ in range(S)], 0
