@@ -803,27 +803,23 @@ __global__ void __launch_bounds__(64, 6) plan_replay_kernel(PlanArgs A) {
           const bool fits = pool_fits && jpool_fits;
           if (!fits) *A.overflow = 1;  // (uniform; every lane stores the same flag)
           // random.shuffle(cand_indexes): draws j_i (i = nc-1 .. 1) to the pool
-          // The region's other entries, 0 and [nc, nc rounded up to 16), get j_i = i: fy_resolve's
-          // steps there move an entry onto itself, so its step loop needs no per-step guard.
+          // The region's tail [nc, nc rounded up to 16) gets j_i = i: fy_resolve's steps there move
+          // an entry onto itself, so its step loop needs no per-step guard. (Entry 0 is not
+          // written here: fy_draws' lanes store their rejected words there, and fy_resolve
+          // takes j_0 = 0 itself.)
           const int32_t ip = nc + lane;
           if constexpr (kJB == 1) {
             uint8_t* jd = static_cast<uint8_t*>(A.jpool) + jb;
             rng.fy_draws(nc, [&](int32_t i, uint32_t j) {
               if (fits) jd[i] = (uint8_t)j;  // (fits is uniform: a scalar branch)
             });
-            if (fits && nc > 0) {
-              if (ip < ((nc + 15) & ~15)) jd[ip] = (uint8_t)ip;
-              if (lane == 63) jd[0] = 0;
-            }
+            if (fits && ip < ((nc + 15) & ~15)) jd[ip] = (uint8_t)ip;
           } else {
             uint16_t* jd = static_cast<uint16_t*>(A.jpool) + jb;
             rng.fy_draws(nc, [&](int32_t i, uint32_t j) {
               if (fits) jd[i] = (uint16_t)j;
             });
-            if (fits && nc > 0) {
-              if (ip < ((nc + 15) & ~15)) jd[ip] = (uint16_t)ip;
-              if (lane == 63) jd[0] = 0;
-            }
+            if (fits && ip < ((nc + 15) & ~15)) jd[ip] = (uint16_t)ip;
           }
           STAMP_ADD(2, st_t);
           // decisions of the masked candidates in shuffled order (pretrain.py:208-221)
@@ -1721,21 +1717,27 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
     if (8 * h < num) mp[h] = acc;  // slots [8h, 8h+8) complete (the top group zero-padded)
   };
   // kBF: the same steps without exec-mask branches. The planner pads a pair's draw region
-  // (entry 0 and [nc, nc rounded up to 16) hold j_i = i), so every step of a loaded vector
-  // is x[j] = x[i] unguarded (a padding step rewrites x[i] onto itself); a group in which no
+  // ([nc, nc rounded up to 16) hold j_i = i) and step 0 takes j = 0 (entry 0 of the region is
+  // never a draw), so every step of a loaded vector is x[j] = x[i] unguarded (a padding step
+  // rewrites x[i] onto itself); a group in which no
   // lane of the wave finalises a slot is that move alone (read, wait, write: ~2 VALU per
   // step); otherwise each step also reads y = x[j] before the write (i = 0: j = 0, y = x[0])
   // and keeps its position by select. Round 4's guarded steps spent ~10 scalar exec-mask
   // instructions and three branches per step.
   const int32_t padd = fast ? 1 : 0, thr = fast ? na : INT32_MAX;  // pos = y + padd + (y >= thr)
+  // draw u of a group (step 8h + u); step 0 has none: j_0 = 0
+  auto draw = [&](int h, const uint32_t* w, int u) -> int {
+    const int j = sizeof(D) == 1 ? (int)((w[u >> 2] >> (8 * (u & 3))) & 0xFFu)
+                                 : (int)((w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
+    return u == 0 && h == 0 ? 0 : j;
+  };
   auto group_bf = [&](int h, const uint32_t* w) {
     if (__any(8 * h < num)) {
       uint32_t pos[8];
 #pragma unroll
       for (int u = 7; u >= 0; --u) {
         const int i = 8 * h + u;
-        const int j = sizeof(D) == 1 ? (int)((w[u >> 2] >> (8 * (u & 3))) & 0xFFu)
-                                     : (int)((w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
+        const int j = draw(h, w, u);
         const uint32_t xi = x.get(i);
         const int y = (int)x.get(j);
         x.set(j, xi);
@@ -1746,11 +1748,7 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
                            pos[6] | pos[7] << 16);
     } else if (kRA == 0) {
 #pragma unroll
-      for (int u = 7; u >= 0; --u) {
-        const int j = sizeof(D) == 1 ? (int)((w[u >> 2] >> (8 * (u & 3))) & 0xFFu)
-                                     : (int)((w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
-        x.set(j, x.get(8 * h + u));
-      }
+      for (int u = 7; u >= 0; --u) x.set(draw(h, w, u), x.get(8 * h + u));
     } else {
       // kRA reads ahead: x[i - kRA] is read before step i's write (the group's top kRA entries
       // at its start), so step u's read misses the writes of steps u + 1 .. min(u + kRA, 7),
@@ -1758,9 +1756,7 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
       int jr[8];  // j - 8h: compared with the step offset u
       uint32_t r[8], v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        jr[u] = (sizeof(D) == 1 ? (int)((w[u >> 2] >> (8 * (u & 3))) & 0xFFu)
-                                : (int)((w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu)) - 8 * h;
+      for (int u = 0; u < 8; ++u) jr[u] = draw(h, w, u) - 8 * h;
 #pragma unroll
       for (int u = 7; u >= 8 - kRA; --u) r[u] = x.get(8 * h + u);
 #pragma unroll
