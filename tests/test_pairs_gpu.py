@@ -229,3 +229,46 @@ def test_pairs_empty_and_dropped_inputs(ctx):
     assert len(exp['len_a']) > 0
     for k in ('tokens', 'num_tokens', 'len_a', 'pos', 'labels'):
         assert np.array_equal(np.asarray(out[k]).astype(np.int64), np.asarray(exp[k]).astype(np.int64)), k
+
+
+@pytest.mark.parametrize('seq,ratio,env', [(20, 0.9, {}), (20, 0.9, {'LDDL_FY_MODE': '1'}),
+                                           (131, 0.7, {}), (200, 0.02, {}),
+                                           (300, 0.9, {}), (300, 0.9, {'LDDL_FY_RA': '3'}),
+                                           (512, 0.5, {'LDDL_FY_LW': '32'})])
+def test_mask_replay_extremes_vs_oracle(monkeypatch, seq, ratio, env):
+    """The mask replay (`fy_resolve`) against the oracle where its step kinds meet their edges:
+    seq 20 (a handful of candidates, most of each 16-entry draw region padding), masked_lm_ratio
+    0.9 (nearly every group finalises slots) and 0.02 (one mask per pair: move-only groups
+    throughout), seq 131 (the last register-draw length), 200 / 300 / 512 (1- and 2-byte draws,
+    16 and 32 pairs per wave, read-ahead 1 and 3)."""
+    from lddl_amd import synth
+    from lddl_amd.context import Context
+    from lddl_amd.pairs import make_pairs
+    from oracle import oracle as O
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    vocab = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         'lddl_amd', 'assets', 'vocab_synth_uncased_30522.txt')
+    ctx = Context(vocab)
+    corp = synth.generate(seed=700 + seq, n_bytes=300_000, threads=4)
+    part = np.linspace(0, corp.n_doc, 3).astype(np.int64)
+    seeds = np.asarray([21, 22], np.int64)
+    so = torch.from_numpy(corp.sent_off).cuda()
+    ids, sl = ctx.tokenize(torch.from_numpy(corp.text).cuda(), so)
+    pb = make_pairs(ctx, so, ids, sl, torch.from_numpy(corp.doc_sent_off).cuda(),
+                    torch.from_numpy(part).cuda(), torch.from_numpy(seeds).cuda(), seq=seq, dup=2,
+                    masking=True, masked_lm_ratio=ratio).to_host()
+    tok = O.Tokenizer(vocab)
+    e_ids, e_off = tok.tokenize(corp.text, corp.sent_off)
+    exp = {'tokens': [], 'num_tokens': [], 'len_a': [], 'pos': [], 'labels': []}
+    for p in range(2):
+        ds = corp.doc_sent_off[part[p]:part[p + 1] + 1]
+        out = O.partition_pairs(ds, e_off, e_ids, int(seeds[p]), 2, seq, True, tok.vocab_size,
+                                *(tok.token_id(t) for t in ('[CLS]', '[SEP]', '[MASK]')),
+                                masked_lm_ratio=ratio)
+        for k in exp:
+            exp[k].append(out[k])
+    assert len(pb['num_tokens']) > 0
+    for k in exp:
+        assert np.array_equal(np.asarray(pb[k]).astype(np.int64),
+                              np.concatenate(exp[k]).astype(np.int64)), k
