@@ -185,15 +185,7 @@ class DeviceRendered:
         n = {k: v.numpy() for k, v in host.items()}
         bin_id = n['bin_id'].astype(np.int64) if 'bin_id' in n else None
         byte_cols = [(ok, bk) for ok, bk in self._BYTE_COLS if cols.get(bk) is not None]
-        n_part = len(part_rows) - 1
-        p0 = 0
-        while p0 < n_part:
-            def span(p, q):
-                r0, r1 = int(part_rows[p]), int(part_rows[q])
-                return sum(int(n[ok][r1]) - int(n[ok][r0]) for ok, _ in byte_cols)
-            p1 = p0 + 1
-            while p1 < n_part and span(p0, p1 + 1) <= chunk_bytes:
-                p1 += 1
+        for p0, p1 in chunk_groups(part_rows, [n[ok] for ok, _ in byte_cols], chunk_bytes):
             r0, r1 = int(part_rows[p0]), int(part_rows[p1])
             chunk = {}
             with torch.cuda.stream(st):
@@ -213,10 +205,27 @@ class DeviceRendered:
             if bin_id is not None:
                 rd.bin_id = bin_id
             yield p0, p1, rd
-            p0 = p1
         for _, bk in byte_cols:
             cols[bk].record_stream(st)
         self.cols = None
+
+
+def chunk_groups(part_rows, offsets, chunk_bytes):
+    """Consecutive partition groups [p0, p1) for DeviceRendered.to_host_chunks: each group adds
+    partitions while its bytes (summed over the byte columns, whose row offsets are `offsets`)
+    stay <= chunk_bytes; a group holds at least one partition."""
+    n_part = len(part_rows) - 1
+    out, p0 = [], 0
+    while p0 < n_part:
+        def span(q):
+            r0, r1 = int(part_rows[p0]), int(part_rows[q])
+            return sum(int(o[r1]) - int(o[r0]) for o in offsets)
+        p1 = p0 + 1
+        while p1 < n_part and span(p1 + 1) <= chunk_bytes:
+            p1 += 1
+        out.append((p0, p1))
+        p0 = p1
+    return out
 
 
 class _Shifted:
