@@ -552,18 +552,19 @@ class ShardWriters:
             for f in [self.pool.submit(self._merge, k) for k in list(self.pieces)]:
                 f.result()
             os.rmdir(self.piece_dir)
-        paths = []
+        paths, done = [], []
+        empty = output.schema(self.masking, self.binned).empty_table()
         for s in sorted(self.shards):
             for b in range(self.nbins):
                 w = self.writers.pop((s, b), None)
-                if w is not None:
-                    w.close()
-                elif (s, b) in merged:
-                    pass  # written from its pieces above
-                else:
-                    pq.write_table(output.schema(self.masking, self.binned).empty_table(),
-                                   self.name(s, b), compression=output.DEFAULT_COMPRESSION)
+                if w is not None:  # footers written on the pool (one writer per task)
+                    done.append(self.pool.submit(w.close))
+                elif (s, b) not in merged:  # (merged: written from its pieces above)
+                    done.append(self.pool.submit(pq.write_table, empty, self.name(s, b),
+                                                 compression=output.DEFAULT_COMPRESSION))
                 paths.append(self.name(s, b))
+        for f in done:
+            f.result()
         return paths
 
 
