@@ -1675,6 +1675,9 @@ __global__ void __launch_bounds__(64) fy_resolve_kernel(ResolveArgs R) {
       const uint32_t k = (uint32_t)(k0 + (lane >> 1)), kk = k | k << 16;
       base[2 * k + (lane & 1)] = make_uint4(kk, kk, kk, kk);  // row k = 32 bytes = 2 uint4
     }
+    // lanes wrote rows of other lanes' columns: order the fill before any lane reads its own
+    // column (a one-wave workgroup: the barrier is a wait on the LDS stores)
+    __syncthreads();
   }
   if (q >= R.n_pairs) return;
   const int64_t slot = R.src[q];
@@ -2722,6 +2725,16 @@ extern "C" int lddl_pairs_plan(lddl_ctx* c, void* stream, const lddl_pair_params
       const int fy_ra = getenv("LDDL_FY_RA") ? atoi(getenv("LDDL_FY_RA")) : 1;
       // draw vectors (8 steps each) in flight per lane at seq > 256 (A/B: LDDL_FY_PF=2 / 8)
       const int fy_pf = getenv("LDDL_FY_PF") ? atoi(getenv("LDDL_FY_PF")) : 4;
+      // the A/B knobs take only the values a test runs (unsupported values and
+      // combinations were ignored without notice)
+      if (fy_mode < -1 || fy_mode > 1) LDDL_FAIL(-1, "LDDL_FY_MODE must be 0 or 1");
+      if (fy_lw != 16 && fy_lw != 32) LDDL_FAIL(-1, "LDDL_FY_LW must be 16 or 32");
+      if (fy_ra < 0 || fy_ra > 3) LDDL_FAIL(-1, "LDDL_FY_RA must be 0 .. 3");
+      if (fy_pf != 2 && fy_pf != 4 && fy_pf != 8) LDDL_FAIL(-1, "LDDL_FY_PF must be 2, 4 or 8");
+      if (fy_pf != 4 && fy_ra != 1) LDDL_FAIL(-1, "LDDL_FY_PF applies with LDDL_FY_RA=1 only");
+      if ((fy_ra != 1 || fy_pf != 4) && (fy_mode == 0 || fy_lw == 32))
+        LDDL_FAIL(-1, "LDDL_FY_RA / PF select 16-lane branch-free variants (not with LDDL_FY_MODE=0 "
+                      "or LDDL_FY_LW=32)");
 #define LDDL_FY_LAUNCH(T, NG, LW, BF, ...)                                                     \
   hipLaunchKernelGGL((fy_resolve_kernel<T, T, NG, LW, BF, ##__VA_ARGS__>),                     \
                      dim3((unsigned)((P->n_pairs + LW - 1) / LW)), dim3(LW),                   \

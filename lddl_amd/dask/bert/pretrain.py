@@ -346,6 +346,18 @@ def _trace(what, batch):
                                                                threading.current_thread().name))
 
 
+def _row_order(ranges):
+    """The sharded writer's (shard, bin, r0, r1) row ranges in row order (the balanced table is
+    bin-major, `ranges` shard-major), the chunk bounds over them and whether they tile the rows
+    contiguously (then the copy leaves the GPU in groups of them, as process_batch does). Empty
+    ranges sort before the non-empty range that starts at the same row (key (r0, r1)); sorting on
+    r0 alone put an empty (R, R) after (R, R + k) and the check failed for any batch in which a
+    shard received no rows of a bin."""
+    srt = sorted(ranges, key=lambda x: (x[2], x[3]))
+    bounds = [srt[0][2]] + [x[3] for x in srt] if srt else [0]
+    return srt, bounds, all(srt[i][2] == bounds[i] for i in range(len(srt)))
+
+
 def _copy_stream(ctx):
     import torch
     s = getattr(ctx, '_copy_stream', None)
@@ -435,6 +447,7 @@ class ShardWriters:
                                                                          masking, pool)
         self.max_inflight_bytes = max_inflight_bytes  # pinned bytes of rendered batches
         self.writers, self.pending, self.shards, self.jobs = {}, [], set(), []
+        self.last_chunked = None  # the last batch left the GPU in row-range groups (tests)
         needed = (n_local_shards or 0) * nbins
         self.pieces = None  # {(shard, bin): [piece paths]} in piece mode
         if (max_open is not None and needed > max_open) or not _open_file_budget(needed):
@@ -496,11 +509,9 @@ class ShardWriters:
                   for b in range(self.nbins)]
 
         writes = []  # this batch's write futures: its pinned copy lives until they finish
-        # the (shard, bin) row ranges in row order (bin-major): contiguous, so the copy can leave
-        # the GPU in groups of them (output.DeviceRendered.to_host_chunks, as process_batch)
-        srt = sorted(ranges, key=lambda x: x[2])
-        bounds = [srt[0][2]] + [x[3] for x in srt] if srt else [0]
-        chunked = _D2H_CHUNK_BYTES > 0 and all(srt[i][2] == bounds[i] for i in range(len(srt)))
+        srt, bounds, contiguous = _row_order(ranges)
+        chunked = _D2H_CHUNK_BYTES > 0 and contiguous
+        self.last_chunked = chunked
 
         def job(stream=None):
             if chunked:

@@ -308,8 +308,16 @@ def test_pretrain_cli_num_shards_balanced(tmp_path, monkeypatch, binned, masking
     get_bert_pretrain_data_loader consumes them. chunk = 1: the rendered rows leave the GPU one
     (shard, bin) range at a time."""
     from lddl_amd.balance import batch_shard_counts
+    from lddl_amd.dask.bert import pretrain as P0
+    seen = []  # whether each sharded batch's ranges tiled its rows (the chunked copy ran)
+    real_order = P0._row_order
+
+    def row_order(ranges):
+        out = real_order(ranges)
+        seen.append(out[2])
+        return out
+    monkeypatch.setattr(P0, '_row_order', row_order)
     if chunk is not None:
-        from lddl_amd.dask.bert import pretrain as P0
         monkeypatch.setattr(P0, '_D2H_CHUNK_BYTES', chunk)
 
     def dealt(batches, S):  # batches: bin b's rows per GPU batch -> rows per shard
@@ -335,6 +343,7 @@ def test_pretrain_cli_num_shards_balanced(tmp_path, monkeypatch, binned, masking
     assert len(P.rank_batches(P.attach_args().parse_args(
         ['--sink', 'x', '--gpu-batch-bytes', '1', '--shuffle-group-bytes', '1']),
         P.plan_partitions(args))) == n_part  # one batch per partition in shards_b
+    assert seen and all(seen)  # every batch took the chunked copy
     ns = json.loads((tmp_path / 'shards' / '.num_samples.json').read_text())
     ns_b = json.loads((tmp_path / 'shards_b' / '.num_samples.json').read_text())
     assert ns == ns_b  # the same counts per shard (N / N+1 after every batch)

@@ -50,3 +50,27 @@ def test_shifted_column_builds_the_same_table():
                     _Shifted(b[b_off[r0]:b_off[r1]].copy(), int(b_off[r0])), rn, nt)
     assert table(part, r0, r1, False, False).equals(table(full, r0, r1, False, False))
     assert [part.row(r) for r in range(r0, r1)] == [full.row(r) for r in range(r0, r1)]
+
+
+def test_sharded_row_order_with_empty_ranges():
+    """ShardWriters' (shard, bin, r0, r1) ranges come shard-major while the rows are bin-major;
+    shards that got no rows of a bin have empty ranges that start where the next bin's first
+    non-empty range starts. Sorted by (r0, r1) they still tile the rows, so the chunked copy runs
+    (sorting on r0 alone put the empty range after the non-empty one)."""
+    from lddl_amd.dask.bert.pretrain import _row_order
+    rng = np.random.default_rng(5)
+    for trial in range(200):
+        S, B = int(rng.integers(1, 9)), int(rng.integers(1, 6))
+        counts = rng.integers(0, 3, (B, S)) * (rng.random((B, S)) < 0.6)  # many empty
+        starts, o = {}, 0
+        for b in range(B):  # bin-major rows
+            for s in range(S):
+                starts[(s, b)] = (o, o + int(counts[b, s]))
+                o += int(counts[b, s])
+        ranges = [(s, b) + starts[(s, b)] for s in range(S) for b in range(B)]  # shard-major
+        srt, bounds, contiguous = _row_order(ranges)
+        assert contiguous, (trial, ranges)
+        assert bounds[0] == 0 and bounds[-1] == o
+        assert sorted(srt) == sorted(ranges)
+    # a gap is still reported
+    assert not _row_order([(0, 0, 0, 2), (1, 0, 3, 4)])[2]

@@ -82,16 +82,30 @@ def test_mask_pool_overflow_replans(ctx, docs_dev, monkeypatch):
 
 @pytest.mark.parametrize('env', [{'LDDL_FY_MODE': '0'}, {'LDDL_FY_MODE': '1'},
                                  {'LDDL_FY_LW': '32'}, {'LDDL_FY_RA': '0'}, {'LDDL_FY_RA': '2'},
-                                 {'LDDL_FY_RA': '3'}])
+                                 {'LDDL_FY_RA': '3'}, {'LDDL_FY_PF': '2'}, {'LDDL_FY_PF': '8'}])
 def test_fy_resolve_variants_golden(ctx, docs_dev, monkeypatch, env):
     """Every mask-replay variant against the reference goldens: the guarded and the branch-free
     steps at every sequence length (the defaults use one kind per length), and 32 pairs per wave
-    at seq 512, and 0 / 2 / 3 entries read ahead in its move-only groups (default 1; the
-    branch-free steps rely on the planner's padded draw regions)."""
+    at seq 512, 0 / 2 / 3 entries read ahead in its move-only groups (default 1; the
+    branch-free steps rely on the planner's padded draw regions) and 2 / 8 draw vectors in flight
+    (default 4)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     for name in ('s128_mask', 's512_mask', 's64_mask_ratio'):
         test_pairs_golden_gpu(name, ctx, docs_dev)
+
+
+@pytest.mark.parametrize('env', [{'LDDL_FY_RA': '5'}, {'LDDL_FY_PF': '3'}, {'LDDL_FY_LW': '8'},
+                                 {'LDDL_FY_PF': '8', 'LDDL_FY_RA': '2'},
+                                 {'LDDL_FY_MODE': '0', 'LDDL_FY_RA': '2'}])
+def test_fy_resolve_rejects_unsupported_knobs(docs_dev, monkeypatch, env):
+    """Unsupported LDDL_FY_* values and combinations raise instead of falling through to another
+    variant. A fresh Context: the failed call is not allowed to touch the shared one."""
+    from lddl_amd.context import Context
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    with pytest.raises(Exception, match='LDDL_FY'):
+        test_pairs_golden_gpu('s512_mask', Context(VOCAB_UNCASED, True), docs_dev)
 
 
 def test_partition_shuffle_global_path(ctx, docs_dev, monkeypatch):
