@@ -14,7 +14,9 @@ labels). Every step recomputes everything from the text; nothing is cached betwe
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 Multi-GPU: documents are sharded across ranks (each rank owns disjoint documents of the corpus and
-its own partitions); the path has no data-path collective for C2, so `scaling` is "weak".
+its own partitions); the path has no data-path collective for C2, so `scaling` is "weak". At N > 1
+the line also carries `c4_exchange`: one C4-style step per rank (seq 512, 64 bins, 8 x N shards)
+through the load balance, i.e. the RCCL bin-count all-gather and all-to-all-v exchange.
 value = sum over ranks of output tokens (sum of num_tokens, [CLS]/[SEP] included) / max rank time.
 """
 import argparse
@@ -96,6 +98,76 @@ def st_moved_sum(x, world, dev):
     t = torch.tensor([x], dtype=torch.int64, device=RED_DEV or dev)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
+
+
+def st_max(x, world, dev):
+    """Max of a per-rank float over all ranks."""
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=RED_DEV or dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def partition_prefix(corp, part, max_bytes):
+    """The number of leading whole partitions of `part` that hold at most max_bytes of text (at
+    least one)."""
+    doc_b = corp.sent_off[corp.doc_sent_off[part]]  # text byte at each partition boundary
+    p1 = int(np.searchsorted(doc_b, doc_b[0] + max_bytes, 'right')) - 1
+    return int(min(max(p1, 1), len(part) - 1))
+
+
+def c4_exchange(args, ctx, dev, corp, part, seeds, text, world):
+    """N > 1 beside the C2 headline (which has no data-path collective): one C4-style step on
+    every rank — the rank's first ~args.exchange_bytes of text, seq 512, 64 bins of 8 tokens,
+    balanced into 8 x N shards by StreamBalancer — so that a scaling run also measures the two
+    collectives north_star names: the per-bin count all-gather and the all-to-all-v of the rows
+    over each rank's shard quota (RCCL over xGMI; gloo through host tensors in the one-GPU
+    rehearsal). One warm-up step, then one measured step; times are the max over ranks."""
+    from lddl_amd.balance import StreamBalancer
+    from lddl_amd.pairs import make_pairs
+    p1 = partition_prefix(corp, part, args.exchange_bytes)
+    d1 = int(part[p1])
+    s1 = int(corp.doc_sent_off[d1])
+    b1 = int(corp.sent_off[s1])
+    up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    sent_off, doc_off = up(corp.sent_off[:s1 + 1]), up(corp.doc_sent_off[:d1 + 1])
+    part_off, part_seed = up(part[:p1 + 1]), up(seeds[:p1])
+    S = 8 * world
+    out = None
+    for it in range(2):
+        ids, sl = ctx.tokenize(text[:b1], sent_off)
+        pb = make_pairs(ctx, sent_off, ids, sl, doc_off, part_off, part_seed, seq=512, dup=5,
+                        masking=True, short_seq_prob=0.1, masked_lm_ratio=0.15)
+        del ids, sl
+        sb = StreamBalancer(ctx, 8, 64, num_shards=S)
+        tm = {}
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        bb = sb.step(pb, timings=tm)
+        if it == 1:
+            out = {
+                'workload': 'C4-style exchange step beside the C2 headline: each rank\'s first '
+                            'partitions (~{} MB of text), seq 512, duplicate_factor 5, static '
+                            'masking, 64 bins of 8 tokens, StreamBalancer into {} shards'.format(
+                                args.exchange_bytes // 10 ** 6, S),
+                'backend': dist.get_backend() if world > 1 else None,
+                'text_bytes_per_rank_max': int(st_max(float(b1), world, dev)),
+                'rows': st_moved_sum(int(pb.n_pairs), world, dev),
+                'moved_rows': st_moved_sum(int(bb.moved_rows), world, dev),
+                'counts_allgather_and_plan_ms': st_max((tm['plan'] - tm['bin']) * 1e3, world, dev),
+                'exchange_ms': st_max((tm['exchange'] - tm['plan']) * 1e3, world, dev),
+                'balance_ms': st_max((tm['regroup'] - tm['start']) * 1e3, world, dev),
+                'num_shards': S,
+                'shard_counts_spread': int((sb.all_shard_counts.max(0) -
+                                            sb.all_shard_counts.min(0)).max()),
+                'note': 'moved_rows: rows received from other ranks (only the per-bin surplus over '
+                        'each rank\'s shard quota moves, balance.py); exchange_ms: the all-to-all-v '
+                        'of row metadata and the token / position / label columns; not part of '
+                        'value'}
+        del bb, pb, sb
+    return out
 
 
 def granted_cores():
@@ -648,6 +720,11 @@ def main():
                                                            'punkt_params.json'),
                     help='PunktParameters JSON for the trained-model segmentation line '
                          '(with_segmentation.trained); empty string skips it')
+    ap.add_argument('--exchange-bytes', type=int, default=3_000_000_000,
+                    help='c2 at N > 1: text per rank of the c4_exchange sub-line (one C4-style '
+                         'balance step over RCCL beside the headline)')
+    ap.add_argument('--no-exchange-line', dest='exchange_line', action='store_false',
+                    help='c2 at N > 1: skip the c4_exchange sub-line')
     ap.add_argument('--rng', choices=['replay', 'native'], default='replay',
                     help='replay: CPython MT19937 per partition, bit-exact with the reference; '
                          'native: Philox counter RNG, documents and pairs in parallel')
@@ -664,6 +741,7 @@ def main():
         args.batch_bytes = 25_000_000_000 if args.workload == 'c4' else 10_000_000_000
         if SHARE_DEVICE and args.gpus > 1:  # all ranks share one GPU's HBM in the rehearsal
             args.batch_bytes = min(args.batch_bytes, 2 << 30)
+    args.exchange_bytes = min(args.exchange_bytes, args.batch_bytes)
 
     if args.workload == 'c5' and args.gpus > 1:
         raise SystemExit('C5 is measured per replica (--gpus 1)')
@@ -923,6 +1001,10 @@ def main():
             seg['trained'] = timed_segmented(args, rank, world, ctx, dev,
                                              PunktParams.from_json(args.punkt_params))
             seg['trained']['punkt_params'] = os.path.relpath(args.punkt_params, REPO)
+    exch = None
+    if world > 1 and args.workload == 'c2' and args.exchange_line:
+        torch.cuda.empty_cache()
+        exch = c4_exchange(args, ctx, dev, corp, part, seeds, text, world)
     mem = torch.cuda.memory_stats()
     if rank != 0:
         dist.destroy_process_group()
@@ -1090,6 +1172,8 @@ def main():
                                   'shard quota moves, balance.py)'}
     if alt is not None:
         res['alt_rng'] = alt
+    if exch is not None:
+        res['c4_exchange'] = exch
     if seg is not None:
         res['with_segmentation'] = seg
     if pcie_line is not None:

@@ -262,6 +262,13 @@ struct Pcs {
   __device__ int32_t get(int q) const { return b[64 * q]; }
 };
 
+// The pieces of one hard unit in the split tokenizer: its row of the hard-piece table.
+template <typename P>
+struct GPcs {
+  P* b;
+  __device__ void put(int n, int32_t v) { b[n] = (P)v; }
+};
+
 // Diagnostic build: work counters of phase B (per lane; summed at the kernel's end).
 struct TokStats {
 #ifdef LDDL_STAMPS
@@ -320,43 +327,27 @@ __device__ inline int32_t probe_finish(const Tables& T, const B32& a, int len, P
 }
 
 // Bloom candidates for the pieces starting at a's first byte: bit L-1 set iff the filter may
-// contain (cont, bytes[0, L)), L = 1 .. maxl (<= 32). LDDL_BLOOM_GROUP > 1 reads the filter words
-// of that many lengths before testing any (A/B: 2 -> 19.31 ms per 2 GB, 4 -> 21.1 and 8 -> 22.9
-// against 19.32 with 1; profiles/r05i_tok_variants.txt): the grouped reads cost registers and
-// the kernel spills, and the round trip they hide is not what it waits on.
-#ifndef LDDL_BLOOM_GROUP
-#define LDDL_BLOOM_GROUP 1
-#endif
-constexpr int kBloomGroup = LDDL_BLOOM_GROUP;
+// contain (cont, bytes[0, L)), L = 1 .. maxl (<= 32). (Round 5 read the filter words of 2 / 4 / 8
+// lengths before testing any: 19.31 / 21.1 / 22.9 ms per 2 GB against 19.32, the grouped reads
+// cost registers; profiles/r05i_tok_variants.txt, code on branch ab/tok-cp-variants.)
 __device__ inline uint32_t bloom_candidates32(const uint32_t* bloom, const B32& a, int maxl,
                                               uint32_t cont, TokStats* ts = nullptr) {
   uint32_t h = 0, cand = 0;
-  // lengths in groups of kBloomGroup: a group's filter words are all read before any is used,
-  // so the wave waits on one LDS round trip per group, not per length (round 4 waited on each
-  // length's read before computing the next: a dependent LDS latency per length)
 #pragma unroll
-  for (int L0 = 1; L0 <= 32; L0 += kBloomGroup) {
+  for (int L = 1; L <= 32; ++L) {
     // wave-uniform exit (lanes past their own maxl compute don't-care bits, masked below): no
     // exec-mask bookkeeping per length
-    if (!ballot(L0 <= maxl)) break;
-    uint32_t wrd[kBloomGroup], msk[kBloomGroup];
-#pragma unroll
-    for (int q = 0; q < kBloomGroup; ++q) {
-      const int L = L0 + q;
-      if (ts) {
-        ts->wave(4);
-        ts->add(5, L <= maxl);
-      }
-      const uint64_t wv = L <= 8 ? a.w0 : L <= 16 ? a.w1 : L <= 24 ? a.w2 : a.w3;
-      const uint32_t byte = (uint32_t)(wv >> (8 * ((L - 1) & 7))) & 0xFFu;
-      h = h * kBloomP + byte + 1u;
-      const uint32_t x = bloom_mix(h, (uint32_t)L, cont);
-      msk[q] = bloom_bits(x);
-      wrd[q] = bloom[bloom_word(x)];
+    if (!ballot(L <= maxl)) break;
+    if (ts) {
+      ts->wave(4);
+      ts->add(5, L <= maxl);
     }
-#pragma unroll
-    for (int q = 0; q < kBloomGroup; ++q)
-      cand |= (wrd[q] & msk[q]) == msk[q] ? 1u << (L0 + q - 1) : 0u;
+    const uint64_t wv = L <= 8 ? a.w0 : L <= 16 ? a.w1 : L <= 24 ? a.w2 : a.w3;
+    const uint32_t byte = (uint32_t)(wv >> (8 * ((L - 1) & 7))) & 0xFFu;
+    h = h * kBloomP + byte + 1u;
+    const uint32_t x = bloom_mix(h, (uint32_t)L, cont);
+    const uint32_t msk = bloom_bits(x);
+    cand |= (bloom[bloom_word(x)] & msk) == msk ? 1u << (L - 1) : 0u;
   }
   return maxl >= 32 ? cand : cand & ((1u << maxl) - 1u);
 }
@@ -415,8 +406,9 @@ __device__ inline int32_t piece_step(const Tables& T, const uint32_t* bloom, con
 // all bits for ASCII). Returns the piece count written to pc, or -1 if more than kPcs pieces.
 // (Round 3 probed the full length alone first, then two candidates per round trip: 21.9 ms per
 // 2 GiB against 20.7 now; three candidates per trip spilled VGPRs and took 22.1 ms, r04o.)
+template <typename Sink>  // Pcs (an LDS column) or GPcs (a global row)
 __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v, int nb,
-                           uint64_t ends, Pcs& pc, bool first_probe_missed = false,
+                           uint64_t ends, Sink& pc, bool first_probe_missed = false,
                            TokStats* ts = nullptr) {
   int n = 0, start = 0;
   while (start < nb) {
@@ -668,8 +660,8 @@ struct UnitWord {
 };
 
 // unit_word's generic (non-ASCII) normalisation without an LDS row: the normalised bytes are
-// appended straight into the four registers of the word (rare path; kCP's phase B, whose lanes
-// normalise at different times and so cannot share the piece columns as row space).
+// appended straight into the four registers of the word (the split tokenizer's hard-unit kernel,
+// whose lanes have no LDS row of their own).
 __device__ inline void put_byte32(B32& v, int pos, uint32_t b) {
   const uint64_t x = (uint64_t)(b & 0xFFu) << (8 * (pos & 7));
   const int q = pos >> 3;
@@ -866,6 +858,23 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
 // kept a ring of in-flight sentences; its per-window bookkeeping was ~half of the kernel's
 // instructions (profiles/r03l_pmc_tokenizer_variants.txt).
 // ---------------------------------------------------------------------------------------------
+//
+// Split form (LDDL_TOKENIZE_PATH=split): the same streaming kernel resolves phase A only and
+// leaves phase B and placement to two more launches (phase B kept 43 % of its
+// lanes busy per piece-step inside the streaming kernel, whose 146 KB of LDS per workgroup held
+// it at 4 waves per SIMD):
+//   tokenize_batch_kernel<true>  per chunk, the units' phase-A results in queue order as a
+//                  compact unit stream over the chunk's own region of `ids` (ids[A + i] for the
+//                  chunk's i-th unit: the piece id | kUCs, or kUHard | h) and each sentence's unit
+//                  count in sent_len; a hard unit's record (text offset, length, flags) goes to a
+//                  global list, claimed kHBlk entries at a time per wave.
+//   tokenize_hard_kernel         greedy longest match of every listed unit, one lane per unit, at
+//                  full occupancy (no classification state): its pieces to row h of the
+//                  hard-piece table, the count to hn[h].
+//   tokenize_place_kernel        per chunk, pieces per sentence (forward pass over the stream),
+//                  then the stream expanded in place from the back (see the kernel) to the final
+//                  ids[sent_off[s] + k] layout and sent_len.
+// ---------------------------------------------------------------------------------------------
 constexpr int kSF = 192;   // units resolved per pass (kSF / 64 phase-A rounds)
 // queue capacity: before a bank < kSF complete units; a bank adds <= 64 ends and leaves <= 65
 // units open (started, end not yet enqueued)
@@ -880,7 +889,8 @@ constexpr int32_t kHardBit = INT32_MIN;  // q_res: pieces are in column (res & 6
 constexpr int32_t kQPos = (1 << 28) - 1;
 constexpr int32_t kQSlow = INT32_MIN;
 constexpr int64_t kMaxSpan = 1 << 28;  // longer chunks go to the lane kernel
-// r_cnt: pieces so far (bits 0..28) | kRFb (the sentence goes to the lane kernel) | kLenHasClsSep
+// r_cnt: pieces (split: units) so far (bits 0..28) | kRFb (the sentence goes to the lane kernel)
+// | kLenHasClsSep
 constexpr int32_t kRFb = 1 << 29;
 constexpr int32_t kRCnt = kRFb - 1;
 static_assert(kLenHasClsSep == (1 << 30), "r_cnt flag layout");
@@ -901,14 +911,25 @@ struct alignas(16) StreamLds {
   alignas(16) int32_t pcs[kPcs * 64];
 };
 static_assert(kPcs * 64 * 4 >= 64 * kNorm, "normalised-word rows must fit the piece columns");
-// kCP: phase A's results go to the wave's global scratch, so only the unit queue and the chunk's
-// sentence tables stay in LDS (3.8 KB per wave instead of 7.0: two workgroups fit a CU)
-struct alignas(16) StreamLdsCP {
+
+// ---- split form ----
+// unit stream entry: an easy unit's piece id | kUCs (a literal [CLS] / [SEP]), or kUHard | h
+constexpr uint32_t kUHard = 1u << 31, kUCs = 1u << 30, kUId = kUCs - 1;
+// hard list entry (uint2): x = text offset bits 0..31; y = offset bits 32..39 | length << 8 |
+// kHSlow (normalise through the table) | kHMiss (phase A probed the whole word: not one piece) |
+// kHValid (entries a wave's block never filled have y = 0)
+constexpr uint32_t kHSlow = 1u << 16, kHMiss = 1u << 17, kHValid = 1u << 18;
+constexpr int kHBlk = 256;  // hard-list entries a wave claims at a time (one global atomic each)
+constexpr uint32_t kNoBlk = 0xFFFFFFFFu;
+constexpr int64_t kMaxTextBytes = 1ll << 40;  // text offsets of the hard list
+
+struct alignas(16) StreamLdsSplit {
   int32_t q_s[kQ];
   int32_t q_e[kQ];
-  int32_t trash[64];
+  uint8_t q_slot[kQ];
   int32_t s_off[kChunk + 1];
-  int32_t r_cnt[kChunk];
+  int32_t r_cnt[kChunk];  // units (bits 0..28) | kRFb
+  int32_t trash[64];      // target of the bank loop's lanes that store nothing
 };
 
 #ifdef LDDL_STAMPS
@@ -927,38 +948,19 @@ constexpr int kTokRegions = 6;  // 0 banks, 1 phase A, 2 phase B, 3 place, 4 que
   do {               \
   } while (0)
 #endif
-// Chunk-phased resolution (kCP): phase A still runs every kSF queued units, but its results go to
-// a per-wave global scratch (L2-resident) as one 32-bit record per unit, and the hard units to a
-// list there; phase B and placement run once per chunk (or when the scratch fills), phase B over
-// the whole chunk's hard units with lane refill: a lane that finishes its word takes the next one,
-// so the wave's piece-steps are not bounded by the longest word of each 64 (round 4: 43 % of the
-// lanes busy per piece-step, 1 phase-B pass per flush with ~48 hard units).
-// record: bits 0..20 piece id (easy; bit 21 literal [CLS]/[SEP]) or, with kRecHard, the hard-list
-// index (bits 0..12) and, once phase B is done, the piece count + 1 (bits 13..20; 0: the lane
-// kernel); bits 22..28 the unit's sentence slot in the chunk
-constexpr int kSpanCap = 8192;     // text bytes per (sub-)chunk in kCP mode (13-bit indices)
-constexpr int kRecCap = kSpanCap;  // unit records per sub-chunk (a unit has >= 1 byte)
-constexpr int kHardCap = kSpanCap;
-constexpr uint32_t kRecHard = 1u << 29, kRecCS = 1u << 21, kRecVal = (1u << 21) - 1;
-constexpr int kRecSlotShift = 22;
-static_assert(kChunk <= 128, "sentence slot: 7 bits of the record");
-// per-wave scratch (32-bit words): records, hard list (start, len | slow << 16 | known-miss << 17 |
-// record index << 18),
-// hard pieces [h * kPcs + q], hard piece counts (-1: the sentence goes to the lane kernel)
-constexpr int kScrRec = 0, kScrHl = kRecCap, kScrHp = kScrHl + 2 * kHardCap,
-              kScrHn = kScrHp + kPcs * kHardCap, kScrWords = kScrHn + kHardCap;
 
-template <bool kCP, int kW, int kWPE, int kCPRoundsInFlight = 3>  // kW waves per workgroup,
-// >= kWPE waves per SIMD; kCP: phase-A rounds of 64 units in flight together
+// kSplit: phase A only (the split form above), kRF phase-A rounds in flight; kW waves per
+// workgroup, >= kWPE waves per SIMD.
+template <bool kSplit, int kW, int kWPE, int kRF = 3>
 __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
     Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
     int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
     int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr,
-    uint32_t* __restrict__ scratch) {
+    uint2* __restrict__ hlist, uint32_t* __restrict__ hctr, uint32_t hcap) {
   __shared__ uint32_t s_ascii[128];
   __shared__ uint8_t s_cls[256];
-  __shared__ uint32_t s_bloom[kBloomWords];
-  using WL = std::conditional_t<kCP, StreamLdsCP, StreamLds>;
+  __shared__ uint32_t s_bloom[kSplit ? 1 : kBloomWords];
+  using WL = std::conditional_t<kSplit, StreamLdsSplit, StreamLds>;
   __shared__ WL s_w[kW];
 #ifdef LDDL_STAMPS
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
@@ -979,22 +981,20 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
     }
     s_cls[c] = (uint8_t)v;
   }
-  for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
+  if constexpr (!kSplit)
+    for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
   __syncthreads();
   const int lane = lane_id();
   WL& W = s_w[threadIdx.x >> 6];
   // target of the bank loop's lanes that store nothing (no exec-mask branch): the piece columns,
-  // unused outside a flush (kCP: a trash row of its own)
+  // unused outside a flush (split: a trash row of its own)
   int32_t* const trashp = [&]() -> int32_t* {
-    if constexpr (kCP) return &W.trash[lane_id()];
+    if constexpr (kSplit) return &W.trash[lane_id()];
     else return &W.pcs[lane_id()];
   }();
-  uint32_t* __restrict__ wscr =
-      kCP ? scratch + ((int64_t)blockIdx.x * kW + (threadIdx.x >> 6)) * kScrWords : nullptr;
-  uint32_t* __restrict__ s_rec = wscr + kScrRec;
-  int2* __restrict__ s_hl = reinterpret_cast<int2*>(wscr + kScrHl);
-  int32_t* __restrict__ s_hp = reinterpret_cast<int32_t*>(wscr + kScrHp);
-  int32_t* __restrict__ s_hn = reinterpret_cast<int32_t*>(wscr + kScrHn);
+  // split: the wave's current block of the hard list [hbase, hbase + kHBlk), hused taken
+  uint32_t hbase = kNoBlk;
+  int hused = kHBlk;
   // sentence indices fit int32 (lddl_tokenize: n_sent < INT32_MAX - 2^22)
   const int32_t n_sent32 = (int32_t)n_sent;
   // Chunks: wave w starts with chunk w, then takes the next unclaimed chunk from chunk_ctr
@@ -1008,32 +1008,14 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
   const uint64_t upto = (2ull << lane) - 1;  // lanes <= this one (lane 63: all)
 
   while (c0 < n_sent32) {
-   const int32_t cend = n_sent32 - c0 < kChunk ? n_sent32 : c0 + kChunk;
-   // kCP: the claimed chunk is processed in sub-chunks of at most kSpanCap bytes (so that its units,
-   // hence its records and hard units, fit the wave's scratch: a unit has >= 1 byte); a sentence
-   // longer than that alone goes to the lane kernel
-   for (int32_t cb = c0; cb < cend;) {
-    int32_t n = cend - cb;
-    if constexpr (kCP) {
-      const int64_t a0 = sent_off[cb];
-      int32_t fit = 0;
-      for (int j0 = 0; j0 < n; j0 += 64) {
-        const int j = j0 + lane;
-        fit += __popcll(ballot(j < n && sent_off[cb + j + 1] - a0 <= (int64_t)kSpanCap));
-      }
-      if (fit == 0) {  // one sentence of more than kSpanCap bytes
-        if (lane == 0) fb_list[atomicAdd(fb_n, 1u)] = cb;
-        cb += 1;
-        continue;
-      }
-      n = fit;
-    }
-    const int32_t c0 = cb;  // (this sub-chunk's first sentence)
-    cb += n;
+    const int32_t n = n_sent32 - c0 < kChunk ? n_sent32 - c0 : kChunk;
     const int64_t A = sent_off[c0];
     const int64_t span64 = sent_off[c0 + n] - A;
     if (span64 >= kMaxSpan) {  // pathological chunk (>= 256 MiB of text): the lane kernel
-      for (int j = lane; j < n; j += 64) fb_list[atomicAdd(fb_n, 1u)] = c0 + j;
+      for (int j = lane; j < n; j += 64) {
+        if constexpr (kSplit) sent_len[c0 + j] = kRFb;  // (the placement kernel lists it)
+        else fb_list[atomicAdd(fb_n, 1u)] = c0 + j;
+      }
     } else {
       for (int j = lane; j <= n; j += 64) W.s_off[j] = (int32_t)(sent_off[c0 + j] - A);
       for (int j = lane; j < n; j += 64) W.r_cnt[j] = 0;
@@ -1053,9 +1035,32 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         return j;
       };
 
+      int ns = 0, ne = 0;  // queued unit starts / ends
+      int32_t ucur = 0;    // split: units of this chunk streamed so far
+
+      // drop the processed units [0, m) from the queue: < 128 starts and < 128 ends remain
+      // (read all, then write)
+      auto drop = [&](int m) {
+        const int rs = ns - m, re = ne - m;
+        int32_t a0 = 0, a1 = 0, e0 = 0, e1 = 0;
+        uint8_t l0 = 0, l1 = 0;
+        if (lane < rs) a0 = W.q_s[m + lane], l0 = W.q_slot[m + lane];
+        if (lane + 64 < rs) a1 = W.q_s[m + 64 + lane], l1 = W.q_slot[m + 64 + lane];
+        if (lane < re) e0 = W.q_e[m + lane];
+        if (lane + 64 < re) e1 = W.q_e[m + 64 + lane];
+        wave_sync();
+        if (lane < rs) W.q_s[lane] = a0, W.q_slot[lane] = l0;
+        if (lane + 64 < rs) W.q_s[64 + lane] = a1, W.q_slot[64 + lane] = l1;
+        if (lane < re) W.q_e[lane] = e0;
+        if (lane + 64 < re) W.q_e[64 + lane] = e1;
+        wave_sync();
+        ns = rs;
+        ne = re;
+      };
+
       // place queue units [u0, u1) (all resolved) in order: segmented scan per sentence
       auto place = [&](int u0, int u1) {
-        if constexpr (!kCP) {
+        if constexpr (!kSplit) {
         for (int r0 = u0; r0 < u1; r0 += 64) {
           const int u = r0 + lane;
           const bool act = u < u1;
@@ -1092,11 +1097,9 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         }
       };
 
-      int ns = 0, ne = 0;  // queued unit starts / ends
-
       // resolve and place the complete units [0, m), then drop them from the queue
       auto flush = [&](int m) {
-        if constexpr (!kCP) {
+        if constexpr (!kSplit) {
         TOK_STAMP(0);
         // phase A: specials and single-piece words
         int nh = 0;
@@ -1202,205 +1205,46 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         }
         place(placed, m);
         TOK_STAMP(3);
-        // drop the processed units: < 128 starts and < 128 ends remain (read all, then write)
-        const int rs = ns - m, re = ne - m;
-        int32_t a0 = 0, a1 = 0, e0 = 0, e1 = 0;
-        uint8_t l0 = 0, l1 = 0;
-        if (lane < rs) a0 = W.q_s[m + lane], l0 = W.q_slot[m + lane];
-        if (lane + 64 < rs) a1 = W.q_s[m + 64 + lane], l1 = W.q_slot[m + 64 + lane];
-        if (lane < re) e0 = W.q_e[m + lane];
-        if (lane + 64 < re) e1 = W.q_e[m + 64 + lane];
-        wave_sync();
-        if (lane < rs) W.q_s[lane] = a0, W.q_slot[lane] = l0;
-        if (lane + 64 < rs) W.q_s[64 + lane] = a1, W.q_slot[64 + lane] = l1;
-        if (lane < re) W.q_e[lane] = e0;
-        if (lane + 64 < re) W.q_e[64 + lane] = e1;
-        wave_sync();
-        ns = rs;
-        ne = re;
+        drop(m);
         TOK_STAMP(4);
         }
       };
 
-      // ---- chunk-phased resolution (kCP) ----
-      int nrec = 0, nhard = 0;  // records / hard units of this sub-chunk in the scratch
-
-      // phase B over the scratch's hard units [0, nhard), lanes refilled from the list. Latency
-      // hiding: the list is read 64 entries at a time into a register window (a refilled lane
-      // takes its entry from the window by a lane shuffle), and a refilled lane's text load is
-      // issued at the end of one iteration and consumed at the end of the next, so it overlaps
-      // the busy lanes' probes instead of adding a round trip to each iteration. Finished units
-      // write their piece count into their record (placement then reads records only).
-      auto phase_b_cp = [&]() {
-        enum { kIdle = 0, kLoading = 1, kBusy = 2 };
-        int state = kIdle, h = -1, nb = 0, start = 0, np = 0, hlen = 0;
-        uint32_t hflags = 0;
-        B32 v{0, 0, 0, 0};
-        uint64_t ends = 0;
-        int nextu = 0;  // wave-uniform: the next unassigned hard unit
-        int wbase = 0;  // wave-uniform: the window holds entries [wbase, wbase + 64)
-        int2 win = lane < nhard ? s_hl[lane] : make_int2(0, 0);
-        auto finish = [&](int npc) {
-          const int ri = (int)(hflags >> 18);  // the unit's record index
-          s_rec[ri] = (s_rec[ri] & ~kRecVal) | (uint32_t)h | ((uint32_t)(npc + 1) << 13);
-          state = kIdle;
-          h = -1;
-        };
-        auto refill = [&]() {
-          const bool want = state == kIdle;
-          const uint64_t Wm = ballot(want);
-          const int room = wbase + 64 - nextu;  // window entries not yet taken
-          const int take = __popcll(Wm) < room ? __popcll(Wm) : room;
-          const int k = (int)popc_below(Wm);
-          const int cand = nextu + k;
-          const int src = (nextu - wbase + k) & 63;
-          const int2 he = make_int2(__shfl(win.x, src, 64), __shfl(win.y, src, 64));
-          if (want && k < take && cand < nhard) {
-            h = cand;
-            hlen = he.y & 0xFFFF;
-            hflags = (uint32_t)he.y & 0xFFFF0000u;
-            const int st = he.x;
-            const bool slow = (he.y >> 16) & 1;
-            if (!slow && hlen <= 32 && T.ascii_mode != 0) {
-              v = load32(text, n_bytes, A + st);  // consumed at the end of the next iteration
-              state = kLoading;
-            } else {  // normalised now, into registers (rare)
-              const UnitWord uw = unit_word_reg(T, s_ascii, text, A + st, hlen);
-              if (uw.status != 0) {  // empty (every char dropped) or too long
-                finish(uw.status > 0 ? 0 : -1);
-              } else {
-                v = uw.v;
-                nb = uw.nb;
-                ends = uw.ends;
-                start = 0;
-                np = 0;
-                state = kBusy;
-              }
-            }
-          }
-          nextu = nextu + take < nhard ? nextu + take : nhard;
-          if (nextu == wbase + 64 && nextu < nhard) {  // the next window
-            wbase = nextu;
-            win = wbase + lane < nhard ? s_hl[wbase + lane] : make_int2(0, 0);
-          }
-        };
-        refill();
-        while (ballot(state != kIdle) || nextu < nhard) {
-          if (state == kBusy) {
-            if (tsp) {
-              tsp->wave(2);
-              tsp->add(3, 1);
-            }
-            int len;
-            const int32_t id = piece_step(T, s_bloom, v, nb, ends, start, ((hflags >> 17) & 1) != 0, len, tsp);
-            if (id < 0) {  // no piece: the whole word is [UNK]
-              s_hp[h * kPcs] = T.special_id[kUnk];
-              finish(1);
-            } else if (np == kPcs) {  // too many pieces: the sentence goes to the lane kernel
-              finish(-1);
-            } else {
-              s_hp[h * kPcs + np] = id;
-              ++np;
-              start += len;
-              if (start >= nb) finish(np);
-            }
-          } else if (state == kLoading) {  // its text (loaded last iteration) is in v
-            if (T.ascii_mode == 1) v = B32{swar_lower(v.w0), swar_lower(v.w1), swar_lower(v.w2), swar_lower(v.w3)};
-            nb = hlen;
-            ends = ~0ull;
-            start = 0;
-            np = 0;
-            state = kBusy;
-          }
-          refill();
-        }
-      };
-
-      // place the scratch's records [0, nrec) in order (segmented scan per sentence slot); a hard
-      // unit's record holds its hard index and (piece count + 1) << 13 (0: the lane kernel)
-      auto place_cp = [&]() {
-        uint32_t nxt = lane < nrec ? s_rec[lane] : 0u;
-        for (int r0 = 0; r0 < nrec; r0 += 64) {
-          const int u = r0 + lane;
-          const bool act = u < nrec;
-          const uint32_t rec = nxt;
-          nxt = u + 64 < nrec ? s_rec[u + 64] : 0u;  // next group's records in flight
-          const bool hard = (rec & kRecHard) != 0;
-          const int hv = hard ? (int)(rec & 0x1FFF) : (int)(rec & kRecVal);
-          int npc = act ? (hard ? (int)((rec >> 13) & 0xFF) - 1 : 1) : 0;
-          const int slot = act ? (int)((rec >> kRecSlotShift) & 127u) : -1;
-          if (npc < 0) {  // the sentence goes to the lane kernel
-            atomicOr(&W.r_cnt[slot], kRFb);
-            npc = 0;
-          }
-          const int incl = wave_incl_scan(npc);
-          const int excl = incl - npc;
-          const int prev_slot = wave_prev(slot);
-          const uint64_t F = ballot(act && (lane == 0 || slot != prev_slot));
-          const int s0 = 63 - __clzll(F & upto);
-          const int seg_excl = excl - __shfl(excl, s0, 64);
-          const int next_slot = wave_next(slot);
-          const bool seg_last = act && (lane == 63 || u + 1 >= nrec || next_slot != slot);
-          if (act) {
-            const int o = (W.r_cnt[slot] & kRCnt) + seg_excl;
-            const int64_t bb = A + W.s_off[slot];
-            if (hard) {
-              for (int q = 0; q < npc; ++q)
-                if (o + q < max_pieces) ids[bb + o + q] = s_hp[hv * kPcs + q];
-            } else if (o < max_pieces) {
-              ids[bb + o] = hv;
-              if (rec & kRecCS) atomicOr(&W.r_cnt[slot], kLenHasClsSep);
-            }
-          }
-          wave_sync();
-          if (seg_last) W.r_cnt[slot] += seg_excl + npc;  // (count bits only: < 2^28 pieces)
-          wave_sync();
-        }
-      };
-
-      auto chunk_flush_cp = [&]() {
-        TOK_STAMP(0);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        phase_b_cp();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        TOK_STAMP(2);
-        place_cp();
-        TOK_STAMP(3);
-        nrec = nhard = 0;
-      };
-
-      // phase A of the queued units [0, m): a record per unit, hard units to the list; then drop
-      // them from the queue
-      auto flush_cp = [&](int m) {
-        TOK_STAMP(0);
-        // kRF rounds of 64 units in flight at a time (all their text loads, then all their first
-        // table loads, then the checks); fewer rounds in flight hold fewer registers
+      // split: phase A of the queued units [0, m), their stream entries and hard-list records,
+      // the sentences' unit counts; then drop them from the queue
+      auto flush_split = [&](int m) {
+        if constexpr (kSplit) {
         constexpr int kR = kSF / 64;
-        constexpr int kRF = kCPRoundsInFlight;
-        static_assert(kR % kRF == 0, "phase A rounds");
-#pragma unroll 1
+        static_assert(kR % kRF == 0, "phase A rounds in flight");
+        int32_t* __restrict__ stream = ids + A + ucur;
+        int slots[kR];
+        // kRF rounds of 64 units in flight at a time (their text loads, then their first table
+        // loads, then the checks): fewer rounds in flight hold fewer registers
+#pragma unroll
         for (int r0 = 0; r0 < kR; r0 += kRF) {
           bool elig[kRF], hardr[kRF];
-          int lenr[kRF], str[kRF];  // lenr: length | sentence slot << 16 | slow << 23
-          int32_t resr[kRF];        // id | kRecCS
+          int lenr[kRF];
+          int32_t qsr[kRF];
+          uint32_t resr[kRF];
           B32 vv[kRF];
           Probe pr[kRF];
 #pragma unroll
           for (int r = 0; r < kRF; ++r) {
             const int u = 64 * (r0 + r) + lane;
             elig[r] = hardr[r] = false;
-            lenr[r] = str[r] = 0;
+            lenr[r] = 0;
             resr[r] = 0;
+            qsr[r] = 0;
+            slots[r0 + r] = -1;
             if (u < m) {
               const int32_t qs = W.q_s[u];
-              const int st = qs & 0xFFFF, kind = (qs >> 28) & 7;
+              const int st = qs & kQPos, kind = (qs >> 28) & 7;
               const int len = W.q_e[u] - st + 1;
-              lenr[r] = len | (qs & 0x7F0000) | (qs < 0 ? 1 << 23 : 0);  // slot from the bank loop
-              str[r] = st;
+              qsr[r] = qs;
+              lenr[r] = len;
+              slots[r0 + r] = W.q_slot[u];
               if (kind >= 2) {
-                resr[r] = T.special_id[kind - 2] | ((kind - 2 == kCls || kind - 2 == kSep) ? (int32_t)kRecCS : 0);
+                resr[r] = (uint32_t)T.special_id[kind - 2] | (kind - 2 == kCls || kind - 2 == kSep ? kUCs : 0u);
               } else if (qs >= 0 && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32) {
                 elig[r] = true;
                 vv[r] = load32(text, n_bytes, A + st);
@@ -1414,46 +1258,69 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
             if (elig[r]) {
               if (T.ascii_mode == 1)
                 vv[r] = B32{swar_lower(vv[r].w0), swar_lower(vv[r].w1), swar_lower(vv[r].w2), swar_lower(vv[r].w3)};
-              pr[r] = probe_first(T, vv[r], lenr[r] & 0xFFFF, 0);
+              pr[r] = probe_first(T, vv[r], lenr[r], 0);
             }
 #pragma unroll
           for (int r = 0; r < kRF; ++r) {
             bool km = false;
             if (elig[r]) {
-              resr[r] = probe_finish(T, vv[r], lenr[r] & 0xFFFF, pr[r]);
-              hardr[r] = km = resr[r] < 0;
+              const int32_t id = probe_finish(T, vv[r], lenr[r], pr[r]);
+              resr[r] = (uint32_t)id;
+              hardr[r] = km = id < 0;
             }
             const int u = 64 * (r0 + r) + lane;
-            const uint64_t H = ballot(hardr[r]);
-            const int hidx = nhard + (int)popc_below(H);
-            if (u < m) {
-              const uint32_t slotb = (uint32_t)((lenr[r] >> 16) & 127) << kRecSlotShift;
-              s_rec[nrec + u] = hardr[r] ? (kRecHard | (uint32_t)hidx | slotb) : ((uint32_t)resr[r] | slotb);
+            const bool act = u < m;
+            const bool slow = qsr[r] < 0;
+            // units the hard kernel does not take send their sentence to the lane kernel: ASCII
+            // words of > 32 bytes (their normalised form is as long) and > 255 bytes of anything
+            bool fb = hardr[r] && (slow ? lenr[r] > 255 : lenr[r] > 32);
+            const bool hk = hardr[r] && !fb;
+            const uint64_t Hm = ballot(hk);
+            const int nh = __popcll(Hm);
+            if (nh && hused + nh > kHBlk) {  // a new block (wave-uniform)
+              if (hbase != kNoBlk)  // the rest of the old one: entries the hard kernel skips
+                for (int t = hused + lane; t < kHBlk; t += 64) hlist[hbase + t] = make_uint2(0u, 0u);
+              uint32_t nb = 0;
+              if (lane == 0) nb = atomicAdd(hctr, (uint32_t)kHBlk);
+              nb = __builtin_amdgcn_readfirstlane(nb);
+              // past the list's capacity: no block (the host sees the count and runs again with a
+              // list that holds it; meanwhile these units go to the lane kernel)
+              hbase = (uint64_t)nb + kHBlk <= (uint64_t)hcap ? nb : kNoBlk;
+              hused = 0;
             }
-            if (hardr[r])  // start, len | slow << 16 | known miss << 17 | record index << 18
-              s_hl[hidx] = make_int2(str[r], (lenr[r] & 0xFFFF) | ((lenr[r] >> 23) & 1) << 16 |
-                                                 (km ? 1 << 17 : 0) | (nrec + u) << 18);
-            nhard += __popcll(H);
+            const bool have = hbase != kNoBlk;
+            if (act) {
+              uint32_t val = resr[r];
+              if (hk && have) {
+                const uint32_t h = hbase + (uint32_t)hused + popc_below(Hm);
+                const int64_t pos = A + (qsr[r] & kQPos);
+                hlist[h] = make_uint2((uint32_t)pos, (uint32_t)(pos >> 32) | (uint32_t)lenr[r] << 8 |
+                                                         (slow ? kHSlow : 0u) | (km ? kHMiss : 0u) | kHValid);
+                val = kUHard | h;
+              }
+              fb |= hk && !have;
+              stream[u] = (int32_t)val;
+              if (fb) atomicOr(&W.r_cnt[slots[r0 + r]], kRFb);
+            }
+            if (have) hused += nh;
           }
         }
-        nrec += m;
-        TOK_STAMP(1);
-        // drop the processed units: < 128 starts and < 128 ends remain (read all, then write)
-        const int rs = ns - m, re = ne - m;
-        int32_t a0 = 0, a1 = 0, e0 = 0, e1 = 0;
-        if (lane < rs) a0 = W.q_s[m + lane];
-        if (lane + 64 < rs) a1 = W.q_s[m + 64 + lane];
-        if (lane < re) e0 = W.q_e[m + lane];
-        if (lane + 64 < re) e1 = W.q_e[m + 64 + lane];
         wave_sync();
-        if (lane < rs) W.q_s[lane] = a0;
-        if (lane + 64 < rs) W.q_s[64 + lane] = a1;
-        if (lane < re) W.q_e[lane] = e0;
-        if (lane + 64 < re) W.q_e[64 + lane] = e1;
+        // units per sentence: segmented counts of the slots (non-decreasing in queue order)
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+          const int u = 64 * r + lane;
+          const bool act = u < m;
+          const int slot = slots[r];
+          const uint64_t F = ballot(act && (lane == 0 || slot != wave_prev(slot)));
+          const bool last = act && (lane == 63 || u + 1 >= m || wave_next(slot) != slot);
+          const int s0 = 63 - __clzll(F & upto);
+          if (last) atomicAdd(&W.r_cnt[slot], lane - s0 + 1);
+        }
         wave_sync();
-        ns = rs;
-        ne = re;
-        TOK_STAMP(4);
+        ucur += m;
+        drop(m);
+        }
       };
 
       // ---- the chunk's banks ----
@@ -1467,28 +1334,17 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
       int32_t jn = 1;  // the next sentence start to mark
       uint32_t nextS = (uint32_t)__builtin_amdgcn_readfirstlane(W.s_off[1]);
       const uint32_t last = span ? span - 1 : 0;
-      // software prefetch three banks ahead (clamped into the chunk; bytes past it are unused);
-      // with LDDL_TOK_CLS_AHEAD the fast-path class of the next bank's byte is also looked up one
-      // bank ahead (measured neutral: the class read's wait is not on the critical path)
+      // software prefetch three banks ahead (clamped into the chunk; bytes past it are unused)
       uint32_t cur = 0x20u, pf1 = 0x20u, pf2 = 0x20u;
       if (span) {
         cur = ctext[(uint32_t)lane < last ? (uint32_t)lane : last];
         pf1 = ctext[64u + lane < last ? 64u + lane : last];
         pf2 = ctext[128u + lane < last ? 128u + lane : last];
       }
-#ifndef LDDL_TOK_CLS_AHEAD  // 1: the class read a bank ahead (A/B: 19.31 vs 19.32 ms, r05i)
-#define LDDL_TOK_CLS_AHEAD 0
-#endif
-      uint32_t vcur = s_cls[cur];
       uint32_t x0 = 0;
       for (; x0 < span; x0 += 64) {
         const uint32_t byte = cur;
-#if LDDL_TOK_CLS_AHEAD
-        const uint32_t v = vcur;
-        vcur = s_cls[pf1];  // the next bank's (its byte was loaded two banks ago)
-#else
         const uint32_t v = s_cls[byte];
-#endif
         cur = pf1;
         pf1 = pf2;
         {
@@ -1499,7 +1355,7 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         const bool in = x < span;
         uint64_t BRK = 0;
         // this lane's sentence slot (the last sentence starting at or before byte x, as sent_of),
-        // stored with its unit start so that placement (kCP: phase A) needs no search
+        // stored with its unit start so that placement needs no search
         int32_t lslot = jn - 1;
         while (nextS < x0 + 64) {
           BRK |= 1ull << (nextS - x0);
@@ -1509,8 +1365,8 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         }
         const uint64_t VALID = ballot(in);
         uint64_t RUN, UNIT, CONT, SL = 0;
-        // unit start: chunk-relative byte | kind << 28 (| slot << 16 in kCP: x < kSpanCap)
-        int32_t sval = kCP ? (int32_t)(x | (uint32_t)lslot << 16) : (int32_t)x;
+        // unit start: chunk-relative byte | kind << 28
+        int32_t sval = (int32_t)x;
         if (!(ballot(v >= kFSlow) | insc | k1 | k2 | k3)) {  // plain ASCII bank
           RUN = ballot(v == kFRun) & VALID;
           UNIT = VALID & ~ballot(v == kFSep);
@@ -1564,8 +1420,7 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
           const uint64_t ISO = ballot(cat == kCatIso), LEAD = ballot(cplen > 0);
           UNIT = ballot(cat != kCatSep);
           CONT = (RUN & ((RUN << 1) | cin) & ~BRK) | (ISO & ~LEAD) | inside;
-          sval = (int32_t)(x | ((uint32_t)(spk >= 0 ? 2 + spk : 0) << 28) |
-                           (kCP ? (uint32_t)lslot << 16 : 0u));
+          sval = (int32_t)(x | ((uint32_t)(spk >= 0 ? 2 + spk : 0) << 28));
           SL = ballot(slow && cat != kCatSep);
           k1 = (V2 | V3 | V4) >> 63;
           k2 = (V3 | V4) >> 62;
@@ -1582,10 +1437,9 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
           const bool st_here = (US >> lane) & 1ull;
           int32_t* dst = st_here ? &W.q_s[r] : trashp;
           *dst = sval;
-          if constexpr (!kCP) {  // the unit's sentence slot (placement needs no search)
-            uint8_t* sd = st_here ? &W.q_slot[r] : reinterpret_cast<uint8_t*>(trashp);
-            *sd = (uint8_t)lslot;
-          }
+          // the unit's sentence slot (placement needs no search)
+          uint8_t* sd = st_here ? &W.q_slot[r] : reinterpret_cast<uint8_t*>(trashp);
+          *sd = (uint8_t)lslot;
         }
         if (SL) {  // slow bytes flag their unit (started in this bank or before)
           if ((SL >> lane) & 1ull) atomicOr(&W.q_s[ns + (int)__popcll(US & upto) - 1], kQSlow);
@@ -1604,7 +1458,7 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         CONTp = CONT;
         if (ne >= kSF) {
           wave_sync();
-          if constexpr (kCP) flush_cp(kSF);
+          if constexpr (kSplit) flush_split(kSF);
           else flush(kSF);
         }
       }
@@ -1617,16 +1471,16 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
       }
       wave_sync();
       TOK_STAMP(0);
-      if constexpr (kCP) {
-        while (ne > 0) flush_cp(ne < kSF ? ne : kSF);
-        chunk_flush_cp();
-      } else {
-        while (ne > 0) flush(ne < kSF ? ne : kSF);
+      while (ne > 0) {
+        if constexpr (kSplit) flush_split(ne < kSF ? ne : kSF);
+        else flush(ne < kSF ? ne : kSF);
       }
       // the chunk's sentences
       for (int j = lane; j < n; j += 64) {
         const int32_t rc = W.r_cnt[j];
-        if (rc & kRFb) {
+        if constexpr (kSplit) {
+          sent_len[c0 + j] = rc;  // units | kRFb: the placement kernel's input
+        } else if (rc & kRFb) {
           fb_list[atomicAdd(fb_n, 1u)] = c0 + j;
         } else {
           const int32_t cnt = rc & kRCnt;
@@ -1635,12 +1489,15 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
       }
       wave_sync();  // before the next chunk reuses s_off / r_cnt
     }
-   }
     TOK_STAMP(5);
     int32_t nc = 0;
     if (lane == 0) nc = atomicAdd(chunk_ctr, kChunk);
     nc = __builtin_amdgcn_readfirstlane(nc);
     c0 = nc < n_sent32 ? nc : n_sent32;
+  }
+  if constexpr (kSplit) {  // the rest of the wave's last block: entries the hard kernel skips
+    if (hbase != kNoBlk)
+      for (int t = hused + lane; t < kHBlk; t += 64) hlist[hbase + t] = make_uint2(0u, 0u);
   }
 #ifdef LDDL_STAMPS
   if (lane == 0 && g_tok_tl) {
@@ -1658,6 +1515,191 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
 #endif
 }
 
+// Split form, phase B: the greedy longest match of every unit of the hard list (one lane per
+// unit; the Bloom filter in LDS), pieces to hp[h * kPcs + q], their count to hn[h]. A count <= 0
+// sends the sentence to the lane kernel: -1 for more than kPcs pieces or a normalised word of
+// more than kNorm bytes, and a unit whose every character the normaliser drops (0 pieces) too,
+// because the in-place placement relies on >= 1 piece per unit.
+// (tuning knobs of the split form, set while it is measured; fixed once chosen)
+#ifndef LDDL_HARD_BLOCK
+#define LDDL_HARD_BLOCK 256
+#endif
+#ifndef LDDL_HARD_WPE
+#define LDDL_HARD_WPE 1
+#endif
+#ifndef LDDL_SPLIT_SW
+#define LDDL_SPLIT_SW 8
+#endif
+#ifndef LDDL_SPLIT_WPE
+#define LDDL_SPLIT_WPE 4
+#endif
+#ifndef LDDL_SPLIT_RF
+#define LDDL_SPLIT_RF 3
+#endif
+constexpr int kHardBlock = LDDL_HARD_BLOCK;
+template <typename P>
+__global__ void __launch_bounds__(kHardBlock, LDDL_HARD_WPE) tokenize_hard_kernel(
+    Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const uint2* __restrict__ hlist,
+    const uint32_t* __restrict__ hctr, uint32_t hcap, P* __restrict__ hp, int8_t* __restrict__ hn) {
+  __shared__ uint32_t s_ascii[128];
+  __shared__ uint32_t s_bloom[kBloomWords];
+  for (int c = threadIdx.x; c < 128; c += blockDim.x) s_ascii[c] = tab_entry(T, (uint32_t)c);
+  for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
+  __syncthreads();
+  const uint32_t nh = *hctr < hcap ? *hctr : hcap;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += stride) {
+    const uint2 e = hlist[h];
+    if (!(e.y & kHValid)) continue;
+    const int64_t pos = (int64_t)e.x | ((int64_t)(e.y & 0xFFu) << 32);
+    const int len = (int)((e.y >> 8) & 0xFFu);
+    UnitWord uw;
+    if (!(e.y & kHSlow) && T.ascii_mode != 0 && len <= 32) {
+      B32 v = load32(text, n_bytes, pos);
+      if (T.ascii_mode == 1) v = B32{swar_lower(v.w0), swar_lower(v.w1), swar_lower(v.w2), swar_lower(v.w3)};
+      uw.v = v;
+      uw.nb = len;
+      uw.ends = ~0ull;
+      uw.status = 0;
+    } else {
+      uw = unit_word_reg(T, s_ascii, text, pos, len);
+    }
+    int npc = -1;
+    if (uw.status == 0) {
+      GPcs<P> pc{hp + (int64_t)h * kPcs};
+      npc = wordpiece32(T, s_bloom, uw.v, uw.nb, uw.ends, pc, (e.y & kHMiss) != 0);
+    }
+    hn[h] = (int8_t)(npc > 0 ? npc : -1);
+  }
+}
+
+// Split form, placement: one wave per chunk of kChunk sentences (the streaming kernel's chunks).
+// sent_len holds each sentence's unit count (| kRFb); the chunk's unit stream is ids[A + i],
+// A = sent_off[c0]. Pass 1 (forward) sums each sentence's pieces (1 per easy unit, hn[h] per hard
+// one). Pass 2 walks the stream from the back, 64 units at a time, and writes every unit's
+// pieces to ids[sent_off[s] + o] (o < max_pieces). In place, because no write reaches a stream
+// entry not yet read: unit i of sentence s (its j-th) is stream entry A + i with
+// i = (units of the sentences before s) + j <= (sent_off[s] - A) + j, and its pieces start at
+// sent_off[s] + o_i with o_i >= j (every unit has >= 1 piece: a unit with none sends its sentence
+// to the lane kernel), so a group's writes land at or after its own entries — read first, in
+// registers — and after every entry of the groups before it; the scans that place a group use all
+// its lanes' entries, so its stores issue after all of its loads have returned.
+template <typename P>
+__global__ void __launch_bounds__(256) tokenize_place_kernel(
+    const int64_t* __restrict__ sent_off, int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids,
+    int32_t* __restrict__ sent_len, const P* __restrict__ hp, const int8_t* __restrict__ hn,
+    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n) {
+  constexpr int kWv = 4;
+  __shared__ int32_t s_us[kWv][kChunk + 1];  // the sentences' first stream entries; [n] = units
+  __shared__ int32_t s_tot[kWv][kChunk];     // pieces | kRFb | kLenHasClsSep
+  __shared__ int32_t s_done[kWv][kChunk];    // pieces of the units already placed (pass 2)
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  int32_t* us = s_us[wv];
+  int32_t* tot = s_tot[wv];
+  int32_t* done = s_done[wv];
+  const uint64_t upto = (2ull << lane) - 1;
+  const uint64_t below = (1ull << lane) - 1;
+  const int64_t n_chunks = (n_sent + kChunk - 1) / kChunk;
+  for (int64_t c = (int64_t)blockIdx.x * kWv + wv; c < n_chunks; c += (int64_t)gridDim.x * kWv) {
+    const int64_t c0 = c * kChunk;
+    const int n = n_sent - c0 < kChunk ? (int)(n_sent - c0) : kChunk;
+    const int64_t A = sent_off[c0];
+    int32_t carry = 0;
+#pragma unroll
+    for (int j0 = 0; j0 < kChunk; j0 += 64) {
+      const int j = j0 + lane;
+      const int32_t r = j < n ? sent_len[c0 + j] : 0;
+      const int32_t cnt = r & kRCnt;
+      const int32_t incl = wave_incl_scan(cnt);
+      if (j < n) {
+        us[j] = carry + incl - cnt;
+        tot[j] = r & kRFb;
+        done[j] = 0;
+      }
+      carry += __builtin_amdgcn_readlane(incl, 63);
+    }
+    if (lane == 0) us[n] = carry;
+    wave_sync();
+    const int32_t nu = carry;
+    const int32_t* __restrict__ stream = ids + A;
+    auto sent_of = [&](int32_t i) -> int {  // the sentence of stream entry i (us[j] <= i < us[j+1])
+      int j = 0;
+#pragma unroll
+      for (int step = kChunk / 2; step >= 1; step >>= 1) {
+        const int k = j + step;
+        j = (k < n && us[k] <= i) ? k : j;
+      }
+      return j;
+    };
+    // one group of 64 entries: entry, sentence, pieces, segment (same sentence) structure
+    struct G {
+      uint32_t v;
+      int s, c, seg_excl;
+      bool act, last;
+    };
+    auto group = [&](int32_t g0) -> G {
+      G g;
+      const int32_t i = g0 + lane;
+      g.act = i < nu;
+      g.v = g.act ? (uint32_t)stream[i] : 0u;
+      g.s = g.act ? sent_of(i) : -1;
+      int c = 0;
+      if (g.act) c = (g.v & kUHard) ? (int)hn[g.v & ~kUHard] : 1;
+      g.c = c > 0 ? c : 0;
+      if (g.act && c <= 0) atomicOr(&tot[g.s], kRFb);
+      const uint64_t F = ballot(g.act && (lane == 0 || g.s != wave_prev(g.s)));
+      g.last = g.act && (lane == 63 || i + 1 >= nu || wave_next(g.s) != g.s);
+      const int incl = wave_incl_scan(g.c);
+      const int excl = incl - g.c;
+      g.seg_excl = excl - __shfl(excl, 63 - __clzll(F & upto), 64);
+      return g;
+    };
+    // pass 1: pieces per sentence
+    for (int32_t g0 = 0; g0 < nu; g0 += 64) {
+      const G g = group(g0);
+      wave_sync();
+      if (g.last) atomicAdd(&tot[g.s], g.seg_excl + g.c);
+      wave_sync();
+    }
+    // pass 2: from the back
+    for (int32_t g0 = nu > 0 ? ((nu - 1) & ~63) : -64; g0 >= 0; g0 -= 64) {
+      const G g = group(g0);
+      // the segment's sum: its last lane's inclusive value
+      const uint64_t E = ballot(g.last);
+      const int s1 = __ffsll((long long)(E & ~below)) - 1;
+      const int segsum = __shfl(g.seg_excl + g.c, s1 < 0 ? 63 : s1, 64);
+      if (g.act) {
+        const int32_t t = tot[g.s];
+        if (!(t & kRFb)) {
+          const int o = (t & kRCnt) - done[g.s] - segsum + g.seg_excl;
+          int32_t* __restrict__ out = ids + sent_off[c0 + g.s] + o;
+          if (g.v & kUHard) {
+            const P* p = hp + (int64_t)(g.v & ~kUHard) * kPcs;
+            for (int q = 0; q < g.c; ++q)
+              if (o + q < max_pieces) out[q] = (int32_t)p[q];
+          } else if (o < max_pieces) {
+            out[0] = (int32_t)(g.v & kUId);
+            if (g.v & kUCs) atomicOr(&tot[g.s], kLenHasClsSep);
+          }
+        }
+      }
+      wave_sync();
+      if (g.last) done[g.s] += segsum;
+      wave_sync();
+    }
+    for (int j = lane; j < n; j += 64) {
+      const int32_t t = tot[j];
+      if (t & kRFb) {
+        fb_list[atomicAdd(fb_n, 1u)] = (int32_t)(c0 + j);
+      } else {
+        const int32_t cnt = t & kRCnt;
+        sent_len[c0 + j] = (cnt < max_pieces ? cnt : max_pieces) | (t & kLenHasClsSep);
+      }
+    }
+    wave_sync();
+  }
+}
+
 }  // namespace
 }  // namespace lddl
 
@@ -1672,7 +1714,10 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
   if (n_sent >= (int64_t)INT32_MAX - (1 << 22)) LDDL_FAIL(-1, "too many sentences in one call (%lld)", (long long)n_sent);
   if (n_sent == 0) return 0;
   hipStream_t st = as_stream(stream);
-  const char* path = getenv("LDDL_TOKENIZE_PATH");  // diagnostics: "lane" = fallback kernel only
+  // diagnostics / A/B (each run by tests/test_tokenize_gpu.py): "lane" = the fallback kernel
+  // only, "wave" = one sentence per wavefront, "fused" / "split" = the streaming kernel with
+  // phase B inside / in its own launch
+  const char* path = getenv("LDDL_TOKENIZE_PATH");
   if (path && !strcmp(path, "lane")) {
     const int64_t grid = std::min<int64_t>((n_sent + kBlock - 1) / kBlock, 65536);
     hipLaunchKernelGGL(tokenize_lane_kernel, dim3((unsigned)grid), dim3(kBlock), 0, st, c->tab,
@@ -1680,13 +1725,17 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     LDDL_HIP(hipGetLastError());
     return 0;
   }
+  if (path && strcmp(path, "wave") && strcmp(path, "fused") && strcmp(path, "split"))
+    LDDL_FAIL(-1, "LDDL_TOKENIZE_PATH must be lane, wave, fused or split (got %s)", path);
+  const bool split = path ? !strcmp(path, "split") : false;
   // fallback list: [0] = count, then sentence indices
   constexpr int kFbHead = 1;
   DevArena::Block fbb;
-  // + the batch kernel's chunk counter after the list
-  LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)(n_sent + kFbHead + 1), st, fbb));
+  // + the batch kernel's chunk counter and the split form's hard-list counter after the list
+  LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)(n_sent + kFbHead + 2), st, fbb));
   int32_t* fb = static_cast<int32_t*>(fbb.p);
   int32_t* chunk_ctr = fb + kFbHead + n_sent;
+  uint32_t* hctr = reinterpret_cast<uint32_t*>(chunk_ctr + 1);
   LDDL_HIP(hipMemsetAsync(fb, 0, sizeof(int32_t) * kFbHead, st));
   int n_cu = 256;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -1701,20 +1750,10 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
                        d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + kFbHead,
                        reinterpret_cast<uint32_t*>(fb));
   } else {
-    // A/B: chunk-phased phase B + placement, with 16 / 12 / 10 / 8 waves per workgroup
-    const int cpw = !path ? 0 : !strcmp(path, "cp") ? 16 : !strcmp(path, "cp12") ? 12
-                  : !strcmp(path, "cp10") ? 10 : !strcmp(path, "cp8") ? 8 : 0;
-    const bool cp = cpw > 0;
-    // A/B: the round-4 kernel with 8-wave workgroups (88 KB of LDS: room beside it on a CU for
-    // other kernels' workgroups, e.g. the pair planner of the previous chunk)
-    const bool b8 = path && !strcmp(path, "batch8");
-    const void* kfn = cpw == 16 ? (const void*)tokenize_batch_kernel<true, 16, 1, 3>
-                    : cpw == 12 ? (const void*)tokenize_batch_kernel<true, 12, 6, 1>
-                    : cpw == 10 ? (const void*)tokenize_batch_kernel<true, 10, 5, 1>
-                    : cpw == 8 ? (const void*)tokenize_batch_kernel<true, 8, 4, 3>
-                    : b8 ? (const void*)tokenize_batch_kernel<false, 8, 1, 3>
-                               : (const void*)tokenize_batch_kernel<false, kBW, 1, 3>;
-    const int wpb = cp ? cpw : b8 ? 8 : kBW;  // waves per workgroup
+    constexpr int kSW = LDDL_SPLIT_SW;  // split: waves per workgroup of the streaming kernel
+    const void* kfn = split ? (const void*)tokenize_batch_kernel<true, kSW, LDDL_SPLIT_WPE, LDDL_SPLIT_RF>
+                            : (const void*)tokenize_batch_kernel<false, kBW, 1>;
+    const int wpb = split ? kSW : kBW;  // waves per workgroup
     LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 64 * wpb, 0));
     // each wave streams >= ~16 sentences so its unit queue stays full across sentences
     const int64_t want = (n_sent + 16 * wpb - 1) / (16 * wpb);
@@ -1733,21 +1772,62 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
 #endif
     // the first grid x wpb chunks are taken statically (chunk w by wave w)
     const int64_t first = std::min<int64_t>(grid * wpb * kChunk, (int64_t)INT32_MAX);
-    LDDL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(chunk_ctr), (int)first, 1, st));
-    DevArena::Block scr;
-    if (cp) LDDL_HIP(c->arena.take(sizeof(uint32_t) * (size_t)kScrWords * (size_t)(grid * wpb), st, scr));
-    uint32_t* scrp = cp ? static_cast<uint32_t*>(scr.p) : nullptr;
-#define LDDL_TOK_LAUNCH(KCP, KW, KWPE, KRF)                                                       \
-  hipLaunchKernelGGL((tokenize_batch_kernel<KCP, KW, KWPE, KRF>), dim3((unsigned)grid), dim3(64 * KW), 0, \
-                     st, c->tab, d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len,  \
-                     fb + kFbHead, reinterpret_cast<uint32_t*>(fb), chunk_ctr, scrp)
-    if (cpw == 16) LDDL_TOK_LAUNCH(true, 16, 1, 3);
-    else if (cpw == 12) LDDL_TOK_LAUNCH(true, 12, 6, 1);
-    else if (cpw == 10) LDDL_TOK_LAUNCH(true, 10, 5, 1);
-    else if (cpw == 8) LDDL_TOK_LAUNCH(true, 8, 4, 3);
-    else if (b8) LDDL_TOK_LAUNCH(false, 8, 1, 3);
-    else LDDL_TOK_LAUNCH(false, kBW, 1, 3);
-#undef LDDL_TOK_LAUNCH
+    if (!split) {
+      LDDL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(chunk_ctr), (int)first, 1, st));
+      hipLaunchKernelGGL((tokenize_batch_kernel<false, kBW, 1>), dim3((unsigned)grid), dim3(64 * kBW), 0,
+                         st, c->tab, d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len,
+                         fb + kFbHead, reinterpret_cast<uint32_t*>(fb), chunk_ctr, nullptr, nullptr, 0u);
+    } else {
+      if (n_bytes >= kMaxTextBytes) LDDL_FAIL(-1, "split tokenizer: more than 2^40 bytes in one call");
+      // the hard list: sized for one hard unit per 16 bytes of text (the synthetic corpus has one
+      // per ~21), claimed by the waves in blocks; a run that needs more is repeated with the
+      // count it reported (one 4-byte read back), so hp / hn can be sized exactly
+      int64_t cap = std::max<int64_t>(n_bytes / 16, 1 << 16) + (int64_t)grid * kSW * kHBlk;
+      if (const char* e = getenv("LDDL_TOKENIZE_HCAP")) cap = std::max<int64_t>(atoll(e), 1);  // tests: overflow
+      const int64_t kCapMax = (int64_t)(kUHard - 1) - kHBlk;  // h < 2^31
+      uint32_t used = 0;
+      DevArena::Block hlb;
+      for (int attempt = 0;; ++attempt) {
+        cap = std::min<int64_t>((cap + kHBlk - 1) / kHBlk * kHBlk, kCapMax / kHBlk * kHBlk);
+        LDDL_HIP(c->arena.take(sizeof(uint2) * (size_t)cap, st, hlb));
+        LDDL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(chunk_ctr), (int)first, 1, st));
+        LDDL_HIP(hipMemsetAsync(hctr, 0, sizeof(uint32_t), st));
+        hipLaunchKernelGGL((tokenize_batch_kernel<true, kSW, LDDL_SPLIT_WPE, LDDL_SPLIT_RF>), dim3((unsigned)grid), dim3(64 * kSW), 0,
+                           st, c->tab, d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids,
+                           d_sent_len, fb + kFbHead, reinterpret_cast<uint32_t*>(fb), chunk_ctr,
+                           static_cast<uint2*>(hlb.p), hctr, (uint32_t)cap);
+        LDDL_HIP(hipGetLastError());
+        LDDL_HIP(hipMemcpyAsync(&used, hctr, sizeof(used), hipMemcpyDeviceToHost, st));
+        LDDL_HIP(hipStreamSynchronize(st));
+        if ((int64_t)used <= cap) break;
+        c->arena.give(hlb, st);
+        if (attempt >= 2 || cap >= kCapMax / kHBlk * kHBlk)
+          LDDL_FAIL(-1, "split tokenizer: hard list overflow (%u units)", used);
+        cap = (int64_t)used + (int64_t)grid * kSW * kHBlk;
+      }
+      const int64_t nh = used;
+      DevArena::Block hpb, hnb;
+      LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)std::max<int64_t>(nh, 1) * kPcs, st, hpb));
+      LDDL_HIP(c->arena.take((size_t)std::max<int64_t>(nh, 1), st, hnb));
+      int32_t* hp = static_cast<int32_t*>(hpb.p);
+      int8_t* hn = static_cast<int8_t*>(hnb.p);
+      if (nh > 0) {
+        int per = 0;
+        LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tokenize_hard_kernel<int32_t>, kHardBlock, 0));
+        const int64_t hg = std::min<int64_t>((nh + kHardBlock - 1) / kHardBlock, (int64_t)n_cu * std::max(per, 1));
+        hipLaunchKernelGGL(tokenize_hard_kernel<int32_t>, dim3((unsigned)hg), dim3(kHardBlock), 0, st, c->tab,
+                           d_text, n_bytes, static_cast<const uint2*>(hlb.p), hctr, (uint32_t)cap, hp, hn);
+      }
+      const int64_t n_chunks = (n_sent + kChunk - 1) / kChunk;
+      const int64_t pg = std::min<int64_t>((n_chunks + 3) / 4, (int64_t)n_cu * 8);
+      hipLaunchKernelGGL(tokenize_place_kernel<int32_t>, dim3((unsigned)pg), dim3(256), 0, st,
+                         d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, hp, hn, fb + kFbHead,
+                         reinterpret_cast<uint32_t*>(fb));
+      LDDL_HIP(hipGetLastError());
+      c->arena.give(hlb, st);
+      c->arena.give(hpb, st);
+      c->arena.give(hnb, st);
+    }
 #ifdef LDDL_STAMPS
     {  // wave timeline (100 MHz real-time clock)
       const int64_t nw = grid * wpb;
@@ -1794,7 +1874,6 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
       LDDL_HIP(hipFree(rg));
     }
 #endif
-    if (cp) c->arena.give(scr, st);
   }
   const int64_t fgrid = std::min<int64_t>((n_sent + kBlock - 1) / kBlock, (int64_t)n_cu * 2);
   hipLaunchKernelGGL(tokenize_lane_kernel, dim3((unsigned)fgrid), dim3(kBlock), 0, st, c->tab,

@@ -59,3 +59,39 @@ def test_pmc_json_matches_actual_batch_and_template_names():
     assert plan.get('SQ_INSTS_SALU') and plan.get('hbm_bytes_per_launch')
     assert bench.pmc_entry(kernels, 'tokenize_batch_kernel').get('SQ_INSTS_VALU')
     assert bench.pmc_entry(kernels, 'no_such_kernel') == {}
+
+
+def test_partition_prefix():
+    """c4_exchange's sub-batch: whole leading partitions within the byte budget, at least one."""
+    import types
+    import numpy as np
+    sent_off = np.arange(0, 1001, 10, dtype=np.int64)       # 100 sentences of 10 bytes
+    doc_sent_off = np.arange(0, 101, 2, dtype=np.int64)     # 50 documents of 2 sentences
+    corp = types.SimpleNamespace(sent_off=sent_off, doc_sent_off=doc_sent_off)
+    part = np.arange(0, 51, 5, dtype=np.int64)              # 10 partitions of 100 bytes
+    assert bench.partition_prefix(corp, part, 350) == 3
+    assert bench.partition_prefix(corp, part, 400) == 4
+    assert bench.partition_prefix(corp, part, 10) == 1
+    assert bench.partition_prefix(corp, part, 10 ** 9) == 10
+
+
+@pytest.mark.gpu
+def test_bench_c4_exchange_subline_two_ranks():
+    """`bench.py --gpus 2` in the one-GPU rehearsal (LDDL_BENCH_SHARE_DEVICE=1: two ranks on
+    cuda:0, gloo through host tensors): the C2 line carries the c4_exchange sub-line, with rows
+    moved between the ranks and every bin's shards within one row."""
+    import json
+    env = dict(os.environ, LDDL_BENCH_SHARE_DEVICE='1')
+    env.pop('WORLD_SIZE', None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py'), '--gpus', '2', '--steps', '1',
+                        '--warmup', '0', '--batch-bytes', '60000000', '--exchange-bytes', '40000000',
+                        '--no-alt-rng', '--no-segmented-line', '--no-extra-lines'],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith('{')][-1])
+    assert line['n_gpus'] == 2
+    ex = line['c4_exchange']
+    assert ex['backend'] == 'gloo' and ex['num_shards'] == 16
+    assert ex['moved_rows'] > 0 and ex['rows'] > ex['moved_rows']
+    assert ex['shard_counts_spread'] <= 1
+    assert ex['exchange_ms'] >= 0
