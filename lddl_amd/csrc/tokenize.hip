@@ -262,13 +262,6 @@ struct Pcs {
   __device__ int32_t get(int q) const { return b[64 * q]; }
 };
 
-// The pieces of one hard unit in the split tokenizer: its row of the hard-piece table.
-template <typename P>
-struct GPcs {
-  P* b;
-  __device__ void put(int n, int32_t v) { b[n] = (P)v; }
-};
-
 // Diagnostic build: work counters of phase B (per lane; summed at the kernel's end).
 struct TokStats {
 #ifdef LDDL_STAMPS
@@ -406,9 +399,8 @@ __device__ inline int32_t piece_step(const Tables& T, const uint32_t* bloom, con
 // all bits for ASCII). Returns the piece count written to pc, or -1 if more than kPcs pieces.
 // (Round 3 probed the full length alone first, then two candidates per round trip: 21.9 ms per
 // 2 GiB against 20.7 now; three candidates per trip spilled VGPRs and took 22.1 ms, r04o.)
-template <typename Sink>  // Pcs (an LDS column) or GPcs (a global row)
 __device__ int wordpiece32(const Tables& T, const uint32_t* bloom, const B32& v, int nb,
-                           uint64_t ends, Sink& pc, bool first_probe_missed = false,
+                           uint64_t ends, Pcs& pc, bool first_probe_missed = false,
                            TokStats* ts = nullptr) {
   int n = 0, start = 0;
   while (start < nb) {
@@ -659,70 +651,6 @@ struct UnitWord {
   int status;
 };
 
-// unit_word's generic (non-ASCII) normalisation without an LDS row: the normalised bytes are
-// appended straight into the four registers of the word (the split tokenizer's hard-unit kernel,
-// whose lanes have no LDS row of their own).
-__device__ inline void put_byte32(B32& v, int pos, uint32_t b) {
-  const uint64_t x = (uint64_t)(b & 0xFFu) << (8 * (pos & 7));
-  const int q = pos >> 3;
-  v.w0 |= q == 0 ? x : 0ull;
-  v.w1 |= q == 1 ? x : 0ull;
-  v.w2 |= q == 2 ? x : 0ull;
-  v.w3 |= q == 3 ? x : 0ull;
-}
-__device__ inline uint32_t get_byte32(const B32& v, int pos) {
-  const int q = pos >> 3;
-  const uint64_t w = q == 0 ? v.w0 : q == 1 ? v.w1 : q == 2 ? v.w2 : v.w3;
-  return (uint32_t)(w >> (8 * (pos & 7))) & 0xFFu;
-}
-__device__ UnitWord unit_word_reg(const Tables& T, const uint32_t* s_ascii,
-                                  const uint8_t* __restrict__ text, int64_t start, int len) {
-  UnitWord u;
-  u.status = 0;
-  B32 v{0, 0, 0, 0};
-  int nb = 0;
-  int64_t j = start;
-  const int64_t je = start + len;
-  while (j < je) {
-    const uint32_t b0 = text[j];
-    uint32_t cp, e;
-    if (b0 < 0x80) {
-      cp = b0;
-      e = s_ascii[b0];
-      ++j;
-    } else {
-      cp = utf8_next(text, je, j);
-      e = tab_entry(T, cp);
-    }
-    if ((e >> 30) == kDrop) continue;
-    uint8_t ob[12];
-    int olen;
-    if (e & kIdent) olen = put_utf8(ob, cp);
-    else if (e & kMulti) {
-      const uint8_t* p = T.pool + (e & 0xFFFFFFu);
-      olen = p[0];
-      for (int q = 0; q < olen; ++q) ob[q] = p[2 + q];
-    } else olen = put_utf8(ob, e & 0x1FFFFFu);
-    if (nb + olen > kNorm) {
-      u.status = -1;
-      return u;
-    }
-    for (int q = 0; q < olen; ++q) put_byte32(v, nb + q, ob[q]);
-    nb += olen;
-  }
-  u.nb = nb;
-  u.v = v;
-  if (nb == 0) {
-    u.status = 1;
-    return u;
-  }
-  uint64_t ends = 1ull << nb;
-  for (int e = 1; e < nb; ++e)
-    if ((get_byte32(v, e) & 0xC0) != 0x80) ends |= 1ull << e;
-  u.ends = ends;
-  return u;
-}
-
 __device__ UnitWord unit_word(const Tables& T, const uint32_t* s_ascii, const uint8_t* __restrict__ text,
                               int64_t n_bytes, int64_t start, int len, bool unit_slow, uint8_t* w) {
   UnitWord u;
@@ -858,22 +786,6 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
 // kept a ring of in-flight sentences; its per-window bookkeeping was ~half of the kernel's
 // instructions (profiles/r03l_pmc_tokenizer_variants.txt).
 // ---------------------------------------------------------------------------------------------
-//
-// Split form (LDDL_TOKENIZE_PATH=split): the same streaming kernel resolves phase A only and
-// leaves phase B and placement to two more launches (phase B kept 43 % of its
-// lanes busy per piece-step inside the streaming kernel, whose 146 KB of LDS per workgroup held
-// it at 4 waves per SIMD):
-//   tokenize_batch_kernel<true>  per chunk, the units' phase-A results in queue order as a
-//                  compact unit stream over the chunk's own region of `ids` (ids[A + i] for the
-//                  chunk's i-th unit: the piece id | kUCs, or kUHard | h) and each sentence's unit
-//                  count in sent_len; a hard unit's record (text offset, length, flags) goes to a
-//                  global list, claimed kHBlk entries at a time per wave.
-//   tokenize_hard_kernel         greedy longest match of every listed unit, one lane per unit, at
-//                  full occupancy (no classification state): its pieces to row h of the
-//                  hard-piece table, the count to hn[h].
-//   tokenize_place_kernel        per chunk, pieces per sentence (forward pass over the stream),
-//                  then the stream expanded in place from the back (see the kernel) to the final
-//                  ids[sent_off[s] + k] layout and sent_len.
 // ---------------------------------------------------------------------------------------------
 constexpr int kSF = 192;   // units resolved per pass (kSF / 64 phase-A rounds)
 // queue capacity: before a bank < kSF complete units; a bank adds <= 64 ends and leaves <= 65
@@ -889,8 +801,7 @@ constexpr int32_t kHardBit = INT32_MIN;  // q_res: pieces are in column (res & 6
 constexpr int32_t kQPos = (1 << 28) - 1;
 constexpr int32_t kQSlow = INT32_MIN;
 constexpr int64_t kMaxSpan = 1 << 28;  // longer chunks go to the lane kernel
-// r_cnt: pieces (split: units) so far (bits 0..28) | kRFb (the sentence goes to the lane kernel)
-// | kLenHasClsSep
+// r_cnt: pieces so far (bits 0..28) | kRFb (the sentence goes to the lane kernel) | kLenHasClsSep
 constexpr int32_t kRFb = 1 << 29;
 constexpr int32_t kRCnt = kRFb - 1;
 static_assert(kLenHasClsSep == (1 << 30), "r_cnt flag layout");
@@ -912,26 +823,6 @@ struct alignas(16) StreamLds {
 };
 static_assert(kPcs * 64 * 4 >= 64 * kNorm, "normalised-word rows must fit the piece columns");
 
-// ---- split form ----
-// unit stream entry: an easy unit's piece id | kUCs (a literal [CLS] / [SEP]), or kUHard | h
-constexpr uint32_t kUHard = 1u << 31, kUCs = 1u << 30, kUId = kUCs - 1;
-// hard list entry (uint2): x = text offset bits 0..31; y = offset bits 32..39 | length << 8 |
-// kHSlow (normalise through the table) | kHMiss (phase A probed the whole word: not one piece) |
-// kHValid (entries a wave's block never filled have y = 0)
-constexpr uint32_t kHSlow = 1u << 16, kHMiss = 1u << 17, kHValid = 1u << 18;
-constexpr int kHBlk = 256;  // hard-list entries a wave claims at a time (one global atomic each)
-constexpr uint32_t kNoBlk = 0xFFFFFFFFu;
-constexpr int64_t kMaxTextBytes = 1ll << 40;  // text offsets of the hard list
-
-struct alignas(16) StreamLdsSplit {
-  int32_t q_s[kQ];
-  int32_t q_e[kQ];
-  uint8_t q_slot[kQ];
-  int32_t s_off[kChunk + 1];
-  int32_t r_cnt[kChunk];  // units (bits 0..28) | kRFb
-  int32_t trash[64];      // target of the bank loop's lanes that store nothing
-};
-
 #ifdef LDDL_STAMPS
 __device__ unsigned long long* g_tok_tl;  // diagnostic build: [wave][2] s_memrealtime start / end
 // diagnostic build: shader cycles per region, summed over waves (kTokRegions entries)
@@ -949,19 +840,14 @@ constexpr int kTokRegions = 6;  // 0 banks, 1 phase A, 2 phase B, 3 place, 4 que
   } while (0)
 #endif
 
-// kSplit: phase A only (the split form above), kRF phase-A rounds in flight; kW waves per
-// workgroup, >= kWPE waves per SIMD.
-template <bool kSplit, int kW, int kWPE, int kRF = 3>
-__global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
+__global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
     Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
     int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
-    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr,
-    uint2* __restrict__ hlist, uint32_t* __restrict__ hctr, uint32_t hcap) {
+    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr) {
   __shared__ uint32_t s_ascii[128];
   __shared__ uint8_t s_cls[256];
-  __shared__ uint32_t s_bloom[kSplit ? 1 : kBloomWords];
-  using WL = std::conditional_t<kSplit, StreamLdsSplit, StreamLds>;
-  __shared__ WL s_w[kW];
+  __shared__ uint32_t s_bloom[kBloomWords];
+  __shared__ StreamLds s_w[kBW];
 #ifdef LDDL_STAMPS
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long reg_acc[kTokRegions] = {0, 0, 0, 0, 0, 0};
@@ -981,20 +867,13 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
     }
     s_cls[c] = (uint8_t)v;
   }
-  if constexpr (!kSplit)
-    for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
+  for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
   __syncthreads();
   const int lane = lane_id();
-  WL& W = s_w[threadIdx.x >> 6];
+  StreamLds& W = s_w[threadIdx.x >> 6];
   // target of the bank loop's lanes that store nothing (no exec-mask branch): the piece columns,
-  // unused outside a flush (split: a trash row of its own)
-  int32_t* const trashp = [&]() -> int32_t* {
-    if constexpr (kSplit) return &W.trash[lane_id()];
-    else return &W.pcs[lane_id()];
-  }();
-  // split: the wave's current block of the hard list [hbase, hbase + kHBlk), hused taken
-  uint32_t hbase = kNoBlk;
-  int hused = kHBlk;
+  // unused outside a flush
+  int32_t* const trashp = &W.pcs[lane_id()];
   // sentence indices fit int32 (lddl_tokenize: n_sent < INT32_MAX - 2^22)
   const int32_t n_sent32 = (int32_t)n_sent;
   // Chunks: wave w starts with chunk w, then takes the next unclaimed chunk from chunk_ctr
@@ -1002,7 +881,7 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
   // tail: waves of one SIMD are issued oldest first, so the first finishes ~25 % before the last.
   int32_t c0;
   {
-    const int64_t w = (int64_t)blockIdx.x * kW + (threadIdx.x >> 6);
+    const int64_t w = (int64_t)blockIdx.x * kBW + (threadIdx.x >> 6);
     c0 = w * kChunk < n_sent32 ? (int32_t)(w * kChunk) : n_sent32;
   }
   const uint64_t upto = (2ull << lane) - 1;  // lanes <= this one (lane 63: all)
@@ -1012,10 +891,7 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
     const int64_t A = sent_off[c0];
     const int64_t span64 = sent_off[c0 + n] - A;
     if (span64 >= kMaxSpan) {  // pathological chunk (>= 256 MiB of text): the lane kernel
-      for (int j = lane; j < n; j += 64) {
-        if constexpr (kSplit) sent_len[c0 + j] = kRFb;  // (the placement kernel lists it)
-        else fb_list[atomicAdd(fb_n, 1u)] = c0 + j;
-      }
+      for (int j = lane; j < n; j += 64) fb_list[atomicAdd(fb_n, 1u)] = c0 + j;
     } else {
       for (int j = lane; j <= n; j += 64) W.s_off[j] = (int32_t)(sent_off[c0 + j] - A);
       for (int j = lane; j < n; j += 64) W.r_cnt[j] = 0;
@@ -1036,7 +912,6 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
       };
 
       int ns = 0, ne = 0;  // queued unit starts / ends
-      int32_t ucur = 0;    // split: units of this chunk streamed so far
 
       // drop the processed units [0, m) from the queue: < 128 starts and < 128 ends remain
       // (read all, then write)
@@ -1060,7 +935,6 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
 
       // place queue units [u0, u1) (all resolved) in order: segmented scan per sentence
       auto place = [&](int u0, int u1) {
-        if constexpr (!kSplit) {
         for (int r0 = u0; r0 < u1; r0 += 64) {
           const int u = r0 + lane;
           const bool act = u < u1;
@@ -1094,12 +968,10 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
           if (seg_last) W.r_cnt[slot] += seg_excl + npc;  // (count bits only: < 2^28 pieces)
           wave_sync();
         }
-        }
       };
 
       // resolve and place the complete units [0, m), then drop them from the queue
       auto flush = [&](int m) {
-        if constexpr (!kSplit) {
         TOK_STAMP(0);
         // phase A: specials and single-piece words
         int nh = 0;
@@ -1207,120 +1079,6 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         TOK_STAMP(3);
         drop(m);
         TOK_STAMP(4);
-        }
-      };
-
-      // split: phase A of the queued units [0, m), their stream entries and hard-list records,
-      // the sentences' unit counts; then drop them from the queue
-      auto flush_split = [&](int m) {
-        if constexpr (kSplit) {
-        constexpr int kR = kSF / 64;
-        static_assert(kR % kRF == 0, "phase A rounds in flight");
-        int32_t* __restrict__ stream = ids + A + ucur;
-        int slots[kR];
-        // kRF rounds of 64 units in flight at a time (their text loads, then their first table
-        // loads, then the checks): fewer rounds in flight hold fewer registers
-#pragma unroll
-        for (int r0 = 0; r0 < kR; r0 += kRF) {
-          bool elig[kRF], hardr[kRF];
-          int lenr[kRF];
-          int32_t qsr[kRF];
-          uint32_t resr[kRF];
-          B32 vv[kRF];
-          Probe pr[kRF];
-#pragma unroll
-          for (int r = 0; r < kRF; ++r) {
-            const int u = 64 * (r0 + r) + lane;
-            elig[r] = hardr[r] = false;
-            lenr[r] = 0;
-            resr[r] = 0;
-            qsr[r] = 0;
-            slots[r0 + r] = -1;
-            if (u < m) {
-              const int32_t qs = W.q_s[u];
-              const int st = qs & kQPos, kind = (qs >> 28) & 7;
-              const int len = W.q_e[u] - st + 1;
-              qsr[r] = qs;
-              lenr[r] = len;
-              slots[r0 + r] = W.q_slot[u];
-              if (kind >= 2) {
-                resr[r] = (uint32_t)T.special_id[kind - 2] | (kind - 2 == kCls || kind - 2 == kSep ? kUCs : 0u);
-              } else if (qs >= 0 && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32) {
-                elig[r] = true;
-                vv[r] = load32(text, n_bytes, A + st);
-              } else {
-                hardr[r] = true;
-              }
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < kRF; ++r)
-            if (elig[r]) {
-              if (T.ascii_mode == 1)
-                vv[r] = B32{swar_lower(vv[r].w0), swar_lower(vv[r].w1), swar_lower(vv[r].w2), swar_lower(vv[r].w3)};
-              pr[r] = probe_first(T, vv[r], lenr[r], 0);
-            }
-#pragma unroll
-          for (int r = 0; r < kRF; ++r) {
-            bool km = false;
-            if (elig[r]) {
-              const int32_t id = probe_finish(T, vv[r], lenr[r], pr[r]);
-              resr[r] = (uint32_t)id;
-              hardr[r] = km = id < 0;
-            }
-            const int u = 64 * (r0 + r) + lane;
-            const bool act = u < m;
-            const bool slow = qsr[r] < 0;
-            // units the hard kernel does not take send their sentence to the lane kernel: ASCII
-            // words of > 32 bytes (their normalised form is as long) and > 255 bytes of anything
-            bool fb = hardr[r] && (slow ? lenr[r] > 255 : lenr[r] > 32);
-            const bool hk = hardr[r] && !fb;
-            const uint64_t Hm = ballot(hk);
-            const int nh = __popcll(Hm);
-            if (nh && hused + nh > kHBlk) {  // a new block (wave-uniform)
-              if (hbase != kNoBlk)  // the rest of the old one: entries the hard kernel skips
-                for (int t = hused + lane; t < kHBlk; t += 64) hlist[hbase + t] = make_uint2(0u, 0u);
-              uint32_t nb = 0;
-              if (lane == 0) nb = atomicAdd(hctr, (uint32_t)kHBlk);
-              nb = __builtin_amdgcn_readfirstlane(nb);
-              // past the list's capacity: no block (the host sees the count and runs again with a
-              // list that holds it; meanwhile these units go to the lane kernel)
-              hbase = (uint64_t)nb + kHBlk <= (uint64_t)hcap ? nb : kNoBlk;
-              hused = 0;
-            }
-            const bool have = hbase != kNoBlk;
-            if (act) {
-              uint32_t val = resr[r];
-              if (hk && have) {
-                const uint32_t h = hbase + (uint32_t)hused + popc_below(Hm);
-                const int64_t pos = A + (qsr[r] & kQPos);
-                hlist[h] = make_uint2((uint32_t)pos, (uint32_t)(pos >> 32) | (uint32_t)lenr[r] << 8 |
-                                                         (slow ? kHSlow : 0u) | (km ? kHMiss : 0u) | kHValid);
-                val = kUHard | h;
-              }
-              fb |= hk && !have;
-              stream[u] = (int32_t)val;
-              if (fb) atomicOr(&W.r_cnt[slots[r0 + r]], kRFb);
-            }
-            if (have) hused += nh;
-          }
-        }
-        wave_sync();
-        // units per sentence: segmented counts of the slots (non-decreasing in queue order)
-#pragma unroll
-        for (int r = 0; r < kR; ++r) {
-          const int u = 64 * r + lane;
-          const bool act = u < m;
-          const int slot = slots[r];
-          const uint64_t F = ballot(act && (lane == 0 || slot != wave_prev(slot)));
-          const bool last = act && (lane == 63 || u + 1 >= m || wave_next(slot) != slot);
-          const int s0 = 63 - __clzll(F & upto);
-          if (last) atomicAdd(&W.r_cnt[slot], lane - s0 + 1);
-        }
-        wave_sync();
-        ucur += m;
-        drop(m);
-        }
       };
 
       // ---- the chunk's banks ----
@@ -1458,8 +1216,7 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
         CONTp = CONT;
         if (ne >= kSF) {
           wave_sync();
-          if constexpr (kSplit) flush_split(kSF);
-          else flush(kSF);
+          flush(kSF);
         }
       }
       {  // the last bank's ends (nothing continues past the chunk)
@@ -1471,16 +1228,11 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
       }
       wave_sync();
       TOK_STAMP(0);
-      while (ne > 0) {
-        if constexpr (kSplit) flush_split(ne < kSF ? ne : kSF);
-        else flush(ne < kSF ? ne : kSF);
-      }
+      while (ne > 0) flush(ne < kSF ? ne : kSF);
       // the chunk's sentences
       for (int j = lane; j < n; j += 64) {
         const int32_t rc = W.r_cnt[j];
-        if constexpr (kSplit) {
-          sent_len[c0 + j] = rc;  // units | kRFb: the placement kernel's input
-        } else if (rc & kRFb) {
+        if (rc & kRFb) {
           fb_list[atomicAdd(fb_n, 1u)] = c0 + j;
         } else {
           const int32_t cnt = rc & kRCnt;
@@ -1495,13 +1247,9 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
     nc = __builtin_amdgcn_readfirstlane(nc);
     c0 = nc < n_sent32 ? nc : n_sent32;
   }
-  if constexpr (kSplit) {  // the rest of the wave's last block: entries the hard kernel skips
-    if (hbase != kNoBlk)
-      for (int t = hused + lane; t < kHBlk; t += 64) hlist[hbase + t] = make_uint2(0u, 0u);
-  }
 #ifdef LDDL_STAMPS
   if (lane == 0 && g_tok_tl) {
-    const int64_t wv = (int64_t)blockIdx.x * kW + (threadIdx.x >> 6);
+    const int64_t wv = (int64_t)blockIdx.x * kBW + (threadIdx.x >> 6);
     g_tok_tl[2 * wv] = rt0;
     g_tok_tl[2 * wv + 1] = __builtin_amdgcn_s_memrealtime();
   }
@@ -1513,191 +1261,6 @@ __global__ void __launch_bounds__(64 * kW, kWPE) tokenize_batch_kernel(
       if (lane == 0) atomicAdd(g_tok_reg + kTokRegions + q, (unsigned long long)v);
     }
 #endif
-}
-
-// Split form, phase B: the greedy longest match of every unit of the hard list (one lane per
-// unit; the Bloom filter in LDS), pieces to hp[h * kPcs + q], their count to hn[h]. A count <= 0
-// sends the sentence to the lane kernel: -1 for more than kPcs pieces or a normalised word of
-// more than kNorm bytes, and a unit whose every character the normaliser drops (0 pieces) too,
-// because the in-place placement relies on >= 1 piece per unit.
-// (tuning knobs of the split form, set while it is measured; fixed once chosen)
-#ifndef LDDL_HARD_BLOCK
-#define LDDL_HARD_BLOCK 256
-#endif
-#ifndef LDDL_HARD_WPE
-#define LDDL_HARD_WPE 1
-#endif
-#ifndef LDDL_SPLIT_SW
-#define LDDL_SPLIT_SW 8
-#endif
-#ifndef LDDL_SPLIT_WPE
-#define LDDL_SPLIT_WPE 4
-#endif
-#ifndef LDDL_SPLIT_RF
-#define LDDL_SPLIT_RF 3
-#endif
-constexpr int kHardBlock = LDDL_HARD_BLOCK;
-template <typename P>
-__global__ void __launch_bounds__(kHardBlock, LDDL_HARD_WPE) tokenize_hard_kernel(
-    Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const uint2* __restrict__ hlist,
-    const uint32_t* __restrict__ hctr, uint32_t hcap, P* __restrict__ hp, int8_t* __restrict__ hn) {
-  __shared__ uint32_t s_ascii[128];
-  __shared__ uint32_t s_bloom[kBloomWords];
-  for (int c = threadIdx.x; c < 128; c += blockDim.x) s_ascii[c] = tab_entry(T, (uint32_t)c);
-  for (int c = threadIdx.x; c < kBloomWords; c += blockDim.x) s_bloom[c] = T.bloom[c];
-  __syncthreads();
-  const uint32_t nh = *hctr < hcap ? *hctr : hcap;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += stride) {
-    const uint2 e = hlist[h];
-    if (!(e.y & kHValid)) continue;
-    const int64_t pos = (int64_t)e.x | ((int64_t)(e.y & 0xFFu) << 32);
-    const int len = (int)((e.y >> 8) & 0xFFu);
-    UnitWord uw;
-    if (!(e.y & kHSlow) && T.ascii_mode != 0 && len <= 32) {
-      B32 v = load32(text, n_bytes, pos);
-      if (T.ascii_mode == 1) v = B32{swar_lower(v.w0), swar_lower(v.w1), swar_lower(v.w2), swar_lower(v.w3)};
-      uw.v = v;
-      uw.nb = len;
-      uw.ends = ~0ull;
-      uw.status = 0;
-    } else {
-      uw = unit_word_reg(T, s_ascii, text, pos, len);
-    }
-    int npc = -1;
-    if (uw.status == 0) {
-      GPcs<P> pc{hp + (int64_t)h * kPcs};
-      npc = wordpiece32(T, s_bloom, uw.v, uw.nb, uw.ends, pc, (e.y & kHMiss) != 0);
-    }
-    hn[h] = (int8_t)(npc > 0 ? npc : -1);
-  }
-}
-
-// Split form, placement: one wave per chunk of kChunk sentences (the streaming kernel's chunks).
-// sent_len holds each sentence's unit count (| kRFb); the chunk's unit stream is ids[A + i],
-// A = sent_off[c0]. Pass 1 (forward) sums each sentence's pieces (1 per easy unit, hn[h] per hard
-// one). Pass 2 walks the stream from the back, 64 units at a time, and writes every unit's
-// pieces to ids[sent_off[s] + o] (o < max_pieces). In place, because no write reaches a stream
-// entry not yet read: unit i of sentence s (its j-th) is stream entry A + i with
-// i = (units of the sentences before s) + j <= (sent_off[s] - A) + j, and its pieces start at
-// sent_off[s] + o_i with o_i >= j (every unit has >= 1 piece: a unit with none sends its sentence
-// to the lane kernel), so a group's writes land at or after its own entries — read first, in
-// registers — and after every entry of the groups before it; the scans that place a group use all
-// its lanes' entries, so its stores issue after all of its loads have returned.
-template <typename P>
-__global__ void __launch_bounds__(256) tokenize_place_kernel(
-    const int64_t* __restrict__ sent_off, int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids,
-    int32_t* __restrict__ sent_len, const P* __restrict__ hp, const int8_t* __restrict__ hn,
-    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n) {
-  constexpr int kWv = 4;
-  __shared__ int32_t s_us[kWv][kChunk + 1];  // the sentences' first stream entries; [n] = units
-  __shared__ int32_t s_tot[kWv][kChunk];     // pieces | kRFb | kLenHasClsSep
-  __shared__ int32_t s_done[kWv][kChunk];    // pieces of the units already placed (pass 2)
-  const int lane = lane_id(), wv = threadIdx.x >> 6;
-  int32_t* us = s_us[wv];
-  int32_t* tot = s_tot[wv];
-  int32_t* done = s_done[wv];
-  const uint64_t upto = (2ull << lane) - 1;
-  const uint64_t below = (1ull << lane) - 1;
-  const int64_t n_chunks = (n_sent + kChunk - 1) / kChunk;
-  for (int64_t c = (int64_t)blockIdx.x * kWv + wv; c < n_chunks; c += (int64_t)gridDim.x * kWv) {
-    const int64_t c0 = c * kChunk;
-    const int n = n_sent - c0 < kChunk ? (int)(n_sent - c0) : kChunk;
-    const int64_t A = sent_off[c0];
-    int32_t carry = 0;
-#pragma unroll
-    for (int j0 = 0; j0 < kChunk; j0 += 64) {
-      const int j = j0 + lane;
-      const int32_t r = j < n ? sent_len[c0 + j] : 0;
-      const int32_t cnt = r & kRCnt;
-      const int32_t incl = wave_incl_scan(cnt);
-      if (j < n) {
-        us[j] = carry + incl - cnt;
-        tot[j] = r & kRFb;
-        done[j] = 0;
-      }
-      carry += __builtin_amdgcn_readlane(incl, 63);
-    }
-    if (lane == 0) us[n] = carry;
-    wave_sync();
-    const int32_t nu = carry;
-    const int32_t* __restrict__ stream = ids + A;
-    auto sent_of = [&](int32_t i) -> int {  // the sentence of stream entry i (us[j] <= i < us[j+1])
-      int j = 0;
-#pragma unroll
-      for (int step = kChunk / 2; step >= 1; step >>= 1) {
-        const int k = j + step;
-        j = (k < n && us[k] <= i) ? k : j;
-      }
-      return j;
-    };
-    // one group of 64 entries: entry, sentence, pieces, segment (same sentence) structure
-    struct G {
-      uint32_t v;
-      int s, c, seg_excl;
-      bool act, last;
-    };
-    auto group = [&](int32_t g0) -> G {
-      G g;
-      const int32_t i = g0 + lane;
-      g.act = i < nu;
-      g.v = g.act ? (uint32_t)stream[i] : 0u;
-      g.s = g.act ? sent_of(i) : -1;
-      int c = 0;
-      if (g.act) c = (g.v & kUHard) ? (int)hn[g.v & ~kUHard] : 1;
-      g.c = c > 0 ? c : 0;
-      if (g.act && c <= 0) atomicOr(&tot[g.s], kRFb);
-      const uint64_t F = ballot(g.act && (lane == 0 || g.s != wave_prev(g.s)));
-      g.last = g.act && (lane == 63 || i + 1 >= nu || wave_next(g.s) != g.s);
-      const int incl = wave_incl_scan(g.c);
-      const int excl = incl - g.c;
-      g.seg_excl = excl - __shfl(excl, 63 - __clzll(F & upto), 64);
-      return g;
-    };
-    // pass 1: pieces per sentence
-    for (int32_t g0 = 0; g0 < nu; g0 += 64) {
-      const G g = group(g0);
-      wave_sync();
-      if (g.last) atomicAdd(&tot[g.s], g.seg_excl + g.c);
-      wave_sync();
-    }
-    // pass 2: from the back
-    for (int32_t g0 = nu > 0 ? ((nu - 1) & ~63) : -64; g0 >= 0; g0 -= 64) {
-      const G g = group(g0);
-      // the segment's sum: its last lane's inclusive value
-      const uint64_t E = ballot(g.last);
-      const int s1 = __ffsll((long long)(E & ~below)) - 1;
-      const int segsum = __shfl(g.seg_excl + g.c, s1 < 0 ? 63 : s1, 64);
-      if (g.act) {
-        const int32_t t = tot[g.s];
-        if (!(t & kRFb)) {
-          const int o = (t & kRCnt) - done[g.s] - segsum + g.seg_excl;
-          int32_t* __restrict__ out = ids + sent_off[c0 + g.s] + o;
-          if (g.v & kUHard) {
-            const P* p = hp + (int64_t)(g.v & ~kUHard) * kPcs;
-            for (int q = 0; q < g.c; ++q)
-              if (o + q < max_pieces) out[q] = (int32_t)p[q];
-          } else if (o < max_pieces) {
-            out[0] = (int32_t)(g.v & kUId);
-            if (g.v & kUCs) atomicOr(&tot[g.s], kLenHasClsSep);
-          }
-        }
-      }
-      wave_sync();
-      if (g.last) done[g.s] += segsum;
-      wave_sync();
-    }
-    for (int j = lane; j < n; j += 64) {
-      const int32_t t = tot[j];
-      if (t & kRFb) {
-        fb_list[atomicAdd(fb_n, 1u)] = (int32_t)(c0 + j);
-      } else {
-        const int32_t cnt = t & kRCnt;
-        sent_len[c0 + j] = (cnt < max_pieces ? cnt : max_pieces) | (t & kLenHasClsSep);
-      }
-    }
-    wave_sync();
-  }
 }
 
 }  // namespace
@@ -1714,9 +1277,10 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
   if (n_sent >= (int64_t)INT32_MAX - (1 << 22)) LDDL_FAIL(-1, "too many sentences in one call (%lld)", (long long)n_sent);
   if (n_sent == 0) return 0;
   hipStream_t st = as_stream(stream);
-  // diagnostics / A/B (each run by tests/test_tokenize_gpu.py): "lane" = the fallback kernel
-  // only, "wave" = one sentence per wavefront, "fused" / "split" = the streaming kernel with
-  // phase B inside / in its own launch
+  // diagnostics (each run by tests/test_tokenize_gpu.py against the oracle): "lane" = the
+  // fallback kernel for the whole input, "wave" = one sentence per wavefront, "fused" = the
+  // default. (Round 6's split form — phase B and placement in launches of their own — measured
+  // slower and lives on branch ab/tok-split)
   const char* path = getenv("LDDL_TOKENIZE_PATH");
   if (path && !strcmp(path, "lane")) {
     const int64_t grid = std::min<int64_t>((n_sent + kBlock - 1) / kBlock, 65536);
@@ -1725,17 +1289,15 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     LDDL_HIP(hipGetLastError());
     return 0;
   }
-  if (path && strcmp(path, "wave") && strcmp(path, "fused") && strcmp(path, "split"))
-    LDDL_FAIL(-1, "LDDL_TOKENIZE_PATH must be lane, wave, fused or split (got %s)", path);
-  const bool split = path ? !strcmp(path, "split") : false;
+  if (path && strcmp(path, "wave") && strcmp(path, "fused"))
+    LDDL_FAIL(-1, "LDDL_TOKENIZE_PATH must be lane, wave or fused (got %s)", path);
   // fallback list: [0] = count, then sentence indices
   constexpr int kFbHead = 1;
   DevArena::Block fbb;
-  // + the batch kernel's chunk counter and the split form's hard-list counter after the list
-  LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)(n_sent + kFbHead + 2), st, fbb));
+  // + the batch kernel's chunk counter after the list
+  LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)(n_sent + kFbHead + 1), st, fbb));
   int32_t* fb = static_cast<int32_t*>(fbb.p);
   int32_t* chunk_ctr = fb + kFbHead + n_sent;
-  uint32_t* hctr = reinterpret_cast<uint32_t*>(chunk_ctr + 1);
   LDDL_HIP(hipMemsetAsync(fb, 0, sizeof(int32_t) * kFbHead, st));
   int n_cu = 256;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -1750,11 +1312,8 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
                        d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + kFbHead,
                        reinterpret_cast<uint32_t*>(fb));
   } else {
-    constexpr int kSW = LDDL_SPLIT_SW;  // split: waves per workgroup of the streaming kernel
-    const void* kfn = split ? (const void*)tokenize_batch_kernel<true, kSW, LDDL_SPLIT_WPE, LDDL_SPLIT_RF>
-                            : (const void*)tokenize_batch_kernel<false, kBW, 1>;
-    const int wpb = split ? kSW : kBW;  // waves per workgroup
-    LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 64 * wpb, 0));
+    const int wpb = kBW;  // waves per workgroup
+    LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_batch_kernel, 64 * wpb, 0));
     // each wave streams >= ~16 sentences so its unit queue stays full across sentences
     const int64_t want = (n_sent + 16 * wpb - 1) / (16 * wpb);
     int64_t grid = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1)));
@@ -1772,62 +1331,10 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
 #endif
     // the first grid x wpb chunks are taken statically (chunk w by wave w)
     const int64_t first = std::min<int64_t>(grid * wpb * kChunk, (int64_t)INT32_MAX);
-    if (!split) {
-      LDDL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(chunk_ctr), (int)first, 1, st));
-      hipLaunchKernelGGL((tokenize_batch_kernel<false, kBW, 1>), dim3((unsigned)grid), dim3(64 * kBW), 0,
-                         st, c->tab, d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len,
-                         fb + kFbHead, reinterpret_cast<uint32_t*>(fb), chunk_ctr, nullptr, nullptr, 0u);
-    } else {
-      if (n_bytes >= kMaxTextBytes) LDDL_FAIL(-1, "split tokenizer: more than 2^40 bytes in one call");
-      // the hard list: sized for one hard unit per 16 bytes of text (the synthetic corpus has one
-      // per ~21), claimed by the waves in blocks; a run that needs more is repeated with the
-      // count it reported (one 4-byte read back), so hp / hn can be sized exactly
-      int64_t cap = std::max<int64_t>(n_bytes / 16, 1 << 16) + (int64_t)grid * kSW * kHBlk;
-      if (const char* e = getenv("LDDL_TOKENIZE_HCAP")) cap = std::max<int64_t>(atoll(e), 1);  // tests: overflow
-      const int64_t kCapMax = (int64_t)(kUHard - 1) - kHBlk;  // h < 2^31
-      uint32_t used = 0;
-      DevArena::Block hlb;
-      for (int attempt = 0;; ++attempt) {
-        cap = std::min<int64_t>((cap + kHBlk - 1) / kHBlk * kHBlk, kCapMax / kHBlk * kHBlk);
-        LDDL_HIP(c->arena.take(sizeof(uint2) * (size_t)cap, st, hlb));
-        LDDL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(chunk_ctr), (int)first, 1, st));
-        LDDL_HIP(hipMemsetAsync(hctr, 0, sizeof(uint32_t), st));
-        hipLaunchKernelGGL((tokenize_batch_kernel<true, kSW, LDDL_SPLIT_WPE, LDDL_SPLIT_RF>), dim3((unsigned)grid), dim3(64 * kSW), 0,
-                           st, c->tab, d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids,
-                           d_sent_len, fb + kFbHead, reinterpret_cast<uint32_t*>(fb), chunk_ctr,
-                           static_cast<uint2*>(hlb.p), hctr, (uint32_t)cap);
-        LDDL_HIP(hipGetLastError());
-        LDDL_HIP(hipMemcpyAsync(&used, hctr, sizeof(used), hipMemcpyDeviceToHost, st));
-        LDDL_HIP(hipStreamSynchronize(st));
-        if ((int64_t)used <= cap) break;
-        c->arena.give(hlb, st);
-        if (attempt >= 2 || cap >= kCapMax / kHBlk * kHBlk)
-          LDDL_FAIL(-1, "split tokenizer: hard list overflow (%u units)", used);
-        cap = (int64_t)used + (int64_t)grid * kSW * kHBlk;
-      }
-      const int64_t nh = used;
-      DevArena::Block hpb, hnb;
-      LDDL_HIP(c->arena.take(sizeof(int32_t) * (size_t)std::max<int64_t>(nh, 1) * kPcs, st, hpb));
-      LDDL_HIP(c->arena.take((size_t)std::max<int64_t>(nh, 1), st, hnb));
-      int32_t* hp = static_cast<int32_t*>(hpb.p);
-      int8_t* hn = static_cast<int8_t*>(hnb.p);
-      if (nh > 0) {
-        int per = 0;
-        LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tokenize_hard_kernel<int32_t>, kHardBlock, 0));
-        const int64_t hg = std::min<int64_t>((nh + kHardBlock - 1) / kHardBlock, (int64_t)n_cu * std::max(per, 1));
-        hipLaunchKernelGGL(tokenize_hard_kernel<int32_t>, dim3((unsigned)hg), dim3(kHardBlock), 0, st, c->tab,
-                           d_text, n_bytes, static_cast<const uint2*>(hlb.p), hctr, (uint32_t)cap, hp, hn);
-      }
-      const int64_t n_chunks = (n_sent + kChunk - 1) / kChunk;
-      const int64_t pg = std::min<int64_t>((n_chunks + 3) / 4, (int64_t)n_cu * 8);
-      hipLaunchKernelGGL(tokenize_place_kernel<int32_t>, dim3((unsigned)pg), dim3(256), 0, st,
-                         d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, hp, hn, fb + kFbHead,
-                         reinterpret_cast<uint32_t*>(fb));
-      LDDL_HIP(hipGetLastError());
-      c->arena.give(hlb, st);
-      c->arena.give(hpb, st);
-      c->arena.give(hnb, st);
-    }
+    LDDL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(chunk_ctr), (int)first, 1, st));
+    hipLaunchKernelGGL(tokenize_batch_kernel, dim3((unsigned)grid), dim3(64 * kBW), 0, st, c->tab,
+                       d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len,
+                       fb + kFbHead, reinterpret_cast<uint32_t*>(fb), chunk_ctr);
 #ifdef LDDL_STAMPS
     {  // wave timeline (100 MHz real-time clock)
       const int64_t nw = grid * wpb;

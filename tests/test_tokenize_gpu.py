@@ -91,20 +91,8 @@ def _adversarial_corpus(seed=7, n=6000):
     return text, off
 
 
-# the two forms of the streaming tokenizer (phase B inside the streaming kernel / in its own
-# launch with in-place placement); every other test runs the default
-STREAM_PATHS = ['fused', 'split']
-
-
-@pytest.fixture
-def tok_path(request, monkeypatch):
-    monkeypatch.setenv('LDDL_TOKENIZE_PATH', request.param)
-    return request.param
-
-
-@pytest.mark.parametrize('tok_path', STREAM_PATHS, indirect=True)
 @pytest.mark.parametrize('case', ['uncased', 'cased'])
-def test_tokenize_adversarial_vs_oracle(case, ctxs, tok_path):
+def test_tokenize_adversarial_vs_oracle(case, ctxs):
     from oracle import oracle as O
     text, off = _adversarial_corpus()
     vocab = VOCAB_UNCASED if case == 'uncased' else VOCAB_CASED
@@ -116,10 +104,10 @@ def test_tokenize_adversarial_vs_oracle(case, ctxs, tok_path):
         np.testing.assert_array_equal(ids, e)
 
 
-@pytest.mark.parametrize('path', ['lane', 'wave'] + STREAM_PATHS)
+@pytest.mark.parametrize('path', ['lane', 'wave', 'fused'])
 def test_tokenize_paths_vs_oracle(ctxs, monkeypatch, path):
-    """Every LDDL_TOKENIZE_PATH (the lane kernel alone, the unbatched wave kernel, both streaming
-    forms) against the oracle, on the synthetic corpus and on the adversarial one."""
+    """Every LDDL_TOKENIZE_PATH (the lane kernel alone, the unbatched wave kernel, the streaming
+    kernel by name) against the oracle, on the synthetic corpus and on the adversarial one."""
     from lddl_amd import synth
     from oracle import oracle as O
     tok = O.Tokenizer(VOCAB_UNCASED, lowercase=True)
@@ -139,8 +127,7 @@ def test_tokenize_path_unknown_raises(ctxs, monkeypatch):
         ctxs['uncased'].tokenize_host(text, np.asarray([0, len(text)], np.int64))
 
 
-@pytest.mark.parametrize('tok_path', STREAM_PATHS, indirect=True)
-def test_tokenize_long_and_empty_sentences(ctxs, tok_path):
+def test_tokenize_long_and_empty_sentences(ctxs):
     """Sentences far beyond 512 pieces (early stop), runs of empty sentences (ring retirement),
     and one sentence per wave's stream position."""
     from oracle import oracle as O
@@ -155,9 +142,8 @@ def test_tokenize_long_and_empty_sentences(ctxs, tok_path):
         np.testing.assert_array_equal(ids, e)
 
 
-@pytest.mark.parametrize('tok_path', STREAM_PATHS, indirect=True)
 @pytest.mark.parametrize('grid', ['1', '3'])
-def test_tokenize_dynamic_chunks_vs_oracle(ctxs, monkeypatch, grid, tok_path):
+def test_tokenize_dynamic_chunks_vs_oracle(ctxs, monkeypatch, grid):
     """With a grid of 1 or 3 workgroups (LDDL_TOKENIZE_GRID) most sentences are claimed through
     the batch kernel's atomic chunk counter, in chunks of consecutive (adjacent) sentences; the
     output is the oracle's, with runs of empty sentences at chunk boundaries included."""
@@ -168,26 +154,5 @@ def test_tokenize_dynamic_chunks_vs_oracle(ctxs, monkeypatch, grid, tok_path):
     for mp in (512, 9):
         ids, o = ctxs['uncased'].tokenize_host(text, off, max_pieces=mp)
         e, eo = tok.tokenize(text, off, max_pieces=mp)
-        np.testing.assert_array_equal(o, eo)
-        np.testing.assert_array_equal(ids, e)
-
-
-@pytest.mark.parametrize('cap', ['1', '300'])
-def test_tokenize_split_hard_list_overflow(ctxs, monkeypatch, cap):
-    """Split form: a hard-unit list too small for the input (LDDL_TOKENIZE_HCAP, entries) makes
-    the streaming kernel send the units it cannot list to the lane kernel and report the count it
-    needed; the call runs again with a list that holds them. Output = the oracle's, also on a
-    punctuation- and CJK-dense input (a hard unit every few bytes)."""
-    from lddl_amd import synth
-    from oracle import oracle as O
-    monkeypatch.setenv('LDDL_TOKENIZE_PATH', 'split')
-    monkeypatch.setenv('LDDL_TOKENIZE_HCAP', cap)
-    tok = O.Tokenizer(VOCAB_UNCASED, lowercase=True)
-    corp = synth.generate(seed=5, n_bytes=1 << 20, nonascii_frac=0.3)
-    dense = ('中文ÉCOLE ~~ ¿¡ ' * 2000).encode()
-    for text, off in ((corp.text, corp.sent_off),
-                      (np.frombuffer(dense, np.uint8).copy(), np.asarray([0, 7, len(dense)], np.int64))):
-        ids, o = ctxs['uncased'].tokenize_host(text, off)
-        e, eo = tok.tokenize(text, off)
         np.testing.assert_array_equal(o, eo)
         np.testing.assert_array_equal(ids, e)
