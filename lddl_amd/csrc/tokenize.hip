@@ -786,7 +786,39 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
 // kept a ring of in-flight sentences; its per-window bookkeeping was ~half of the kernel's
 // instructions (profiles/r03l_pmc_tokenizer_variants.txt).
 // ---------------------------------------------------------------------------------------------
+//
+// Word memo (round 6). Phase B (greedy longest match of the multi-piece and non-ASCII words) is
+// ~half of the kernel's wave cycles, and its words repeat: in the synthetic corpus 26 % of the
+// pre-tokenizer units are multi-piece, and 95 % of those occurrences are words already seen in
+// the first 3 % of the text (Zipf). lddl_tokenize therefore runs the kernel twice per call: over
+// a leading sample of the sentences (kMemoBuild: every resolved multi-piece word's pieces go to a
+// device table, one slot per hash, the first writer claims it by CAS), then over the rest
+// (kMemoLookup: a phase-B lane reads its word's slot — one 64-byte entry, normalised bytes as the
+// key — and runs the greedy match only on a miss). The table belongs to the call: it is cleared
+// before the sample pass, and the two launches order every write before every read, so an entry
+// is always one complete (word, pieces) record. The pieces are a function of the normalised word
+// alone, so the output is the same with or without the memo (tests run both).
 // ---------------------------------------------------------------------------------------------
+enum : int { kMemoOff = 0, kMemoBuild = 1, kMemoLookup = 2 };
+constexpr int kMemoLog2 = 21;  // 2 M entries x 64 B = 128 MiB
+struct WordMemo {
+  uint4* tab;  // entry e: tab[4e], tab[4e+1] key bytes 0..31 (zero past nb), tab[4e+2] pieces
+               // (8 x uint16), tab[4e+3].x meta: kMemoReady | nb | npc << 8 (0: empty)
+  uint32_t mask;
+};
+constexpr uint32_t kMemoReady = 1u << 31, kMemoClaim = 1u << 30;
+__device__ inline B32 memo_key(const B32& v, int nb) {
+  return B32{keep_bytes(v.w0, nb), keep_bytes(v.w1, nb - 8), keep_bytes(v.w2, nb - 16),
+             keep_bytes(v.w3, nb - 24)};
+}
+__device__ inline uint32_t memo_slot(const B32& k, int nb) {
+  uint64_t h = k.w0 * 0x9E3779B97F4A7C15ull ^ (uint64_t)nb;
+  h = (h ^ (h >> 29) ^ k.w1) * 0xBF58476D1CE4E5B9ull;
+  h = (h ^ (h >> 32) ^ k.w2) * 0x94D049BB133111EBull;
+  h = (h ^ (h >> 29) ^ k.w3) * 0x9E3779B97F4A7C15ull;
+  return (uint32_t)(h >> 32);
+}
+
 constexpr int kSF = 192;   // units resolved per pass (kSF / 64 phase-A rounds)
 // queue capacity: before a bank < kSF complete units; a bank adds <= 64 ends and leaves <= 65
 // units open (started, end not yet enqueued)
@@ -840,10 +872,12 @@ constexpr int kTokRegions = 6;  // 0 banks, 1 phase A, 2 phase B, 3 place, 4 que
   } while (0)
 #endif
 
+template <int kMemo>  // kMemoOff / kMemoBuild / kMemoLookup (word memo above)
 __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
     Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
     int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
-    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr) {
+    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr,
+    WordMemo M) {
   __shared__ uint32_t s_ascii[128];
   __shared__ uint8_t s_cls[256];
   __shared__ uint32_t s_bloom[kBloomWords];
@@ -1059,8 +1093,47 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
           int npc = 0;
           if (lane < hn) {
             Pcs pc{W.pcs + lane};
-            if (uw.status == 0) npc = wordpiece32(T, s_bloom, uw.v, uw.nb, uw.ends, pc, known_miss, tsp);
-            else if (uw.status < 0) npc = -1;
+            if (uw.status == 0) {
+              if constexpr (kMemo == kMemoOff) {
+                npc = wordpiece32(T, s_bloom, uw.v, uw.nb, uw.ends, pc, known_miss, tsp);
+              } else {
+                const B32 key = memo_key(uw.v, uw.nb);
+                uint4* e = M.tab + 4 * (size_t)(memo_slot(key, uw.nb) & M.mask);
+                bool hit = false;
+                if constexpr (kMemo == kMemoLookup) {
+                  const uint4 k0 = e[0], k1 = e[1], pz = e[2];
+                  const uint32_t meta = e[3].x;
+                  hit = (meta & kMemoReady) && (int)(meta & 0xFFu) == uw.nb &&
+                        ((k0.x | (uint64_t)k0.y << 32) ^ key.w0 | (k0.z | (uint64_t)k0.w << 32) ^ key.w1 |
+                         (k1.x | (uint64_t)k1.y << 32) ^ key.w2 | (k1.z | (uint64_t)k1.w << 32) ^ key.w3) == 0;
+                  if (hit) {
+                    npc = (int)((meta >> 8) & 0xFu);
+                    const uint32_t pw[4] = {pz.x, pz.y, pz.z, pz.w};
+#pragma unroll
+                    for (int q = 0; q < kPcs; ++q)
+                      if (q < npc) pc.put(q, (int32_t)((pw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu));
+                  }
+                }
+                if (!hit) npc = wordpiece32(T, s_bloom, uw.v, uw.nb, uw.ends, pc, known_miss, tsp);
+                if constexpr (kMemo == kMemoBuild) {
+                  // first writer of the slot in this call claims it; no lane of this launch reads
+                  if (npc >= 1 && atomicCAS(&e[3].x, 0u, kMemoClaim) == 0u) {
+                    uint32_t pw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                    for (int q = 0; q < kPcs; ++q)
+                      if (q < npc) pw[q >> 1] |= ((uint32_t)pc.get(q) & 0xFFFFu) << (16 * (q & 1));
+                    e[0] = make_uint4((uint32_t)key.w0, (uint32_t)(key.w0 >> 32), (uint32_t)key.w1,
+                                      (uint32_t)(key.w1 >> 32));
+                    e[1] = make_uint4((uint32_t)key.w2, (uint32_t)(key.w2 >> 32), (uint32_t)key.w3,
+                                      (uint32_t)(key.w3 >> 32));
+                    e[2] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+                    e[3].x = kMemoReady | (uint32_t)uw.nb | (uint32_t)npc << 8;
+                  }
+                }
+              }
+            } else if (uw.status < 0) {
+              npc = -1;
+            }
             if (npc < 0) {  // the sentence goes to the lane kernel
               atomicOr(&W.r_cnt[sent_of(st)], kRFb);
               npc = 0;
@@ -1279,7 +1352,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
   hipStream_t st = as_stream(stream);
   // diagnostics (each run by tests/test_tokenize_gpu.py against the oracle): "lane" = the
   // fallback kernel for the whole input, "wave" = one sentence per wavefront, "fused" = the
-  // default. (Round 6's split form — phase B and placement in launches of their own — measured
+  // default, "plain" = the streaming kernel without the word memo. (Round 6's split form — phase B and placement in launches of their own — measured
   // slower and lives on branch ab/tok-split)
   const char* path = getenv("LDDL_TOKENIZE_PATH");
   if (path && !strcmp(path, "lane")) {
@@ -1289,8 +1362,8 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     LDDL_HIP(hipGetLastError());
     return 0;
   }
-  if (path && strcmp(path, "wave") && strcmp(path, "fused"))
-    LDDL_FAIL(-1, "LDDL_TOKENIZE_PATH must be lane, wave or fused (got %s)", path);
+  if (path && strcmp(path, "wave") && strcmp(path, "fused") && strcmp(path, "plain"))
+    LDDL_FAIL(-1, "LDDL_TOKENIZE_PATH must be lane, wave, fused or plain (got %s)", path);
   // fallback list: [0] = count, then sentence indices
   constexpr int kFbHead = 1;
   DevArena::Block fbb;
@@ -1313,28 +1386,74 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
                        reinterpret_cast<uint32_t*>(fb));
   } else {
     const int wpb = kBW;  // waves per workgroup
-    LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_batch_kernel, 64 * wpb, 0));
-    // each wave streams >= ~16 sentences so its unit queue stays full across sentences
-    const int64_t want = (n_sent + 16 * wpb - 1) / (16 * wpb);
-    int64_t grid = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1)));
-    // tests: a smaller grid makes small inputs take the dynamic chunk claims
-    if (const char* g = getenv("LDDL_TOKENIZE_GRID")) grid = std::max<int64_t>(1, std::min<int64_t>(grid, atoll(g)));
+    LDDL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_batch_kernel<kMemoOff>, 64 * wpb, 0));
 #ifdef LDDL_STAMPS
+    const int64_t grid_max = (int64_t)n_cu * std::max(per_cu, 1);
     unsigned long long* tl = nullptr;
     unsigned long long* rg = nullptr;
-    LDDL_HIP(hipMalloc(&tl, 16 * grid * wpb));
-    LDDL_HIP(hipMemsetAsync(tl, 0, 16 * grid * wpb, st));
+    LDDL_HIP(hipMalloc(&tl, 16 * grid_max * wpb));
+    LDDL_HIP(hipMemsetAsync(tl, 0, 16 * grid_max * wpb, st));
     LDDL_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tok_tl), &tl, sizeof(tl), 0, hipMemcpyHostToDevice, st));
     LDDL_HIP(hipMalloc(&rg, 8 * (kTokRegions + 10)));
     LDDL_HIP(hipMemsetAsync(rg, 0, 8 * (kTokRegions + 10), st));
     LDDL_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tok_reg), &rg, sizeof(rg), 0, hipMemcpyHostToDevice, st));
 #endif
-    // the first grid x wpb chunks are taken statically (chunk w by wave w)
-    const int64_t first = std::min<int64_t>(grid * wpb * kChunk, (int64_t)INT32_MAX);
-    LDDL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(chunk_ctr), (int)first, 1, st));
-    hipLaunchKernelGGL(tokenize_batch_kernel, dim3((unsigned)grid), dim3(64 * kBW), 0, st, c->tab,
-                       d_text, n_bytes, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len,
-                       fb + kFbHead, reinterpret_cast<uint32_t*>(fb), chunk_ctr);
+    int64_t grid = 0;
+    // one launch of the streaming kernel over sentences [s0, s0 + n) (the sentence offsets are
+    // absolute, so a sub-range is a pointer offset), then the lane kernel for its fallback list
+    auto pass = [&](int64_t s0, int64_t n, int memo, WordMemo M) -> int {
+      const int64_t want = (n + 16 * wpb - 1) / (16 * wpb);
+      grid = std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cu * std::max(per_cu, 1)));
+      // tests: a smaller grid makes small inputs take the dynamic chunk claims
+      if (const char* g = getenv("LDDL_TOKENIZE_GRID")) grid = std::max<int64_t>(1, std::min<int64_t>(grid, atoll(g)));
+      // the first grid x wpb chunks are taken statically (chunk w by wave w)
+      const int64_t first = std::min<int64_t>(grid * wpb * kChunk, (int64_t)INT32_MAX);
+      LDDL_HIP(hipMemsetAsync(fb, 0, sizeof(int32_t) * kFbHead, st));
+      LDDL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(chunk_ctr), (int)first, 1, st));
+      const void* kfn = memo == kMemoBuild ? (const void*)tokenize_batch_kernel<kMemoBuild>
+                      : memo == kMemoLookup ? (const void*)tokenize_batch_kernel<kMemoLookup>
+                                            : (const void*)tokenize_batch_kernel<kMemoOff>;
+      const int64_t* so = d_sent_off + s0;
+      int32_t* sl = d_sent_len + s0;
+      int32_t* fl = fb + kFbHead;
+      uint32_t* fn = reinterpret_cast<uint32_t*>(fb);
+      void* args[] = {&c->tab, (void*)&d_text, &n_bytes, (void*)&so, &n, &max_pieces, &d_ids, &sl,
+                      &fl, &fn, &chunk_ctr, &M};
+      LDDL_HIP(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(64 * kBW), args, 0, st));
+      const int64_t fgrid = std::min<int64_t>((n + kBlock - 1) / kBlock, (int64_t)n_cu * 2);
+      hipLaunchKernelGGL(tokenize_lane_kernel, dim3((unsigned)fgrid), dim3(kBlock), 0, st, c->tab,
+                         d_text, so, n, max_pieces, d_ids, sl, fl, reinterpret_cast<const uint32_t*>(fb));
+      LDDL_HIP(hipGetLastError());
+      return 0;
+    };
+    // the word memo (above): a leading sample of 1/32 of the sentences (at least kMemoMinSample)
+    // builds it, the rest reads it. Off for vocabs whose ids do not fit 16 bits, for inputs too
+    // small to repay the second launch, and with LDDL_TOKENIZE_PATH=plain.
+    constexpr int64_t kMemoMinSample = 1 << 14;
+    int64_t n_sample = std::max<int64_t>(n_sent / 32, kMemoMinSample);
+    bool memo = c->vocab_size <= 65536 && n_sent >= 4 * kMemoMinSample;
+    if (const char* e = getenv("LDDL_TOKENIZE_MEMO_SAMPLE")) {  // tests: the memo on small inputs
+      n_sample = atoll(e);
+      memo = c->vocab_size <= 65536 && n_sample > 0 && n_sample < n_sent;
+    }
+    if (path && !strcmp(path, "plain")) memo = false;
+    int rc = 0;
+    if (!memo) {
+      rc = pass(0, n_sent, kMemoOff, WordMemo{nullptr, 0});
+    } else {
+      DevArena::Block mb;
+      const size_t entries = (size_t)1 << kMemoLog2;
+      LDDL_HIP(c->arena.take(64 * entries, st, mb));
+      LDDL_HIP(hipMemsetAsync(mb.p, 0, 64 * entries, st));
+      const WordMemo M{static_cast<uint4*>(mb.p), (uint32_t)(entries - 1)};
+      rc = pass(0, n_sample, kMemoBuild, M);
+      if (!rc) rc = pass(n_sample, n_sent - n_sample, kMemoLookup, M);
+      c->arena.give(mb, st);
+    }
+    if (rc) {
+      c->arena.give(fbb, st);
+      return rc;
+    }
 #ifdef LDDL_STAMPS
     {  // wave timeline (100 MHz real-time clock)
       const int64_t nw = grid * wpb;
@@ -1382,11 +1501,13 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     }
 #endif
   }
-  const int64_t fgrid = std::min<int64_t>((n_sent + kBlock - 1) / kBlock, (int64_t)n_cu * 2);
-  hipLaunchKernelGGL(tokenize_lane_kernel, dim3((unsigned)fgrid), dim3(kBlock), 0, st, c->tab,
-                     d_text, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + kFbHead,
-                     reinterpret_cast<const uint32_t*>(fb));
-  LDDL_HIP(hipGetLastError());
+  if (path && !strcmp(path, "wave")) {  // the wave kernel's fallback list
+    const int64_t fgrid = std::min<int64_t>((n_sent + kBlock - 1) / kBlock, (int64_t)n_cu * 2);
+    hipLaunchKernelGGL(tokenize_lane_kernel, dim3((unsigned)fgrid), dim3(kBlock), 0, st, c->tab,
+                       d_text, d_sent_off, n_sent, max_pieces, d_ids, d_sent_len, fb + kFbHead,
+                       reinterpret_cast<const uint32_t*>(fb));
+    LDDL_HIP(hipGetLastError());
+  }
   c->arena.give(fbb, st);
   return 0;
 }

@@ -91,6 +91,20 @@ def _adversarial_corpus(seed=7, n=6000):
     return text, off
 
 
+def _assert_same(ids, o, e, eo, text, off):
+    """ids / offsets against the oracle's; on a difference, name the first sentence that differs
+    (its text and both piece lists)."""
+    if np.array_equal(o, eo) and np.array_equal(ids, e):
+        return
+    for k in range(len(off) - 1):
+        a, b = ids[o[k]:o[k + 1]], e[eo[k]:eo[k + 1]]
+        if not np.array_equal(a, b):
+            raise AssertionError('sentence {} of {} ({!r}): got {} expected {}'.format(
+                k, len(off) - 1, bytes(text[off[k]:off[k + 1]])[:300], a.tolist()[:60],
+                b.tolist()[:60]))
+    raise AssertionError('outputs differ')
+
+
 @pytest.mark.parametrize('case', ['uncased', 'cased'])
 def test_tokenize_adversarial_vs_oracle(case, ctxs):
     from oracle import oracle as O
@@ -104,10 +118,11 @@ def test_tokenize_adversarial_vs_oracle(case, ctxs):
         np.testing.assert_array_equal(ids, e)
 
 
-@pytest.mark.parametrize('path', ['lane', 'wave', 'fused'])
+@pytest.mark.parametrize('path', ['lane', 'wave', 'fused', 'plain'])
 def test_tokenize_paths_vs_oracle(ctxs, monkeypatch, path):
     """Every LDDL_TOKENIZE_PATH (the lane kernel alone, the unbatched wave kernel, the streaming
-    kernel by name) against the oracle, on the synthetic corpus and on the adversarial one."""
+    kernel by name and without the word memo) against the oracle, on the synthetic corpus and on
+    the adversarial one."""
     from lddl_amd import synth
     from oracle import oracle as O
     tok = O.Tokenizer(VOCAB_UNCASED, lowercase=True)
@@ -156,3 +171,29 @@ def test_tokenize_dynamic_chunks_vs_oracle(ctxs, monkeypatch, grid):
         e, eo = tok.tokenize(text, off, max_pieces=mp)
         np.testing.assert_array_equal(o, eo)
         np.testing.assert_array_equal(ids, e)
+
+
+@pytest.mark.parametrize('case', ['uncased', 'cased'])
+@pytest.mark.parametrize('sample', ['1', '64', '1000'])
+def test_tokenize_word_memo_vs_oracle(ctxs, monkeypatch, case, sample):
+    """The word memo (a sample pass stores each multi-piece word's pieces, the rest of the call
+    reads them; on by default for inputs of >= 64 K sentences): forced onto small inputs with a
+    sample of 1 / 64 / 1000 sentences (LDDL_TOKENIZE_MEMO_SAMPLE), the output is the oracle's on
+    the synthetic corpus (repeated words: memo hits), the adversarial one (non-ASCII words
+    normalised before the lookup, [UNK], > 8 pieces, dropped characters) and with the dynamic
+    chunk claims of a one-workgroup grid."""
+    from lddl_amd import synth
+    from oracle import oracle as O
+    vocab = VOCAB_UNCASED if case == 'uncased' else VOCAB_CASED
+    tok = O.Tokenizer(vocab, lowercase=case == 'uncased')
+    monkeypatch.setenv('LDDL_TOKENIZE_MEMO_SAMPLE', sample)
+    corp = synth.generate(seed=77, n_bytes=1 << 20, nonascii_frac=0.05)
+    for text, off in ((corp.text, corp.sent_off), _adversarial_corpus(seed=5, n=4000)):
+        for grid in (None, '1'):
+            if grid:
+                monkeypatch.setenv('LDDL_TOKENIZE_GRID', grid)
+            for mp in (512, 9):
+                ids, o = ctxs[case].tokenize_host(text, off, max_pieces=mp)
+                e, eo = tok.tokenize(text, off, max_pieces=mp)
+                _assert_same(ids, o, e, eo, text, off)
+            monkeypatch.delenv('LDDL_TOKENIZE_GRID', raising=False)

@@ -10,14 +10,15 @@ import sys
 
 import torch
 
-sys.path.insert(0, '.')
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
 from lddl_amd import synth  # noqa: E402
 from lddl_amd.context import Context  # noqa: E402
 
 nbytes = int(float(sys.argv[1]))
 variants = sys.argv[2:] or ['batch']
 corp = synth.generate(seed=1234, n_bytes=nbytes, nonascii_frac=0.01, threads=16)
-ctx = Context('lddl_amd/assets/vocab_synth_uncased_30522.txt')
+ctx = Context(os.path.join(REPO, 'lddl_amd', 'assets', 'vocab_synth_uncased_30522.txt'))
 text = torch.from_numpy(corp.text).cuda()
 off = torch.from_numpy(corp.sent_off).cuda()
 ref = None
