@@ -787,7 +787,8 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
 // instructions (profiles/r03l_pmc_tokenizer_variants.txt).
 // ---------------------------------------------------------------------------------------------
 //
-// Word memo (round 6). Phase B (greedy longest match of the multi-piece and non-ASCII words) is
+// Word memo (round 6; 19.27 -> 15.25 ms per 2 GB, profiles/r06l_*, r06m_*). Phase B (greedy
+// longest match of the multi-piece and non-ASCII words) is
 // ~half of the kernel's wave cycles, and its words repeat: in the synthetic corpus 26 % of the
 // pre-tokenizer units are multi-piece, and 95 % of those occurrences are words already seen in
 // the first 3 % of the text (Zipf). lddl_tokenize therefore runs the kernel twice per call: over
@@ -800,7 +801,11 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
 // alone, so the output is the same with or without the memo (tests run both).
 // ---------------------------------------------------------------------------------------------
 enum : int { kMemoOff = 0, kMemoBuild = 1, kMemoLookup = 2 };
-constexpr int kMemoLog2 = 21;  // 2 M entries x 64 B = 128 MiB
+// 4 M entries x 64 B = 256 MiB (2 M: 15.49 ms per 2 GB, 1 M: 15.83, 4 M: 15.25 — fewer words
+// lose their slot to another; profiles/r06m_tok_memo_tuning.txt)
+constexpr int kMemoLog2 = 22;
+// the sample: 1/32 of the sentences (1/8: 16.06 ms per 2 GB, 1/16: 15.68, 1/64: 15.83)
+constexpr int kMemoDiv = 32;
 struct WordMemo {
   uint4* tab;  // entry e: tab[4e], tab[4e+1] key bytes 0..31 (zero past nb), tab[4e+2] pieces
                // (8 x uint16), tab[4e+3].x meta: kMemoReady | nb | npc << 8 (0: empty)
@@ -1430,7 +1435,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, void* stream, const uint8_t* d_text, i
     // builds it, the rest reads it. Off for vocabs whose ids do not fit 16 bits, for inputs too
     // small to repay the second launch, and with LDDL_TOKENIZE_PATH=plain.
     constexpr int64_t kMemoMinSample = 1 << 14;
-    int64_t n_sample = std::max<int64_t>(n_sent / 32, kMemoMinSample);
+    int64_t n_sample = std::max<int64_t>(n_sent / kMemoDiv, kMemoMinSample);
     bool memo = c->vocab_size <= 65536 && n_sent >= 4 * kMemoMinSample;
     if (const char* e = getenv("LDDL_TOKENIZE_MEMO_SAMPLE")) {  // tests: the memo on small inputs
       n_sample = atoll(e);
