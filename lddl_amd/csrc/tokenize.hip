@@ -1062,7 +1062,19 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
               W.q_npc[u] = 1;
             }
             const uint64_t H = ballot(hardr[r]);
-            if (hardr[r]) W.h_idx[nh + (int)popc_below(H)] = (HIdx)u;
+            if (hardr[r]) {
+              const int k = nh + (int)popc_below(H);
+              W.h_idx[k] = (HIdx)u;
+              // a probed word that missed: its (lowercased) bytes go to phase-B row k, so the
+              // first phase-B pass reads them from LDS instead of loading the text again
+              if (elig[r] && k < 64) {
+                uint4* row = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(W.pcs) + 32 * k);
+                row[0] = make_uint4((uint32_t)vv[r].w0, (uint32_t)(vv[r].w0 >> 32), (uint32_t)vv[r].w1,
+                                    (uint32_t)(vv[r].w1 >> 32));
+                row[1] = make_uint4((uint32_t)vv[r].w2, (uint32_t)(vv[r].w2 >> 32), (uint32_t)vv[r].w3,
+                                    (uint32_t)(vv[r].w3 >> 32));
+              }
+            }
             nh += __popcll(H);
           }
         }
@@ -1091,8 +1103,18 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
             const int len = W.q_e[u] - st + 1;
             const bool slow = qs < 0;
             known_miss = !slow && T.ascii_mode != 0 && len <= T.max_piece_bytes && len <= 32;
-            uw = unit_word(T, s_ascii, text, n_bytes, A + st, len, slow,
-                           reinterpret_cast<uint8_t*>(W.pcs) + 32 * lane);
+            if (h0 == 0 && known_miss) {  // phase A left the word in this lane's row
+              const uint4* row = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(W.pcs) + 32 * lane);
+              const uint4 r0 = row[0], r1 = row[1];
+              uw.v = B32{r0.x | (uint64_t)r0.y << 32, r0.z | (uint64_t)r0.w << 32,
+                         r1.x | (uint64_t)r1.y << 32, r1.z | (uint64_t)r1.w << 32};
+              uw.nb = len;
+              uw.ends = ~0ull;
+              uw.status = 0;
+            } else {
+              uw = unit_word(T, s_ascii, text, n_bytes, A + st, len, slow,
+                             reinterpret_cast<uint8_t*>(W.pcs) + 32 * lane);
+            }
           }
           wave_sync();  // every normalised word is in registers: the rows become piece columns
           int npc = 0;
