@@ -217,11 +217,18 @@ def load_pmc(batch_sizes):
 
 
 def pmc_entry(kernels, kernel):
-    """A kernel's counters by name; template instantiations (`name<...>`) match their base name."""
+    """A kernel's counters per step by name: template instantiations (`name<...>`) match their base
+    name and are summed (the tokenizer runs as a memo-building and a memo-reading launch per
+    call, tokenize_batch_kernel<1> and <2>)."""
+    out = {}
     for k, v in kernels.items():
         if k == kernel or k.startswith(kernel + '<'):
-            return v
-    return {}
+            for n, x in v.items():
+                if isinstance(x, (int, float)) and not isinstance(x, bool):
+                    out[n] = out.get(n, 0) + x
+                else:
+                    out.setdefault(n, x)
+    return out
 
 
 def cgroup_cpu_stat():
@@ -993,7 +1000,9 @@ def main():
         alt = {'rng': other, 'value': atok / adt, 'ms_per_step': adt / args.steps * 1e3,
                'plan_ms': float(np.mean([x['plan_ms'] for x in astats]))}
     seg = None
-    if args.segmented_line and world == 1:  # the same path from raw document text: Punkt first
+    # the same path from raw document text: Punkt first (one step over the whole batch, so not
+    # for C4, whose 25 GB per GPU only fit as sub-batches)
+    if args.segmented_line and world == 1 and args.workload != 'c4':
         torch.cuda.empty_cache()
         seg = timed_segmented(args, rank, world, ctx, dev)
         if args.punkt_params:  # the trained-model kernel on the same documents
