@@ -611,19 +611,33 @@ __device__ inline void densify_group(int64_t k0, const int64_t* __restrict__ ks_
   const int64_t base = kscan[k0];
   // the sentence loop indices are wave-uniform: lane values via readlane, not LDS permutes
   auto rl = [](int32_t v, int i) { return __builtin_amdgcn_readlane(v, i); };
+  // kU chunks of 64 tokens per round: their sources first, then all kU loads, then the stores,
+  // so a wave has kU loads in flight instead of one dependent load -> store per chunk
+  constexpr int kU = 4;
   int j = 0;
-  for (int32_t c0 = 0; c0 < total; c0 += 64) {
-    const int32_t x = c0 + lane, hi = min(c0 + 63, total - 1);
-    while (rl(incl, j) <= c0) ++j;  // first sentence overlapping the chunk
-    int64_t src = 0;
-    for (int jj = j;; ++jj) {
-      const int32_t e = rl(incl, jj);
-      const int32_t b = e - rl(len, jj);
-      const int64_t s = ((int64_t)rl((int32_t)(st >> 32), jj) << 32) | (uint32_t)rl((int32_t)st, jj);
-      if (x >= b && x < e) src = s + (x - b);
-      if (e > hi) break;
+  for (int32_t c0 = 0; c0 < total; c0 += 64 * kU) {
+    int64_t src[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int32_t cu = c0 + 64 * u, x = cu + lane, hi = min(cu + 63, total - 1);
+      src[u] = 0;
+      if (cu < total) {
+        while (rl(incl, j) <= cu) ++j;  // first sentence overlapping the chunk
+        for (int jj = j;; ++jj) {
+          const int32_t e = rl(incl, jj);
+          const int32_t b = e - rl(len, jj);
+          const int64_t s = ((int64_t)rl((int32_t)(st >> 32), jj) << 32) | (uint32_t)rl((int32_t)st, jj);
+          if (x >= b && x < e) src[u] = s + (x - b);
+          if (e > hi) break;
+        }
+      }
     }
-    if (x < total) dense.st(base + x, ids[src]);
+    int32_t v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) v[u] = c0 + 64 * u + lane < total ? ids[src[u]] : 0;
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (c0 + 64 * u + lane < total) dense.st(base + c0 + 64 * u + lane, v[u]);
   }
 }
 
@@ -2159,11 +2173,17 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather16_kernel(GatherArgs G,
       const uint32_t inc = seg_scan<LP>(c, lane, &tot);
       int32_t rr = (int32_t)(inc - c);
 #pragma unroll
-      for (int e = 0; e < NT; ++e) {  // branch-free: an unmasked element writes the lane's trash entry
+      for (int e = 0; e < NT; ++e) {
+        // only masked elements write their staging entries (exec-masked stores). Writing every
+        // element, the unmasked ones to a per-lane trash entry, was 70 % of the kernel's LDS bank
+        // conflicts (two lanes per dword, four pairs per wave on the same banks) at the same time
+        // per launch (profiles/r06w_gather_lds_attribution.txt)
         const bool m = (mk >> e) & 1u;
-        const int32_t xe = x + e, at = m ? rr : kStageRows + ql;
-        spos[at] = (uint16_t)(xe < na ? xe + 1 : xe + 2);
-        slab[at] = v[e >> 3][e & 7];
+        const int32_t xe = x + e;
+        if (m) {
+          spos[rr] = (uint16_t)(xe < na ? xe + 1 : xe + 2);
+          slab[rr] = v[e >> 3][e & 7];
+        }
         v[e >> 3][e & 7] = m && dd[e] != kKeep16 ? (uint16_t)dd[e] : v[e >> 3][e & 7];
         rr += m ? 1 : 0;
       }
