@@ -613,7 +613,7 @@ __device__ inline void densify_group(int64_t k0, const int64_t* __restrict__ ks_
   auto rl = [](int32_t v, int i) { return __builtin_amdgcn_readlane(v, i); };
   // kU chunks of 64 tokens per round: their sources first, then all kU loads, then the stores,
   // so a wave has kU loads in flight instead of one dependent load -> store per chunk
-  constexpr int kU = 4;
+  constexpr int kU = 4;  // (8: 6.0 -> 6.3 ms, profiles/r06y)
   int j = 0;
   for (int32_t c0 = 0; c0 < total; c0 += 64 * kU) {
     int64_t src[kU];
