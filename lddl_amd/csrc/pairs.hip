@@ -276,29 +276,42 @@ struct WaveRng {
       int32_t R = (lane * 77) >> 8;
       uint32_t x;
       uint64_t rej;
+      // Convergence is tested on the rejection masks (one scalar 64-bit compare): from the second
+      // pass on, R = popc_below(previous mask), so equal masks give equal R in every lane (bit 63
+      // moves no R: at most one extra pass). The loop carries no vector compare and no R copy.
       if (s0 >= 64) {  // every word of the window has a step (u >= 2)
-        while (true) {
+        auto pass = [&]() {
           const int32_t u = u1 + R;
           x = w >> __clz((uint32_t)u);
-          rej = ballot(x >= (uint32_t)u);
-          const int32_t R2 = (int32_t)popc_below(rej);
 #ifdef LDDL_STAMPS
           ++n_pass;
 #endif
-          if (ballot(R2 != R) == 0) break;
-          R = R2;
+          return ballot(x >= (uint32_t)u);
+        };
+        uint64_t prev = pass();
+        R = (int32_t)popc_below(prev);
+        rej = pass();
+        while (rej != prev) {
+          prev = rej;
+          R = (int32_t)popc_below(rej);
+          rej = pass();
         }
       } else {  // words past the last step (u <= 1) are held "accepted", so they settle at once
-        while (true) {
+        auto pass = [&]() {
           const int32_t u = u1 + R;
           x = w >> (__clz((uint32_t)u) & 31);
-          rej = ballot(x >= (uint32_t)u) & ballot(u > 1);
-          const int32_t R2 = (int32_t)popc_below(rej);
 #ifdef LDDL_STAMPS
           ++n_pass;
 #endif
-          if (ballot(R2 != R) == 0) break;
-          R = R2;
+          return ballot(x >= (uint32_t)u) & ballot(u > 1);
+        };
+        uint64_t prev = pass();
+        R = (int32_t)popc_below(prev);
+        rej = pass();
+        while (rej != prev) {
+          prev = rej;
+          R = (int32_t)popc_below(rej);
+          rej = pass();
         }
       }
 #ifdef LDDL_STAMPS
@@ -530,6 +543,21 @@ struct LenWin {
   int32_t win, pre;
   uint64_t fl;  // lanes whose sentence holds a literal [CLS]/[SEP]
   __device__ void reset(const int32_t* p, int nn) { len = p; n = nn; wbase = -1024; }
+  // the first window of a document loaded ahead (issued one document early, so the chain does not
+  // wait for it), then taken as the window at sentence 0
+  int32_t pfw;
+  __device__ void prefetch(const int32_t* p, int nn) {
+    const int k = (int)threadIdx.x;
+    pfw = k < nn ? p[k] : 0;
+  }
+  __device__ void reset_prefetched(const int32_t* p, int nn) {
+    len = p;
+    n = nn;
+    wbase = 0;
+    win = pfw;
+    pre = wave_incl_scan(win & kLenMask);
+    fl = ballot((win & kLenHasClsSep) != 0);
+  }
   __device__ bool has(int j) const { return (unsigned)(j - wbase) < 64u; }  // (j >= 0)
   __device__ void load(int j) {
     wbase = j;
@@ -705,6 +733,7 @@ __global__ void __launch_bounds__(64, 6) plan_replay_kernel(PlanArgs A) {
   // the priority steps at the document counts where progress crosses a quarter (no 64-bit
   // division per document)
   int32_t prio_next = 0, prio_done = 0;
+  if (nd > 0) La.prefetch(ks_len_p + doc_loc(0), doc_loc(1) - doc_loc(0));
   for (int dp = 0; dp < A.dup; ++dp) {
     for (int32_t di = 0; di < nd; ++di) {
       if (prio_done >= prio_next) {
@@ -720,7 +749,14 @@ __global__ void __launch_bounds__(64, 6) plan_replay_kernel(PlanArgs A) {
       const int32_t ls0 = doc_loc(di);
       const int64_t s0 = kbase + ls0;
       const int ns = doc_loc(di + 1) - ls0;
-      La.reset(ks_len_p + ls0, ns);
+      // (the document's first length window was loaded one document ago; 1.5 ms per 10 GB,
+      // profiles/r06p2_planner_loop_ab.txt)
+      La.reset_prefetched(ks_len_p + ls0, ns);
+      {
+        const int32_t dn = di + 1 < nd ? di + 1 : 0;  // the next document (of this or the next pass)
+        const int32_t nl0 = doc_loc(dn);
+        La.prefetch(ks_len_p + nl0, doc_loc(dn + 1) - nl0);
+      }
       int32_t target = max_num;
       if (rng.rand53() < A.k_short) target = rng.randint32(2, max_num);
       // chunks: sentences are accumulated until the target length or the document end
