@@ -1185,10 +1185,11 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
       uint64_t UNITp = 0, CONTp = 0;  // the bank before
       uint64_t cin = 0;               // the byte before the bank is a word-run byte
       // slow-path carries into the next bank: code-point coverage of its first lanes (bit k: lane
-      // k continues a lead of the bank before, for leads of 2 / 3 / 4 bytes), special-token bytes,
-      // and the (class | cplen << 4) of the bank's lanes 61..63
-      uint64_t k1 = 0, k2 = 0, k3 = 0, insc = 0;
-      int32_t plc61 = 0, plc62 = 0, plc63 = 0;
+      // k continues a lead of the bank before, for leads of 2 / 3 / 4 bytes; <= 3 bits each) and
+      // special-token bytes (<= 5 bits), packed k1 | k2 << 8 | k3 << 16 | insc << 24 so that the
+      // plain-bank test reads one scalar (as four 64-bit masks they were spilled and reloaded
+      // every bank); and the (class | cplen << 4) of the bank's lanes 61..63, one byte each
+      uint32_t cpack = 0, plcp = 0;
       int32_t jn = 1;  // the next sentence start to mark
       uint32_t nextS = (uint32_t)__builtin_amdgcn_readfirstlane(W.s_off[1]);
       const uint32_t last = span ? span - 1 : 0;
@@ -1225,11 +1226,13 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
         uint64_t RUN, UNIT, CONT, SL = 0;
         // unit start: chunk-relative byte | kind << 28
         int32_t sval = (int32_t)x;
-        if (!(ballot(v >= kFSlow) | insc | k1 | k2 | k3)) {  // plain ASCII bank
+        if (!(ballot(v >= kFSlow) | (uint64_t)cpack)) {  // plain ASCII bank
           RUN = ballot(v == kFRun) & VALID;
           UNIT = VALID & ~ballot(v == kFSep);
           CONT = RUN & ((RUN << 1) | cin) & ~BRK;
         } else {
+          const uint64_t k1 = cpack & 0xFFu, k2 = (cpack >> 8) & 0xFFu, k3 = (cpack >> 16) & 0xFFu,
+                         insc = cpack >> 24;
           // this lane's sentence end: the next break above the lane, else the first sentence start
           // after the bank
           const uint64_t above = BRK & ~upto;
@@ -1264,7 +1267,8 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
             const bool covered = cont && (((C1 | C2 | C3) >> lane) & 1ull);
             const int dist = !covered ? 0 : ((C1 >> lane) & 1ull) ? 1 : ((C2 >> lane) & 1ull) ? 2 : 3;
             int lead = __shfl(val, lane - dist, 64);
-            if (lane < dist) lead = lane - dist == -1 ? plc63 : lane - dist == -2 ? plc62 : plc61;
+            if (lane < dist)
+              lead = (int)((plcp >> (lane - dist == -1 ? 16 : lane - dist == -2 ? 8 : 0)) & 0xFFu);
             if (covered) {  // a covered continuation takes its lead's class
               cls = (uint32_t)lead & 3u;
               cplen = 0;
@@ -1280,13 +1284,11 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
           CONT = (RUN & ((RUN << 1) | cin) & ~BRK) | (ISO & ~LEAD) | inside;
           sval = (int32_t)(x | ((uint32_t)(spk >= 0 ? 2 + spk : 0) << 28));
           SL = ballot(slow && cat != kCatSep);
-          k1 = (V2 | V3 | V4) >> 63;
-          k2 = (V3 | V4) >> 62;
-          k3 = V4 >> 61;
-          insc = (S >> 63) | (S >> 62) | (S >> 61) | (S >> 60) | (S6 >> 59);
-          plc61 = __builtin_amdgcn_readlane(val, 61);
-          plc62 = __builtin_amdgcn_readlane(val, 62);
-          plc63 = __builtin_amdgcn_readlane(val, 63);
+          cpack = (uint32_t)((V2 | V3 | V4) >> 63) | (uint32_t)((V3 | V4) >> 62) << 8 |
+                  (uint32_t)(V4 >> 61) << 16 |
+                  (uint32_t)((S >> 63) | (S >> 62) | (S >> 61) | (S >> 60) | (S6 >> 59)) << 24;
+          plcp = (uint32_t)__builtin_amdgcn_readlane(val, 61) | (uint32_t)__builtin_amdgcn_readlane(val, 62) << 8 |
+                 (uint32_t)__builtin_amdgcn_readlane(val, 63) << 16;
         }
         // starts of this bank (lanes without one store to their trash slot)
         const uint64_t US = UNIT & ~CONT;
