@@ -921,7 +921,9 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
   int32_t c0;
   {
     const int64_t w = (int64_t)blockIdx.x * kBW + (threadIdx.x >> 6);
-    c0 = w * kChunk < n_sent32 ? (int32_t)(w * kChunk) : n_sent32;
+    // (readfirstlane: the compiler cannot see that threadIdx.x >> 6 is wave-uniform, and a
+    // divergent c0 made the chunk's span, sentence count and every loop over them exec-masked)
+    c0 = __builtin_amdgcn_readfirstlane(w * kChunk < n_sent32 ? (int32_t)(w * kChunk) : n_sent32);
   }
   const uint64_t upto = (2ull << lane) - 1;  // lanes <= this one (lane 63: all)
 
