@@ -136,7 +136,7 @@ constexpr int kEncWaves = 4;
 // phases so that every output element is written exactly once, coalesced.
 __global__ void __launch_bounds__(64 * kEncWaves) encode_kernel(EncodeArgs E) {
   extern __shared__ __attribute__((aligned(16))) int32_t srow[];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = wave_id(), lane = threadIdx.x & 63;
   const int b = blockIdx.x * kEncWaves + w;
   const bool active = b < E.B;
   int32_t* sid = srow + (size_t)w * 2 * E.L;

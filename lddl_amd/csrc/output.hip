@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(256) render_lengths_kernel(RenderArgs R, int64
                                                              int64_t* n_pos, const uint8_t* is_rn,
                                                              uint16_t* num_tokens_out,
                                                              uint8_t* is_rn_out) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave_id();
   if (row >= R.n_rows) return;
   const int64_t q = R.rows ? R.rows[row] : row;
   const int64_t t0 = R.tok_off[q], t1 = R.tok_off[q + 1];
@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(256) render_write_kernel(RenderArgs R, const i
                                                            const int64_t* npy_off, uint8_t* a_bytes,
                                                            uint8_t* b_bytes, uint8_t* l_bytes,
                                                            uint8_t* npy_bytes) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave_id();
   if (row >= R.n_rows) return;
   const int64_t q = R.rows ? R.rows[row] : row;
   const int64_t t0 = R.tok_off[q], t1 = R.tok_off[q + 1];
@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(256) gather_ragged_kernel(Src2<T> src, Src2<in
                                                             int64_t n_rows,
                                                             const int64_t* __restrict__ dst_off,
                                                             T* __restrict__ dst) {
-  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t i = (int64_t)blockIdx.x * 4 + wave_id();
   if (i >= n_rows) return;
   const int64_t r = rows ? rows[i] : i;
   const int64_t* o2 = off.at(r);

@@ -635,7 +635,7 @@ __device__ inline void densify_group(int64_t k0, const int64_t* __restrict__ ks_
   const int32_t len = ok ? ks_len[k] & kLenMask : 0;
   const int64_t st = ok ? ks_start[k] : 0;
   const int32_t incl = wave_incl_scan(len);
-  const int32_t total = __shfl(incl, 63, 64);
+  const int32_t total = __builtin_amdgcn_readlane(incl, 63);  // (uniform: scalar loop bounds)
   const int64_t base = kscan[k0];
   // the sentence loop indices are wave-uniform: lane values via readlane, not LDS permutes
   auto rl = [](int32_t v, int i) { return __builtin_amdgcn_readlane(v, i); };
@@ -1260,7 +1260,7 @@ constexpr uint32_t kNat80 = 3435973837u, kNat90 = 3865470567u;
 // separate streams), so a pair's masks do not depend on the pairs that share its wave.
 __global__ void __launch_bounds__(256) mask_native_kernel(NativeArgs A, int32_t stage_cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_mn[];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int w = wave_id(), lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const int64_t q0 = ((int64_t)blockIdx.x * nw + w) * 64;
   if (q0 >= A.n_pairs) return;
   uint32_t* bm = reinterpret_cast<uint32_t*>(s_mn) + (size_t)w * A.words * 64 + lane;
@@ -1598,7 +1598,7 @@ __global__ void __launch_bounds__(256) densify_kernel(const int64_t* __restrict_
                                                       const int64_t* __restrict__ kscan, int64_t n,
                                                       const int32_t* __restrict__ ids,
                                                       IdPtr dense) {
-  const int64_t k0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  const int64_t k0 = ((int64_t)blockIdx.x * 4 + wave_id()) * 64;
   if (k0 >= n) return;
   densify_group(k0, ks_start, ks_len, kscan, n, ids, dense);
 }
@@ -1931,7 +1931,7 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather_kernel(GatherArgs G, G
   using tok4_t = typename Tok4<IdT>::type;
   const IdT* __restrict__ dense = static_cast<const IdT*>(G.dense);
   extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, sl = lane & 31;
+  const int w = wave_id(), lane = threadIdx.x & 63, h = lane >> 5, sl = lane & 31;
   // XCD-contiguous blocks: the pairs of one partition (which read its dense tokens dup times over)
   // and their mask pool lines meet in one L2
   const int64_t wg = xcd_block((int64_t)blockIdx.y * gridDim.x + blockIdx.x, (int64_t)gridDim.x * gridDim.y);
@@ -2133,7 +2133,7 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) gather16_kernel(GatherArgs G,
   uint16_t* __restrict__ out_tok = static_cast<uint16_t*>(G.out_tok);
   uint16_t* __restrict__ out_lab = static_cast<uint16_t*>(G.out_lab);
   extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, qw = lane / LP, ql = lane % LP;
+  const int w = wave_id(), lane = threadIdx.x & 63, qw = lane / LP, ql = lane % LP;
   // XCD-contiguous blocks (see gather_kernel)
   const int64_t wg = xcd_block((int64_t)blockIdx.y * gridDim.x + blockIdx.x, (int64_t)gridDim.x * gridDim.y);
   const int64_t q = (wg * kGWaves + w) * PW + qw;

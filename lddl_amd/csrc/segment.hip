@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_pe
     int64_t n_doc, int32_t* __restrict__ cand, int32_t* __restrict__ ccnt, int32_t* __restrict__ rs_rel,
     int32_t* __restrict__ cnt) {
   __shared__ uint4 slab_all[kSegWaves][kSlab / 16];
-  const int64_t d = (int64_t)blockIdx.x * kSegWaves + (threadIdx.x >> 6);
+  const int64_t d = (int64_t)blockIdx.x * kSegWaves + wave_id();
   if (d >= n_doc) return;  // wave-uniform
   const int lane = lane_id();
   uint4* slab = slab_all[threadIdx.x >> 6];
@@ -586,7 +586,7 @@ struct CntAt {
 __global__ void segment_flatten_kernel(const int64_t* __restrict__ doc_off, int64_t n_doc,
                                        const int32_t* __restrict__ cand, const int64_t* __restrict__ coff,
                                        int64_t* __restrict__ fq, int32_t* __restrict__ fdoc) {
-  const int64_t d = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t d = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_id();
   if (d >= n_doc) return;
   const int64_t b0 = doc_off[d];
   const int32_t* in = cand + ((b0 - doc_off[0]) >> 1) + d;
@@ -647,7 +647,7 @@ __global__ void __launch_bounds__(kEvalBlock) segment_eval_kernel(
 __global__ void segment_fill_kernel(const int64_t* __restrict__ doc_off, int64_t n_doc,
                                     const int64_t* __restrict__ coff, const int64_t* __restrict__ fbound,
                                     const int64_t* __restrict__ dso, int64_t* __restrict__ sent_off) {
-  const int64_t d = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t d = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_id();
   if (d >= n_doc) return;
   const int lane = lane_id();
   const int64_t o = dso[d];

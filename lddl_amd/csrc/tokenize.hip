@@ -718,7 +718,7 @@ __global__ void __launch_bounds__(64 * kTW) tokenize_wave_kernel(
   const int lane = lane_id();
   WaveLds& W = s_w[threadIdx.x >> 6];
   const int64_t stride = (int64_t)gridDim.x * kTW;
-  for (int64_t s = (int64_t)blockIdx.x * kTW + (threadIdx.x >> 6); s < n_sent; s += stride) {
+  for (int64_t s = (int64_t)blockIdx.x * kTW + wave_id(); s < n_sent; s += stride) {
     const int64_t b0 = sent_off[s], b1 = sent_off[s + 1];
     int64_t pos = b0;
     int32_t emitted = 0, flags = 0;
