@@ -879,7 +879,7 @@ constexpr int kTokRegions = 6;  // 0 banks, 1 phase A, 2 phase B, 3 place, 4 que
 
 template <int kMemo>  // kMemoOff / kMemoBuild / kMemoLookup (word memo above)
 __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
-    Tables T, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
+    Tables T_arg, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
     int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
     int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr,
     WordMemo M) {
@@ -887,6 +887,12 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
   __shared__ uint8_t s_cls[256];
   __shared__ uint32_t s_bloom[kBloomWords];
   __shared__ StreamLds s_w[kBW];
+  // the tables' pointers and scalars live in LDS, read where used: as kernel arguments they held
+  // ~26 SGPRs for the kernel's whole life and pushed the bank loop's own scalars into spills
+  __shared__ Tables s_T;
+  if (threadIdx.x == 0) s_T = T_arg;
+  __syncthreads();
+  const Tables& T = s_T;
 #ifdef LDDL_STAMPS
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long reg_acc[kTokRegions] = {0, 0, 0, 0, 0, 0};
