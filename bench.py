@@ -1013,7 +1013,11 @@ def main():
     exch = None
     if world > 1 and args.workload == 'c2' and args.exchange_line:
         torch.cuda.empty_cache()
-        exch = c4_exchange(args, ctx, dev, corp, part, seeds, text, world)
+        try:  # (after the timed region: a failure here must not cost the headline line)
+            exch = c4_exchange(args, ctx, dev, corp, part, seeds, text, world)
+        except Exception as e:  # noqa: BLE001
+            exch = {'error': '{}: {}'.format(type(e).__name__, e)[:500]}
+            print('c4_exchange failed on rank {}: {}'.format(rank, exch['error']), file=sys.stderr)
     mem = torch.cuda.memory_stats()
     if rank != 0:
         dist.destroy_process_group()
