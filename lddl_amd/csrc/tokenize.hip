@@ -880,8 +880,8 @@ constexpr int kTokRegions = 6;  // 0 banks, 1 phase A, 2 phase B, 3 place, 4 que
 template <int kMemo>  // kMemoOff / kMemoBuild / kMemoLookup (word memo above)
 __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
     Tables T_arg, const uint8_t* __restrict__ text, int64_t n_bytes, const int64_t* __restrict__ sent_off,
-    int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len,
-    int32_t* __restrict__ fb_list, uint32_t* __restrict__ fb_n, int32_t* __restrict__ chunk_ctr,
+    int64_t n_sent, int32_t max_pieces, int32_t* __restrict__ ids, int32_t* __restrict__ sent_len_arg,
+    int32_t* __restrict__ fb_list_arg, uint32_t* __restrict__ fb_n_arg, int32_t* __restrict__ chunk_ctr_arg,
     WordMemo M) {
   __shared__ uint32_t s_ascii[128];
   __shared__ uint8_t s_cls[256];
@@ -890,9 +890,18 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
   // the tables' pointers and scalars live in LDS, read where used: as kernel arguments they held
   // ~26 SGPRs for the kernel's whole life and pushed the bank loop's own scalars into spills
   __shared__ Tables s_T;
-  if (threadIdx.x == 0) s_T = T_arg;
+  // (and the per-chunk / rare output pointers, for the same reason)
+  __shared__ int32_t* s_cold[4];
+  if (threadIdx.x == 0) {
+    s_T = T_arg;
+    s_cold[0] = sent_len_arg;
+    s_cold[1] = fb_list_arg;
+    s_cold[2] = reinterpret_cast<int32_t*>(fb_n_arg);
+    s_cold[3] = chunk_ctr_arg;
+  }
   __syncthreads();
   const Tables& T = s_T;
+  int32_t* const volatile* cold = s_cold;  // read where used (not hoisted into registers)
 #ifdef LDDL_STAMPS
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long reg_acc[kTokRegions] = {0, 0, 0, 0, 0, 0};
@@ -938,7 +947,8 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
     const int64_t A = sent_off[c0];
     const int64_t span64 = sent_off[c0 + n] - A;
     if (span64 >= kMaxSpan) {  // pathological chunk (>= 256 MiB of text): the lane kernel
-      for (int j = lane; j < n; j += 64) fb_list[atomicAdd(fb_n, 1u)] = c0 + j;
+      for (int j = lane; j < n; j += 64)
+        cold[1][atomicAdd(reinterpret_cast<uint32_t*>(cold[2]), 1u)] = c0 + j;
     } else {
       for (int j = lane; j <= n; j += 64) W.s_off[j] = (int32_t)(sent_off[c0 + j] - A);
       for (int j = lane; j < n; j += 64) W.r_cnt[j] = 0;
@@ -1343,17 +1353,17 @@ __global__ void __launch_bounds__(64 * kBW, 1) tokenize_batch_kernel(
       for (int j = lane; j < n; j += 64) {
         const int32_t rc = W.r_cnt[j];
         if (rc & kRFb) {
-          fb_list[atomicAdd(fb_n, 1u)] = c0 + j;
+          cold[1][atomicAdd(reinterpret_cast<uint32_t*>(cold[2]), 1u)] = c0 + j;
         } else {
           const int32_t cnt = rc & kRCnt;
-          sent_len[c0 + j] = (cnt < max_pieces ? cnt : max_pieces) | (rc & kLenHasClsSep);
+          cold[0][c0 + j] = (cnt < max_pieces ? cnt : max_pieces) | (rc & kLenHasClsSep);
         }
       }
       wave_sync();  // before the next chunk reuses s_off / r_cnt
     }
     TOK_STAMP(5);
     int32_t nc = 0;
-    if (lane == 0) nc = atomicAdd(chunk_ctr, kChunk);
+    if (lane == 0) nc = atomicAdd(cold[3], kChunk);
     nc = __builtin_amdgcn_readfirstlane(nc);
     c0 = nc < n_sent32 ? nc : n_sent32;
   }
